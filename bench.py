@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Headline benchmark: individuals x frames / s of 3D pose (8-view ViTPose-H + triangulate).
+
+Workload (BASELINE.json configs[1]), per GPU per step:
+one synchronized frame = 8 views (uint8 BGR 1536x2048) x 4 individuals
+-> 32 top-down crops (UDP warp, bf16 ViTPose-H 256x192, flip test = 64 forwards)
+-> UDP/DARK decode -> score-threshold -> omnidir undistort + DLT of 4 x 17 joints.
+Everything in the step runs on the GPU from inputs already resident in HBM.
+
+Multi-GPU (torch.distributed over RCCL, one process per GPU): frames are sharded
+across ranks (weak scaling, per-GPU work fixed).  Per-frame triangulation needs
+only that frame's 8 views, so the step has no collective; the one real exchange,
+the all-gather of every rank's per-view 2D keypoints that feeds the clip-level
+Viterbi / optim_points stage, runs once inside the timed region.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "macaque-3d-pose-estimation_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "individuals×frames/sec 3D pose (8-view ViTPose-h + triangulate), 1/2/4/8 GPU"
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+N_VIEWS, N_ANIMALS, N_JOINTS = 8, 4, 17
+IMG_H, IMG_W = 1536, 2048
+KP_THR, TRI_THR = 0.30, 0.5   # step1_proc2d.py:68 (KP_THR), config_tmpl.toml:96 (score_threshold)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames-per-step", type=int, default=1)
+    ap.add_argument("--model", default="huge", choices=["huge", "base", "tiny"])
+    ap.add_argument("--resident-frames", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="replay the forward as a hipGraph (disables live timing)")
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, cams_np, n_crops_sample=2):
+    """Oracle (CPU restatement) timed on this host: ViT fp32 flip + decode for a sample of
+    the frame's crops, extrapolated to the frame's 32 crops, + the frame's DLT."""
+    import numpy as np
+    import torch
+    from mqhip import synth
+    from mqhip.weights import make_random_weights
+    from oracle.decode import decode_batch
+    from oracle.geometry import CameraGroupOracle
+    from oracle.vitpose import forward_flip_test
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    w = make_random_weights(cfg, seed=0, device="cpu")
+    x = torch.randn((n_crops_sample, 3, 256, 192))
+    with torch.no_grad():
+        forward_flip_test(x[:1], w, cfg)  # warm-up
+        t0 = time.perf_counter()
+        hm, _, _ = forward_flip_test(x, w, cfg)
+        t_vit = time.perf_counter() - t0
+    hm = hm.numpy()
+    c = np.tile(np.array([[800, 600]], np.float32), (n_crops_sample, 1))
+    s = np.tile(np.array([[300, 400]], np.float32), (n_crops_sample, 1))
+    t0 = time.perf_counter()
+    decode_batch(hm, c, s)
+    t_dec = time.perf_counter() - t0
+    skel = synth.make_skeletons(N_ANIMALS, 1)
+    kp2d = synth.make_kp2d(cams_np, skel)
+    pts = kp2d[:, 0].transpose(1, 0, 2, 3).reshape(N_VIEWS, -1, 3)
+    p = pts[..., :2].copy()
+    p[pts[..., 2] < TRI_THR] = np.nan
+    g = CameraGroupOracle(cams_np)
+    t0 = time.perf_counter()
+    g.triangulate(p)
+    t_tri = time.perf_counter() - t0
+    crops_per_frame = N_VIEWS * N_ANIMALS
+    t_frame = (t_vit + t_dec) * crops_per_frame / n_crops_sample + t_tri
+    return {"value": N_ANIMALS / t_frame, "unit": "individuals×frames/s", "cores": threads, "kind": "port",
+            "sample": f"ViT-{cfg.name} fp32 flip-test forward + UDP decode of {n_crops_sample} of the frame's "
+                      f"{crops_per_frame} crops (x{crops_per_frame // n_crops_sample} extrapolated) + omnidir DLT "
+                      f"of the frame's {N_ANIMALS}x{N_JOINTS} joints; torch CPU {threads} threads",
+            "seconds_per_frame": t_frame}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from mqhip import _lib, synth
+    from mqhip.geometry import CameraGroup
+    from mqhip.pose import VitPoseHip
+    from mqhip.weights import CONFIGS, make_random_weights
+
+    cfg = CONFIGS[args.model]
+    weights = make_random_weights(cfg, seed=0, device=dev)
+    model = VitPoseHip(cfg, weights, device=local, graph=args.graph)
+    del weights
+    lib, ctx = model.lib, model.ctx
+
+    # ---------------- synthetic, HBM-resident inputs (this rank's frames)
+    cams_np = synth.make_cameras(N_VIEWS)
+    group = CameraGroup.from_dicts(cams_np, device=local)
+    cams_dev = group.cams_tensor()
+    P, FPS = args.resident_frames, args.frames_per_step
+    skel = synth.make_skeletons(N_ANIMALS, P * FPS, seed=2 + rank)
+    kp2d = synth.make_kp2d(cams_np, skel, seed=3 + rank)            # (A, F, C, J, 3)
+    boxes = []
+    for f in range(P * FPS):
+        tight = synth.boxes_from_kp2d(kp2d[:, f].transpose(1, 0, 2, 3))  # (C, A, 4)
+        boxes.append(synth.expand_boxes(tight.reshape(-1, 4)))
+    boxes = torch.from_numpy(np.stack(boxes)).to(dev)                  # (P*FPS, C*A, 4) view-major
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    frames = torch.randint(0, 256, (P * FPS, N_VIEWS, IMG_H, IMG_W, 3), generator=g, device=dev,
+                           dtype=torch.uint8)
+    n = FPS * N_VIEWS * N_ANIMALS
+    box_frame = (torch.arange(n, device=dev, dtype=torch.int32) // N_ANIMALS)  # image index within the step
+    crops = torch.empty((n, 3, 256, 192), device=dev)
+    center = torch.empty((n, 2), device=dev)
+    scale = torch.empty((n, 2), device=dev)
+    hm = torch.empty((n, cfg.n_joints, 64, 48), device=dev)
+    kp = torch.empty((n, cfg.n_joints, 2), device=dev, dtype=torch.float64)
+    score = torch.empty((n, cfg.n_joints), device=dev)
+    am = torch.empty((n, cfg.n_joints), device=dev, dtype=torch.int32)
+    n_steps_total = args.warmup + args.steps
+    kp_log = torch.empty((args.steps, n, cfg.n_joints, 3), device=dev, dtype=torch.float32)
+    p3d = torch.empty((FPS, N_ANIMALS * cfg.n_joints, 3), device=dev, dtype=torch.float64)
+    s_ptr = _lib.stream_ptr(dev)
+
+    def step(i, log_slot=None):
+        f0 = (i % P) * FPS
+        fr = frames[f0:f0 + FPS]                                         # (FPS, C, H, W, 3)
+        bx = boxes[f0:f0 + FPS].reshape(-1, 4)
+        _lib.check(lib.mq_crop_udp(ctx.handle, _lib.ptr(fr), IMG_H * IMG_W * 3, IMG_H, IMG_W, _lib.ptr(bx),
+                                   _lib.ptr(box_frame), n, _lib.ptr(crops), _lib.ptr(center), _lib.ptr(scale),
+                                   s_ptr), "crop")
+        _lib.check(lib.mq_vitpose_forward(model.handle, _lib.ptr(crops), n, 1, _lib.ptr(hm), s_ptr), "forward")
+        _lib.check(lib.mq_decode_udp(ctx.handle, _lib.ptr(hm), n, cfg.n_joints, 64, 48, _lib.ptr(center),
+                                     _lib.ptr(scale), _lib.ptr(kp), _lib.ptr(score), _lib.ptr(am), None, s_ptr),
+                   "decode")
+        # step1 (KP_THR) + step4 (score_threshold) masking, then (C, A*J, 2) per frame
+        bad = (score < TRI_THR).unsqueeze(-1)
+        pts = torch.where(bad, torch.full_like(kp, float("nan")), kp)
+        pts = pts.view(FPS, N_VIEWS, N_ANIMALS * cfg.n_joints, 2)
+        for f in range(FPS):
+            pf = pts[f].contiguous()
+            _lib.check(lib.mq_triangulate_dlt(ctx.handle, _lib.ptr(cams_dev), N_VIEWS, _lib.ptr(pf),
+                                              N_ANIMALS * cfg.n_joints, 1, _lib.ptr(p3d[f]), s_ptr), "dlt")
+        if log_slot is not None:
+            kp_log[log_slot, :, :, :2] = kp.float()
+            kp_log[log_slot, :, :, 2] = score
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    timing = not args.graph
+    if timing:
+        _lib.check(lib.mq_vitpose_timing(model.handle, 1), "timing")
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, log_slot=i)
+    if world > 1:
+        gathered = torch.empty((world,) + tuple(kp_log.shape), device=dev, dtype=kp_log.dtype)
+        dist.all_gather_into_tensor(gathered, kp_log)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if timing:
+        _lib.check(lib.mq_vitpose_timing(model.handle, 0), "timing")
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    roof = None
+    if timing:
+        avg_ms, cnt, fl = C.c_double(), C.c_int(), C.c_int64()
+        _lib.check(lib.mq_vitpose_timing_result(model.handle, C.byref(avg_ms), C.byref(cnt), C.byref(fl)),
+                   "timing_result")
+        achieved = fl.value / (avg_ms.value * 1e-3) / 1e12
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_fc1_gemm.json")
+        if os.path.exists(pmc):
+            try:
+                with open(pmc) as f:
+                    traffic = json.load(f).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "kernel": "gemm_bf16_kernel<EPI_GELU_BF16> (FFN fc1, M=%d N=%d K=%d)" % (
+                    2 * n * cfg.tokens, cfg.ffn, cfg.embed_dims),
+                "flops_per_launch": fl.value, "avg_launch_ms": round(avg_ms.value, 5), "launches": cnt.value}
+
+    frames_done = world * args.steps * FPS
+    value = frames_done * N_ANIMALS / dt
+    crops_per_s = frames_done * N_VIEWS * N_ANIMALS / dt
+    model_tflops = crops_per_s * 2 * cfg.flops_per_forward() / 1e12
+    result = {
+        "metric": METRIC, "value": round(value, 3), "unit": "individuals×frames/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic: seeded random ViTPose weights, random uint8 1536x2048 frames, boxes from projected "
+                "synthetic skeletons, 8 omnidir cameras with the reference's intrinsics",
+        "config": {"workload": "BASELINE config 2 per GPU: 1 frame x 8 views x 4 individuals = 32 crops, "
+                               "ViTPose-%s 256x192 flip test (64 forwards), UDP decode, omnidir DLT" % cfg.name,
+                   "frames_per_step_per_gpu": FPS, "crops_per_step_per_gpu": n,
+                   "parallelism": "frame-shard x%d (RCCL all-gather of 2D keypoints)" % world},
+        "individuals_views_frames_per_s": round(value * N_VIEWS, 3),
+        "crops_per_s": round(crops_per_s, 3),
+        "end_to_end_model_tflops": round(model_tflops, 2),
+        "end_to_end_mfma_frac": round(model_tflops / (world * PEAK_BF16_TFLOPS), 4),
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, cams_np)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

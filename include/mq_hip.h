@@ -1,0 +1,134 @@
+/*
+ * mq_hip.h -- C ABI of libmq_hip.so, the MI355X (gfx950) implementation of the
+ * per-frame 2D->3D pose hot path of sidd-bme/macaque-3d-pose-estimation.
+ *
+ * Conventions:
+ *   - every function returns 0 on success, < 0 on error; mq_last_error() gives text;
+ *   - the caller owns every data buffer (device pointers unless stated otherwise);
+ *     contexts / models own their weights and workspaces;
+ *   - work is stream ordered on the hipStream_t passed as `void* stream`
+ *     (NULL = the null stream); nothing synchronises unless stated;
+ *   - missing 2D / 3D data is NaN on the way in and out (Viterbi emits (-1,-1,0.001)
+ *     for missing frames exactly like anipose).
+ *
+ * Camera parameter rows (`cams`, float64, 24 values per camera, device memory):
+ *   fx, fy, skew, cx, cy, xi, k1, k2, p1, p2, R00..R22 (row-major, from rvec via
+ *   Rodrigues), t0, t1, t2, 0, 0.   (OmnidirCamera K / xi / D / rvec / tvec,
+ *   /root/reference/src/third_party/aniposelib/cameras.py:429-555)
+ */
+#ifndef MQ_HIP_H
+#define MQ_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MQ_ABI_VERSION 1
+
+typedef struct mq_ctx mq_ctx;
+typedef struct mq_vitpose mq_vitpose;
+
+int mq_abi_version(void);
+const char* mq_last_error(void);
+
+/* Bind a context to HIP device `device`. */
+int mq_create(int device, mq_ctx** out);
+int mq_destroy(mq_ctx* ctx);
+
+/* ======================================================================= pose
+ * Replaces mmpose.apis.init_model + inference_topdown for the ViTPose top-down
+ * model (reference: src/pipeline/step1_proc2d.py:100-101 init, :294-298 call,
+ * model/pose/td-hm_ViTPose-huge_8xb64-210e_coco-256x192_sn_macaque.py:54-110).
+ */
+
+/* Create an (empty) ViTPose model: ViT-H = (1280, 32, 16, 5120, 17); ViT-B = (768, 12, 12, 3072, 17). */
+int mq_vitpose_create(mq_ctx* ctx, int embed_dims, int num_layers, int num_heads, int ffn_dims, int n_joints,
+                      mq_vitpose** out);
+int mq_vitpose_destroy(mq_vitpose* model);
+
+/* Load one float32 parameter by its mmpose state_dict name (e.g.
+ * "backbone.layers.3.attn.qkv.weight", "head.deconv_layers.1.running_var").
+ * `data` is device memory if on_device != 0, host memory otherwise.  Synchronous. */
+int mq_vitpose_set_param(mq_vitpose* model, const char* name, const float* data, int64_t numel, int on_device);
+
+/* Verify every parameter was loaded and fold the eval BatchNorms. */
+int mq_vitpose_finalize(mq_vitpose* model);
+
+/* Enable (1) / disable (0) hipGraph capture + replay of mq_vitpose_forward. */
+int mq_vitpose_set_graph(mq_vitpose* model, int enable);
+
+/* Live kernel timing for roofline reporting: while enabled, eager forwards (graph
+ * replay is bypassed) record hipEvents around every FFN fc1 GEMM launch on the
+ * launch stream.  _result synchronises on them and returns the average duration
+ * (ms) per launch, the launch count, and the algorithmic FLOPs of one launch. */
+int mq_vitpose_timing(mq_vitpose* model, int enable);
+int mq_vitpose_timing_result(mq_vitpose* model, double* avg_ms, int* count, int64_t* flops_per_launch);
+
+/* GetBBoxCenterScale(1.25) + TopdownAffine(UDP, 192x256) + PoseDataPreprocessor.
+ *   frames   : uint8 BGR images, image i at frames + i * frame_stride, each height x width x 3
+ *   boxes    : float32 (n, 4) xyxy;  box_frame : int32 (n,) image index of each box
+ *   crops    : float32 (n, 3, 256, 192) normalised RGB (the model input)
+ *   center, scale : float32 (n, 2)  (PoseDataSample input_center / input_scale)      */
+int mq_crop_udp(mq_ctx* ctx, const uint8_t* frames, int64_t frame_stride, int height, int width,
+                const float* boxes, const int32_t* box_frame, int n, float* crops, float* center, float* scale,
+                void* stream);
+
+/* Heatmaps of n crops: float32 (n, J, 64, 48).  With flip_test the model runs 2n
+ * forwards and returns (H + flip_back(H_flip)) * 0.5 (test_cfg flip_mode 'heatmap'). */
+int mq_vitpose_forward(mq_vitpose* model, const float* crops, int n, int flip_test, float* heatmaps, void* stream);
+
+/* UDPHeatmap.decode (get_heatmap_maximum + refine_keypoints_dark_udp, blur 11) and
+ * add_pred_to_datasample.  kp_img float64 (n, J, 2) image pixels; score float32 (n, J);
+ * argmax int32 (n, J) flat heatmap index; kp_hm float32 (n, J, 2) heatmap-space (may be NULL). */
+int mq_decode_udp(mq_ctx* ctx, const float* heatmaps, int n, int n_joints, int hm_h, int hm_w,
+                  const float* center, const float* scale, double* kp_img, float* score, int32_t* argmax,
+                  float* kp_hm, void* stream);
+
+/* crop -> forward(flip) -> decode in one call (inference_topdown batched over boxes of
+ * many views).  heatmaps may be NULL. */
+int mq_topdown(mq_vitpose* model, const uint8_t* frames, int64_t frame_stride, int height, int width,
+               const float* boxes, const int32_t* box_frame, int n, int flip_test, double* kp_img, float* score,
+               int32_t* argmax, float* heatmaps, void* stream);
+
+/* ======================================================================= geometry
+ * Replaces aniposelib CameraGroup (cameras.py:593-783), anipose filter_pose_viterbi
+ * (filter_pose.py:48-186) and the mvpose DLT (multicam_toolbox.py:393-486).
+ */
+
+/* OmnidirCamera.undistort_points for every camera: pts/out float64 (C, N, 2). */
+int mq_omnidir_undistort(mq_ctx* ctx, const double* cams, int n_cams, const double* pts, int n, double* out,
+                         void* stream);
+
+/* OmnidirCamera.project for every camera: p3d (N, 3) -> out (C, N, 2). */
+int mq_omnidir_project(mq_ctx* ctx, const double* cams, int n_cams, const double* p3d, int n, double* out,
+                       void* stream);
+
+/* CameraGroup.triangulate: pts (C, N, 2) raw pixels (undistort != 0) or undistorted; out (N, 3). */
+int mq_triangulate_dlt(mq_ctx* ctx, const double* cams, int n_cams, const double* pts, int n, int undistort,
+                       double* out, void* stream);
+
+/* CameraGroup.reprojection_error: p3d (N,3), p2d (C,N,2) -> out (C,N,2) or (N,) if mean. */
+int mq_reproj_error(mq_ctx* ctx, const double* cams, int n_cams, const double* p3d, const double* p2d, int n,
+                    int mean, double* out, void* stream);
+
+/* CameraGroup.triangulate_ransac (triangulate_possible, n_possible = 1):
+ * p3d (N,3), picked uint8 (C,N), p2d (C,N,2), err (N).  threshold 0.5 in the reference. */
+int mq_triangulate_ransac(mq_ctx* ctx, const double* cams, int n_cams, const double* pts, int n, int min_cams,
+                          double threshold, double* p3d, uint8_t* picked, double* p2d, double* err, void* stream);
+
+/* multicam_toolbox.triangulatePoints: und (C,N,2) undistorted, use uint8 (N,C) -> out (N,3). */
+int mq_triangulate_pinv(mq_ctx* ctx, const double* cams, int n_cams, const double* und, const uint8_t* use, int n,
+                        double* out, void* stream);
+
+/* filter_pose_viterbi over every (animal, camera, joint) chain of kp (A,F,C,J,3)
+ * [x, y, score] (step 4 layout of kp2d.pickle) -> out (A,F,C,J,3).  Scratch is
+ * owned by the context.  score_threshold 0.3, n_back 3, offset_threshold 25 in step 4. */
+int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int n_animals, int n_frames, int n_cams, int n_joints,
+                      double score_threshold, int n_back, double offset_threshold, double* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MQ_HIP_H */

@@ -1,0 +1,669 @@
+// C ABI + native runtime of libmq_hip (include/mq_hip.h).
+//
+// The ViTPose runtime owns bf16 weights laid out for the MFMA GEMM (K-contiguous,
+// deconvs packed as [(ky*4+kx)*Cout + co][Cin]) and a workspace sized for the
+// largest batch seen; a forward is ~7 launches per encoder layer, optionally
+// captured once into a hipGraph and replayed (keyed on batch size and the
+// caller's input/output pointers).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "geometry.hpp"
+#include "kernels.hpp"
+#include "mq_hip.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(const std::string& msg, int code = -1) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) return fail(std::string(#expr ": ") + hipGetErrorString(e_), -5); \
+  } while (0)
+
+#define K_TRY(expr)                                              \
+  do {                                                           \
+    int r_ = (expr);                                             \
+    if (r_ != 0) return fail(std::string(#expr " failed"), -6);  \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t b) {
+    if (b <= bytes) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, b) != hipSuccess) return -1;
+    bytes = b;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+}  // namespace
+
+struct mq_ctx {
+  int device = 0;
+  DevBuf scratch;  // geometry scratch (Viterbi back-pointers)
+  DevBuf decode_work;
+};
+
+struct ParamSlot {
+  int kind;  // 0 bf16 linear/conv, 1 f32 plain, 2 deconv pack, 3 bn part (f32 host copy)
+  int64_t numel;
+  void* dst;
+  int cin, cout;
+  bool loaded = false;
+};
+
+struct Layer {
+  float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+  unsigned short *wqkv, *wproj, *wfc1, *wfc2;
+  float *bqkv, *bproj, *bfc1, *bfc2;
+};
+
+struct mq_vitpose {
+  mq_ctx* ctx;
+  int D, L, H, FF, J;
+  int img_h = 256, img_w = 192, patch = 16, pad = 2, dc = 256;
+  int gh, gw, T;
+  DevBuf weights;  // one arena
+  std::vector<Layer> layers;
+  unsigned short *w_patch, *w_dc1, *w_dc2, *w_fin;
+  float *b_patch, *pos, *lnf_g, *lnf_b, *b_fin;
+  float *bn1_scale, *bn1_shift, *bn2_scale, *bn2_shift;
+  std::vector<float> bn_host[8];  // w1,b1,rm1,rv1,w2,b2,rm2,rv2
+  int32_t* flip_idx;
+  std::map<std::string, ParamSlot> slots;
+  bool finalized = false;
+  // workspace
+  DevBuf ws;
+  int ws_F = 0;
+  unsigned short *A0, *Hn, *QKV, *O, *G, *Y1, *cols2, *Y2;
+  float *X, *hm_all;
+  // graph cache (captured and replayed on a private non-blocking stream that is
+  // event-ordered after / before the caller's stream, so callers may pass the
+  // legacy null stream, which cannot be captured)
+  hipStream_t cap_stream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  bool use_graph = false;
+  hipGraphExec_t gexec = nullptr;
+  int g_n = -1, g_flip = -1;
+  const void* g_in = nullptr;
+  void* g_out = nullptr;
+  // live kernel timing (eager forwards only): hipEvent pairs around every FFN fc1
+  // GEMM launch, recorded on the stream the kernel is launched on
+  bool timing = false;
+  int64_t g_rows_timed = 0;
+  std::vector<hipEvent_t> t_events;
+  size_t t_used = 0;
+};
+
+extern "C" {
+
+int mq_abi_version(void) { return MQ_ABI_VERSION; }
+
+const char* mq_last_error(void) { return g_err.c_str(); }
+
+int mq_create(int device, mq_ctx** out) {
+  if (!out) return fail("mq_create: null out");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail("mq_create: bad device index");
+  HIP_TRY(hipSetDevice(device));
+  mq_ctx* c = new mq_ctx();
+  c->device = device;
+  *out = c;
+  return 0;
+}
+
+int mq_destroy(mq_ctx* ctx) {
+  if (!ctx) return 0;
+  (void)hipSetDevice(ctx->device);
+  ctx->scratch.release();
+  ctx->decode_work.release();
+  delete ctx;
+  return 0;
+}
+
+// ----------------------------------------------------------------------------- ViTPose
+int mq_vitpose_create(mq_ctx* ctx, int D, int L, int H, int FF, int J, mq_vitpose** out) {
+  if (!ctx || !out) return fail("mq_vitpose_create: null argument");
+  if (D <= 0 || L <= 0 || H <= 0 || D % H || FF <= 0 || J <= 0 || J > 128) return fail("mq_vitpose_create: bad dims");
+  const int dh = D / H;
+  if (dh != 64 && dh != 80) return fail("mq_vitpose_create: head dim must be 64 or 80");
+  if (D % 64 || FF % 64 || D > 2048) return fail("mq_vitpose_create: dims must be multiples of 64, D <= 2048");
+  HIP_TRY(hipSetDevice(ctx->device));
+  mq_vitpose* m = new mq_vitpose();
+  m->ctx = ctx;
+  m->D = D;
+  m->L = L;
+  m->H = H;
+  m->FF = FF;
+  m->J = J;
+  m->gh = (m->img_h + 2 * m->pad - m->patch) / m->patch + 1;
+  m->gw = (m->img_w + 2 * m->pad - m->patch) / m->patch + 1;
+  m->T = m->gh * m->gw;
+  const int KP = 3 * m->patch * m->patch;
+  const int dc = m->dc;
+  // arena layout
+  std::vector<std::pair<void**, size_t>> plan;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  struct Req {
+    std::string name;
+    int kind;
+    int64_t numel;
+    size_t offset;
+    int cin, cout;
+  };
+  std::vector<Req> reqs;
+  auto add = [&](const std::string& name, int kind, int64_t numel, size_t elem, int cin = 0, int cout = 0) {
+    size_t o = take((size_t)numel * elem);
+    reqs.push_back({name, kind, numel, o, cin, cout});
+    return o;
+  };
+  size_t o_wpatch = add("backbone.patch_embed.projection.weight", 0, (int64_t)D * KP, 2);
+  size_t o_bpatch = add("backbone.patch_embed.projection.bias", 1, D, 4);
+  size_t o_pos = add("backbone.pos_embed", 1, (int64_t)m->T * D, 4);
+  struct LOff {
+    size_t l1g, l1b, l2g, l2b, wq, wp, w1, w2, bq, bp, b1, b2;
+  };
+  std::vector<LOff> lo(L);
+  for (int i = 0; i < L; ++i) {
+    std::string p = "backbone.layers." + std::to_string(i) + ".";
+    lo[i].l1g = add(p + "ln1.weight", 1, D, 4);
+    lo[i].l1b = add(p + "ln1.bias", 1, D, 4);
+    lo[i].wq = add(p + "attn.qkv.weight", 0, (int64_t)3 * D * D, 2);
+    lo[i].bq = add(p + "attn.qkv.bias", 1, 3 * D, 4);
+    lo[i].wp = add(p + "attn.proj.weight", 0, (int64_t)D * D, 2);
+    lo[i].bp = add(p + "attn.proj.bias", 1, D, 4);
+    lo[i].l2g = add(p + "ln2.weight", 1, D, 4);
+    lo[i].l2b = add(p + "ln2.bias", 1, D, 4);
+    lo[i].w1 = add(p + "ffn.layers.0.0.weight", 0, (int64_t)FF * D, 2);
+    lo[i].b1 = add(p + "ffn.layers.0.0.bias", 1, FF, 4);
+    lo[i].w2 = add(p + "ffn.layers.1.weight", 0, (int64_t)D * FF, 2);
+    lo[i].b2 = add(p + "ffn.layers.1.bias", 1, D, 4);
+  }
+  size_t o_lnfg = add("backbone.ln1.weight", 1, D, 4);
+  size_t o_lnfb = add("backbone.ln1.bias", 1, D, 4);
+  size_t o_dc1 = add("head.deconv_layers.0.weight", 2, (int64_t)D * dc * 16, 2, D, dc);
+  size_t o_dc2 = add("head.deconv_layers.3.weight", 2, (int64_t)dc * dc * 16, 2, dc, dc);
+  // final 1x1 conv: pad rows to a multiple of 8 is not needed (N masked in the GEMM)
+  size_t o_fin = add("head.final_layer.weight", 0, (int64_t)J * dc, 2);
+  size_t o_bfin = add("head.final_layer.bias", 1, J, 4);
+  const char* bn_names[8] = {"head.deconv_layers.1.weight", "head.deconv_layers.1.bias",
+                             "head.deconv_layers.1.running_mean", "head.deconv_layers.1.running_var",
+                             "head.deconv_layers.4.weight", "head.deconv_layers.4.bias",
+                             "head.deconv_layers.4.running_mean", "head.deconv_layers.4.running_var"};
+  size_t o_bn = take(4 * (size_t)dc * 4);
+  size_t o_flip = take(128 * 4);
+  if (m->weights.ensure(off)) {
+    delete m;
+    return fail("mq_vitpose_create: hipMalloc of weights failed", -5);
+  }
+  char* base = m->weights.as<char>();
+  for (auto& r : reqs) {
+    ParamSlot s;
+    s.kind = r.kind;
+    s.numel = r.numel;
+    s.dst = base + r.offset;
+    s.cin = r.cin;
+    s.cout = r.cout;
+    m->slots[r.name] = s;
+  }
+  for (int k = 0; k < 8; ++k) {
+    ParamSlot s;
+    s.kind = 3;
+    s.numel = dc;
+    s.dst = nullptr;
+    s.cin = k;
+    s.cout = 0;
+    m->slots[bn_names[k]] = s;
+  }
+  m->w_patch = (unsigned short*)(base + o_wpatch);
+  m->b_patch = (float*)(base + o_bpatch);
+  m->pos = (float*)(base + o_pos);
+  m->layers.resize(L);
+  for (int i = 0; i < L; ++i) {
+    Layer& ly = m->layers[i];
+    ly.ln1_g = (float*)(base + lo[i].l1g);
+    ly.ln1_b = (float*)(base + lo[i].l1b);
+    ly.ln2_g = (float*)(base + lo[i].l2g);
+    ly.ln2_b = (float*)(base + lo[i].l2b);
+    ly.wqkv = (unsigned short*)(base + lo[i].wq);
+    ly.wproj = (unsigned short*)(base + lo[i].wp);
+    ly.wfc1 = (unsigned short*)(base + lo[i].w1);
+    ly.wfc2 = (unsigned short*)(base + lo[i].w2);
+    ly.bqkv = (float*)(base + lo[i].bq);
+    ly.bproj = (float*)(base + lo[i].bp);
+    ly.bfc1 = (float*)(base + lo[i].b1);
+    ly.bfc2 = (float*)(base + lo[i].b2);
+  }
+  m->lnf_g = (float*)(base + o_lnfg);
+  m->lnf_b = (float*)(base + o_lnfb);
+  m->w_dc1 = (unsigned short*)(base + o_dc1);
+  m->w_dc2 = (unsigned short*)(base + o_dc2);
+  m->w_fin = (unsigned short*)(base + o_fin);
+  m->b_fin = (float*)(base + o_bfin);
+  m->bn1_scale = (float*)(base + o_bn);
+  m->bn1_shift = m->bn1_scale + dc;
+  m->bn2_scale = m->bn1_scale + 2 * dc;
+  m->bn2_shift = m->bn1_scale + 3 * dc;
+  m->flip_idx = (int32_t*)(base + o_flip);
+  // macaque flip pairs (model/pose/macaque.py:15-130); identity beyond 17 joints
+  int32_t fi[128];
+  const int32_t mac[17] = {0, 2, 1, 4, 3, 6, 5, 8, 7, 10, 9, 12, 11, 14, 13, 16, 15};
+  for (int k = 0; k < 128; ++k) fi[k] = (J == 17 && k < 17) ? mac[k] : k;
+  HIP_TRY(hipMemcpy(m->flip_idx, fi, sizeof(fi), hipMemcpyHostToDevice));
+  *out = m;
+  return 0;
+}
+
+int mq_vitpose_destroy(mq_vitpose* m) {
+  if (!m) return 0;
+  (void)hipSetDevice(m->ctx->device);
+  if (m->gexec) (void)hipGraphExecDestroy(m->gexec);
+  for (hipEvent_t e : m->t_events) (void)hipEventDestroy(e);
+  if (m->cap_stream) (void)hipStreamDestroy(m->cap_stream);
+  if (m->ev_in) (void)hipEventDestroy(m->ev_in);
+  if (m->ev_out) (void)hipEventDestroy(m->ev_out);
+  m->weights.release();
+  m->ws.release();
+  delete m;
+  return 0;
+}
+
+int mq_vitpose_set_param(mq_vitpose* m, const char* name, const float* data, int64_t numel, int on_device) {
+  if (!m || !name || !data) return fail("mq_vitpose_set_param: null argument");
+  auto it = m->slots.find(name);
+  if (it == m->slots.end()) return fail(std::string("mq_vitpose_set_param: unknown parameter ") + name, -2);
+  ParamSlot& s = it->second;
+  if (numel != s.numel)
+    return fail(std::string("mq_vitpose_set_param: numel mismatch for ") + name + " expected " +
+                    std::to_string(s.numel) + " got " + std::to_string(numel),
+                -3);
+  HIP_TRY(hipSetDevice(m->ctx->device));
+  if (s.kind == 3) {
+    std::vector<float>& h = m->bn_host[s.cin];
+    h.resize(numel);
+    if (on_device)
+      HIP_TRY(hipMemcpy(h.data(), data, numel * 4, hipMemcpyDeviceToHost));
+    else
+      std::memcpy(h.data(), data, numel * 4);
+    s.loaded = true;
+    m->finalized = false;
+    return 0;
+  }
+  const float* src = data;
+  void* tmp = nullptr;
+  if (!on_device) {
+    HIP_TRY(hipMalloc(&tmp, numel * 4));
+    HIP_TRY(hipMemcpy(tmp, data, numel * 4, hipMemcpyHostToDevice));
+    src = (const float*)tmp;
+  }
+  int rc = 0;
+  if (s.kind == 1) {
+    if (hipMemcpy(s.dst, src, numel * 4, hipMemcpyDeviceToDevice) != hipSuccess) rc = -5;
+  } else if (s.kind == 0) {
+    rc = mq::convert_f32_bf16(src, (unsigned short*)s.dst, numel, nullptr);
+  } else if (s.kind == 2) {
+    rc = mq::deconv_weight_pack(src, (unsigned short*)s.dst, s.cin, s.cout, nullptr);
+  }
+  if (rc == 0 && hipDeviceSynchronize() != hipSuccess) rc = -5;
+  if (tmp) (void)hipFree(tmp);
+  if (rc) return fail(std::string("mq_vitpose_set_param: device copy failed for ") + name, rc);
+  s.loaded = true;
+  m->finalized = false;
+  return 0;
+}
+
+int mq_vitpose_finalize(mq_vitpose* m) {
+  if (!m) return fail("mq_vitpose_finalize: null model");
+  for (auto& kv : m->slots)
+    if (!kv.second.loaded) return fail("mq_vitpose_finalize: parameter not loaded: " + kv.first, -2);
+  // eval BatchNorm: y = (x - rm) / sqrt(rv + eps) * w + b = x * scale + shift
+  std::vector<float> ss(4 * m->dc);
+  for (int l = 0; l < 2; ++l) {
+    const std::vector<float>* h = &m->bn_host[4 * l];
+    for (int c = 0; c < m->dc; ++c) {
+      const double sc = (double)h[0][c] / std::sqrt((double)h[3][c] + 1e-5);
+      ss[(2 * l) * m->dc + c] = (float)sc;
+      ss[(2 * l + 1) * m->dc + c] = (float)((double)h[1][c] - (double)h[2][c] * sc);
+    }
+  }
+  HIP_TRY(hipSetDevice(m->ctx->device));
+  HIP_TRY(hipMemcpy(m->bn1_scale, ss.data(), ss.size() * 4, hipMemcpyHostToDevice));
+  m->finalized = true;
+  if (m->gexec) {
+    (void)hipGraphExecDestroy(m->gexec);
+    m->gexec = nullptr;
+  }
+  return 0;
+}
+
+int mq_vitpose_set_graph(mq_vitpose* m, int enable) {
+  if (!m) return fail("mq_vitpose_set_graph: null model");
+  m->use_graph = enable != 0;
+  if (!m->use_graph && m->gexec) {
+    (void)hipGraphExecDestroy(m->gexec);
+    m->gexec = nullptr;
+  }
+  return 0;
+}
+
+static int ensure_workspace(mq_vitpose* m, int F) {
+  if (F <= m->ws_F) return 0;
+  const size_t T = m->T, D = m->D, FF = m->FF, dc = m->dc;
+  const size_t rows = (size_t)F * T;
+  const size_t KP = 3 * m->patch * m->patch;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  size_t oA0 = take(rows * KP * 2);
+  size_t oX = take(rows * D * 4);
+  size_t oH = take(rows * D * 2);
+  size_t oQKV = take(rows * 3 * D * 2);
+  size_t oO = take(rows * D * 2);
+  size_t big = std::max(rows * FF * 2, rows * 16 * dc * 2);  // G and cols1 share
+  size_t oG = take(big);
+  size_t oY1 = take((size_t)F * 4 * T * dc * 2);
+  size_t oC2 = take((size_t)F * 4 * T * 16 * dc * 2);
+  size_t oY2 = take((size_t)F * 16 * T * dc * 2);
+  size_t oHM = take((size_t)F * m->J * 16 * T * 4);
+  if (m->ws.ensure(off)) return fail("workspace hipMalloc failed", -5);
+  char* b = m->ws.as<char>();
+  m->A0 = (unsigned short*)(b + oA0);
+  m->X = (float*)(b + oX);
+  m->Hn = (unsigned short*)(b + oH);
+  m->QKV = (unsigned short*)(b + oQKV);
+  m->O = (unsigned short*)(b + oO);
+  m->G = (unsigned short*)(b + oG);
+  m->Y1 = (unsigned short*)(b + oY1);
+  m->cols2 = (unsigned short*)(b + oC2);
+  m->Y2 = (unsigned short*)(b + oY2);
+  m->hm_all = (float*)(b + oHM);
+  m->ws_F = F;
+  if (m->gexec) {
+    (void)hipGraphExecDestroy(m->gexec);
+    m->gexec = nullptr;
+  }
+  return 0;
+}
+
+static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, float* heatmaps, hipStream_t s) {
+  const int F = flip ? 2 * n : n;
+  const int T = m->T, D = m->D, FF = m->FF, dc = m->dc;
+  const int rows = F * T;
+  const int KP = 3 * m->patch * m->patch;
+  m->g_rows_timed = rows;
+  K_TRY(mq::patch_im2col(crops, m->A0, n, flip ? 2 : 1, m->img_h, m->img_w, m->patch, m->pad, s));
+  mq::GemmArgs g{};
+  g = mq::GemmArgs{m->A0, m->w_patch, m->X, m->b_patch, m->pos, rows, D, KP, KP, KP, D, T};
+  K_TRY(mq::gemm_bf16(g, mq::EPI_POS_F32, s));
+  for (int l = 0; l < m->L; ++l) {
+    const Layer& ly = m->layers[l];
+    K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
+    g = mq::GemmArgs{m->Hn, ly.wqkv, m->QKV, ly.bqkv, nullptr, rows, 3 * D, D, D, D, 3 * D, 0};
+    K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+    K_TRY(mq::attention_bf16(m->QKV, m->O, F, T, D, m->H, s));
+    g = mq::GemmArgs{m->O, ly.wproj, m->X, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
+    K_TRY(mq::gemm_bf16(g, mq::EPI_RESID_F32, s));
+    K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
+    g = mq::GemmArgs{m->Hn, ly.wfc1, m->G, ly.bfc1, nullptr, rows, FF, D, D, D, FF, 0};
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (m->timing) {
+      while (m->t_events.size() < m->t_used + 2) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        m->t_events.push_back(e);
+      }
+      e0 = m->t_events[m->t_used];
+      e1 = m->t_events[m->t_used + 1];
+      m->t_used += 2;
+      HIP_TRY(hipEventRecord(e0, s));
+    }
+    K_TRY(mq::gemm_bf16(g, mq::EPI_GELU_BF16, s));
+    if (m->timing) HIP_TRY(hipEventRecord(e1, s));
+    g = mq::GemmArgs{m->G, ly.wfc2, m->X, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0};
+    K_TRY(mq::gemm_bf16(g, mq::EPI_RESID_F32, s));
+  }
+  K_TRY(mq::layernorm_f32_bf16(m->X, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
+  // head: deconv1 (GEMM + col2im + BN + ReLU)
+  unsigned short* cols1 = m->G;
+  g = mq::GemmArgs{m->Hn, m->w_dc1, cols1, nullptr, nullptr, rows, 16 * dc, D, D, D, 16 * dc, 0};
+  K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+  K_TRY(mq::deconv_col2im_bn_relu(cols1, m->bn1_scale, m->bn1_shift, m->Y1, F, m->gh, m->gw, dc, s));
+  const int rows2 = F * 4 * T;
+  g = mq::GemmArgs{m->Y1, m->w_dc2, m->cols2, nullptr, nullptr, rows2, 16 * dc, dc, dc, dc, 16 * dc, 0};
+  K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+  K_TRY(mq::deconv_col2im_bn_relu(m->cols2, m->bn2_scale, m->bn2_shift, m->Y2, F, 2 * m->gh, 2 * m->gw, dc, s));
+  const int rows3 = F * 16 * T;
+  float* hm_dst = flip ? m->hm_all : heatmaps;
+  g = mq::GemmArgs{m->Y2, m->w_fin, hm_dst, m->b_fin, nullptr, rows3, m->J, dc, dc, dc, m->J, 16 * T};
+  K_TRY(mq::gemm_bf16(g, mq::EPI_NCHW_F32, s));
+  if (flip) K_TRY(mq::flip_average(m->hm_all, heatmaps, n, m->J, 4 * m->gh, 4 * m->gw, m->flip_idx, s));
+  return 0;
+}
+
+int mq_vitpose_forward(mq_vitpose* m, const float* crops, int n, int flip_test, float* heatmaps, void* stream) {
+  if (!m || !crops || !heatmaps) return fail("mq_vitpose_forward: null argument");
+  if (!m->finalized) return fail("mq_vitpose_forward: model not finalized", -2);
+  if (n <= 0) return 0;
+  HIP_TRY(hipSetDevice(m->ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int F = flip_test ? 2 * n : n;
+  int rc = ensure_workspace(m, F);
+  if (rc) return rc;
+  if (!m->use_graph || m->timing) return launch_forward(m, crops, n, flip_test, heatmaps, s);
+  if (!m->cap_stream) {
+    HIP_TRY(hipStreamCreateWithFlags(&m->cap_stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&m->ev_out, hipEventDisableTiming));
+  }
+  hipStream_t cs = m->cap_stream;
+  if (!m->gexec || m->g_n != n || m->g_flip != flip_test || m->g_in != crops || m->g_out != heatmaps) {
+    if (m->gexec) {
+      (void)hipGraphExecDestroy(m->gexec);
+      m->gexec = nullptr;
+    }
+    HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    rc = launch_forward(m, crops, n, flip_test, heatmaps, cs);
+    hipGraph_t graph = nullptr;
+    hipError_t e = hipStreamEndCapture(cs, &graph);
+    if (rc) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    if (e != hipSuccess) return fail(std::string("hipStreamEndCapture: ") + hipGetErrorString(e), -5);
+    e = hipGraphInstantiate(&m->gexec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) return fail(std::string("hipGraphInstantiate: ") + hipGetErrorString(e), -5);
+    m->g_n = n;
+    m->g_flip = flip_test;
+    m->g_in = crops;
+    m->g_out = heatmaps;
+  }
+  HIP_TRY(hipEventRecord(m->ev_in, s));
+  HIP_TRY(hipStreamWaitEvent(cs, m->ev_in, 0));
+  HIP_TRY(hipGraphLaunch(m->gexec, cs));
+  HIP_TRY(hipEventRecord(m->ev_out, cs));
+  HIP_TRY(hipStreamWaitEvent(s, m->ev_out, 0));
+  return 0;
+}
+
+int mq_vitpose_timing(mq_vitpose* m, int enable) {
+  if (!m) return fail("mq_vitpose_timing: null model");
+  m->timing = enable != 0;
+  if (m->timing) m->t_used = 0;
+  return 0;
+}
+
+int mq_vitpose_timing_result(mq_vitpose* m, double* avg_ms, int* count, int64_t* flops_per_launch) {
+  if (!m || !avg_ms || !count) return fail("mq_vitpose_timing_result: null argument");
+  double tot = 0.0;
+  int cnt = 0;
+  for (size_t i = 0; i + 1 < m->t_used; i += 2) {
+    HIP_TRY(hipEventSynchronize(m->t_events[i + 1]));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, m->t_events[i], m->t_events[i + 1]));
+    tot += ms;
+    ++cnt;
+  }
+  *avg_ms = cnt ? tot / cnt : 0.0;
+  *count = cnt;
+  if (flops_per_launch) *flops_per_launch = (int64_t)2 * (int64_t)(m->g_rows_timed) * m->FF * m->D;
+  return 0;
+}
+
+int mq_crop_udp(mq_ctx* ctx, const uint8_t* frames, int64_t frame_stride, int height, int width, const float* boxes,
+                const int32_t* box_frame, int n, float* crops, float* center, float* scale, void* stream) {
+  if (!ctx) return fail("mq_crop_udp: null ctx");
+  if (n < 0 || height <= 0 || width <= 0) return fail("mq_crop_udp: bad sizes");
+  if (n == 0) return 0;
+  if (!frames || !boxes || !box_frame || !crops || !center || !scale) return fail("mq_crop_udp: null buffer");
+  HIP_TRY(hipSetDevice(ctx->device));
+  K_TRY(mq::crop_udp(frames, frame_stride, height, width, boxes, box_frame, n, crops, center, scale,
+                     (hipStream_t)stream));
+  return 0;
+}
+
+int mq_decode_udp(mq_ctx* ctx, const float* heatmaps, int n, int J, int hm_h, int hm_w, const float* center,
+                  const float* scale, double* kp_img, float* score, int32_t* argmax, float* kp_hm, void* stream) {
+  if (!ctx) return fail("mq_decode_udp: null ctx");
+  if (n < 0 || J <= 0 || hm_h <= 0 || hm_w <= 0) return fail("mq_decode_udp: bad sizes");
+  if (n == 0) return 0;
+  if (!heatmaps || !center || !scale || !kp_img || !score || !argmax) return fail("mq_decode_udp: null buffer");
+  if ((size_t)(hm_h * hm_w + (hm_h + 10) * hm_w) * 4 > 64 * 1024) return fail("mq_decode_udp: heatmap too large");
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (ctx->decode_work.ensure((size_t)n * J * hm_h * hm_w * 4)) return fail("decode workspace alloc failed", -5);
+  K_TRY(mq::udp_decode(heatmaps, n, J, hm_h, hm_w, center, scale, 192, 256, ctx->decode_work.as<float>(), kp_img,
+                       score, argmax, kp_hm, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_topdown(mq_vitpose* m, const uint8_t* frames, int64_t frame_stride, int height, int width, const float* boxes,
+               const int32_t* box_frame, int n, int flip_test, double* kp_img, float* score, int32_t* argmax,
+               float* heatmaps, void* stream) {
+  if (!m) return fail("mq_topdown: null model");
+  if (n <= 0) return 0;
+  HIP_TRY(hipSetDevice(m->ctx->device));
+  // scratch: crops, center/scale, heatmaps (if caller passes none)
+  static thread_local DevBuf tmp;  // per-thread staging, grown on demand
+  const size_t crop_b = (size_t)n * 3 * m->img_h * m->img_w * 4;
+  const size_t cs_b = (size_t)n * 4 * 4;
+  const size_t hm_b = (size_t)n * m->J * 16 * m->T * 4;
+  if (tmp.ensure(crop_b + cs_b + hm_b + 1024)) return fail("mq_topdown: scratch alloc failed", -5);
+  char* b = tmp.as<char>();
+  float* crops = (float*)b;
+  float* center = (float*)(b + crop_b);
+  float* scale = center + 2 * n;
+  float* hm = heatmaps ? heatmaps : (float*)(b + crop_b + cs_b);
+  int rc = mq_crop_udp(m->ctx, frames, frame_stride, height, width, boxes, box_frame, n, crops, center, scale, stream);
+  if (rc) return rc;
+  rc = mq_vitpose_forward(m, crops, n, flip_test, hm, stream);
+  if (rc) return rc;
+  return mq_decode_udp(m->ctx, hm, n, m->J, 4 * m->gh, 4 * m->gw, center, scale, kp_img, score, argmax, nullptr,
+                       stream);
+}
+
+// ----------------------------------------------------------------------------- geometry
+static int check_geo(mq_ctx* ctx, const void* cams, int C, int n) {
+  if (!ctx) return fail("null ctx");
+  if (!cams) return fail("null cams");
+  if (C <= 0 || C > 16) return fail("n_cams must be in [1, 16]", -2);
+  if (n < 0) return fail("negative n", -2);
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail("hipSetDevice failed", -5);
+  return 0;
+}
+
+int mq_omnidir_undistort(mq_ctx* ctx, const double* cams, int C, const double* pts, int n, double* out,
+                         void* stream) {
+  int rc = check_geo(ctx, cams, C, n);
+  if (rc) return rc;
+  K_TRY(mq::omnidir_undistort(cams, C, pts, out, n, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_omnidir_project(mq_ctx* ctx, const double* cams, int C, const double* p3d, int n, double* out, void* stream) {
+  int rc = check_geo(ctx, cams, C, n);
+  if (rc) return rc;
+  K_TRY(mq::omnidir_project(cams, C, p3d, out, n, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_triangulate_dlt(mq_ctx* ctx, const double* cams, int C, const double* pts, int n, int undistort, double* out,
+                       void* stream) {
+  int rc = check_geo(ctx, cams, C, n);
+  if (rc) return rc;
+  K_TRY(mq::triangulate_dlt(cams, C, pts, n, undistort, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_reproj_error(mq_ctx* ctx, const double* cams, int C, const double* p3d, const double* p2d, int n, int mean,
+                    double* out, void* stream) {
+  int rc = check_geo(ctx, cams, C, n);
+  if (rc) return rc;
+  K_TRY(mq::reprojection_error(cams, C, p3d, p2d, n, mean, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_triangulate_ransac(mq_ctx* ctx, const double* cams, int C, const double* pts, int n, int min_cams,
+                          double threshold, double* p3d, uint8_t* picked, double* p2d, double* err, void* stream) {
+  int rc = check_geo(ctx, cams, C, n);
+  if (rc) return rc;
+  K_TRY(mq::triangulate_ransac(cams, C, pts, n, min_cams, threshold, p3d, picked, p2d, err, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_triangulate_pinv(mq_ctx* ctx, const double* cams, int C, const double* und, const uint8_t* use, int n,
+                        double* out, void* stream) {
+  int rc = check_geo(ctx, cams, C, n);
+  if (rc) return rc;
+  K_TRY(mq::triangulate_pinv(cams, C, und, use, n, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int A, int F, int C, int J, double score_threshold, int n_back,
+                      double offset_threshold, double* out, void* stream) {
+  if (!ctx || !kp || !out) return fail("mq_viterbi_filter: null argument");
+  if (A < 0 || F < 0 || C < 0 || J < 0) return fail("mq_viterbi_filter: negative size", -2);
+  if (n_back < 1 || n_back > 8) return fail("mq_viterbi_filter: n_back must be in [1, 8]", -2);
+  if ((int64_t)A * F * C * J == 0) return 0;
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (ctx->scratch.ensure((size_t)A * C * J * F * 8)) return fail("viterbi scratch alloc failed", -5);
+  K_TRY(mq::viterbi_filter(kp, A, F, C, J, score_threshold, n_back, offset_threshold, ctx->scratch.as<int8_t>(), out,
+                           (hipStream_t)stream));
+  return 0;
+}
+
+}  // extern "C"

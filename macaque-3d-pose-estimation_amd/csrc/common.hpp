@@ -1,0 +1,48 @@
+// Shared helpers for the MI355X (gfx950 / CDNA4) kernels of libmq_hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short short4v;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef unsigned short bf16_t;  // raw bf16 storage
+
+#define MQ_LDS_GLOBAL(p) ((const void __attribute__((address_space(1)))*)(p))
+#define MQ_LDS_LOCAL(p) ((void __attribute__((address_space(3)))*)(p))
+
+__device__ __forceinline__ float bf16_to_f32(bf16_t v) {
+  return __uint_as_float(((unsigned)v) << 16);
+}
+
+// round-to-nearest-even f32 -> bf16 (NaN kept NaN)
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
+  return (unsigned)f32_to_bf16(a) | ((unsigned)f32_to_bf16(b) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Camera row layout shared with include/mq_hip.h (24 doubles per camera).
+struct CamParams {
+  double fx, fy, skew, cx, cy, xi, k1, k2, p1, p2;
+  double R[9];
+  double t[3];
+  double pad[2];
+};

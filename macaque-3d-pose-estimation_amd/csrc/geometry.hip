@@ -1,0 +1,602 @@
+// float64 multi-view geometry kernels (anipose / mvpose lift).
+// Compiled with -ffp-contract=off so every expression rounds like the numpy oracle.
+#include "common.hpp"
+#include "geometry.hpp"
+
+namespace mq {
+
+__device__ __forceinline__ const CamParams& cam_at(const double* cams, int c) {
+  return *reinterpret_cast<const CamParams*>(cams + 24 * c);
+}
+
+// cv2.omnidir.undistortPoints(p, K, D, xi, R = I) restated (oracle/geometry.py).
+__device__ __forceinline__ void omni_undistort(const CamParams& cp, double u, double v, double& ox, double& oy) {
+  const double fx = cp.fx, fy = cp.fy, cx = cp.cx, cy = cp.cy, s = cp.skew;
+  const double ppx = (u * fy - cx * fy - s * (v - cy)) / (fx * fy);
+  const double ppy = (v - cy) / fy;
+  double x = ppx, y = ppy;
+  for (int it = 0; it < 20; ++it) {
+    const double r2 = x * x + y * y;
+    const double r4 = r2 * r2;
+    x = (ppx - 2 * cp.p1 * x * y - cp.p2 * (r2 + 2 * x * x)) / (1 + cp.k1 * r2 + cp.k2 * r4);
+    y = (ppy - 2 * cp.p2 * x * y - cp.p1 * (r2 + 2 * y * y)) / (1 + cp.k1 * r2 + cp.k2 * r4);
+  }
+  const double xi = cp.xi;
+  const double r2 = x * x + y * y;
+  const double a = r2 + 1;
+  const double b = 2 * xi * r2;
+  const double cc = r2 * xi * xi - 1;
+  const double Zs = (-b + sqrt(b * b - 4 * a * cc)) / (2 * a);
+  const double Xw = x * (Zs + xi), Yw = y * (Zs + xi);
+  const double nrm = sqrt(Xw * Xw + Yw * Yw + Zs * Zs);
+  const double Xs = Xw / nrm, Ys = Yw / nrm, Zn = Zs / nrm;
+  ox = Xs / Zn;
+  oy = Ys / Zn;
+}
+
+// cv2.omnidir.projectPoints(X, rvec, tvec, K, xi, D) restated.
+__device__ __forceinline__ void omni_project(const CamParams& cp, double X, double Y, double Z, double& u,
+                                             double& v) {
+  const double* R = cp.R;
+  const double x0 = R[0] * X + R[1] * Y + R[2] * Z + cp.t[0];
+  const double x1 = R[3] * X + R[4] * Y + R[5] * Z + cp.t[1];
+  const double x2 = R[6] * X + R[7] * Y + R[8] * Z + cp.t[2];
+  const double nrm = sqrt(x0 * x0 + x1 * x1 + x2 * x2);
+  const double xs = x0 / nrm, ys = x1 / nrm, zs = x2 / nrm;
+  const double xu = xs / (zs + cp.xi), yu = ys / (zs + cp.xi);
+  const double r2 = xu * xu + yu * yu;
+  const double r4 = r2 * r2;
+  const double xd = xu * (1 + cp.k1 * r2 + cp.k2 * r4) + 2 * cp.p1 * xu * yu + cp.p2 * (r2 + 2 * xu * xu);
+  const double yd = yu * (1 + cp.k1 * r2 + cp.k2 * r4) + cp.p1 * (r2 + 2 * yu * yu) + 2 * cp.p2 * xu * yu;
+  u = cp.fx * xd + cp.skew * yd + cp.cx;
+  v = cp.fy * yd + cp.cy;
+}
+
+// One-sided (Hestenes) Jacobi SVD of an m x N matrix held as N columns of length M
+// (unused rows zero).  Returns the right singular vectors in V and the column
+// norms (singular values) in sig.
+template <int M, int N>
+__device__ __forceinline__ void jacobi_svd(double (&a)[N][M], double (&V)[N][N], double (&sig)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    bool rotated = false;
+#pragma unroll
+    for (int p = 0; p < N - 1; ++p) {
+#pragma unroll
+      for (int q = p + 1; q < N; ++q) {
+        double alpha = 0, beta = 0, gamma = 0;
+#pragma unroll
+        for (int i = 0; i < M; ++i) {
+          alpha += a[p][i] * a[p][i];
+          beta += a[q][i] * a[q][i];
+          gamma += a[p][i] * a[q][i];
+        }
+        if (fabs(gamma) > 1e-15 * sqrt(alpha * beta) && gamma != 0.0) {
+          rotated = true;
+          const double zeta = (beta - alpha) / (2.0 * gamma);
+          const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+          const double c = 1.0 / sqrt(1.0 + t * t);
+          const double s = c * t;
+#pragma unroll
+          for (int i = 0; i < M; ++i) {
+            const double ap = a[p][i], aq = a[q][i];
+            a[p][i] = c * ap - s * aq;
+            a[q][i] = s * ap + c * aq;
+          }
+#pragma unroll
+          for (int i = 0; i < N; ++i) {
+            const double vp = V[p][i], vq = V[q][i];
+            V[p][i] = c * vp - s * vq;
+            V[q][i] = s * vp + c * vq;
+          }
+        }
+      }
+    }
+    if (!rotated) break;
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i) s += a[j][i] * a[j][i];
+    sig[j] = sqrt(s);
+  }
+}
+
+// Homogeneous DLT (cameras.py:20-32) over the cameras flagged in `use`.
+template <int MAXC>
+__device__ __forceinline__ void dlt_point(const double* cams, int C, const double* ux, const double* uy,
+                                          unsigned use, double out[3]) {
+  double a[4][2 * MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const bool on = (c < C) && ((use >> c) & 1u);
+    if (on) {
+      const CamParams& cp = cam_at(cams, c);
+      const double P0[4] = {cp.R[0], cp.R[1], cp.R[2], cp.t[0]};
+      const double P1[4] = {cp.R[3], cp.R[4], cp.R[5], cp.t[1]};
+      const double P2[4] = {cp.R[6], cp.R[7], cp.R[8], cp.t[2]};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k][2 * c] = ux[c] * P2[k] - P0[k];
+        a[k][2 * c + 1] = uy[c] * P2[k] - P1[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k][2 * c] = 0.0;
+        a[k][2 * c + 1] = 0.0;
+      }
+    }
+  }
+  double V[4][4], sig[4];
+  jacobi_svd<2 * MAXC, 4>(a, V, sig);
+  int jmin = 0;
+#pragma unroll
+  for (int j = 1; j < 4; ++j)
+    if (sig[j] < sig[jmin]) jmin = j;
+  double v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = V[jmin][k];
+  out[0] = v[0] / v[3];
+  out[1] = v[1] / v[3];
+  out[2] = v[2] / v[3];
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ void undistort_kernel(const double* __restrict__ cams, int C, const double* __restrict__ pts,
+                                 double* __restrict__ out, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * N) return;
+  const int c = i / N;
+  double ox, oy;
+  omni_undistort(cam_at(cams, c), pts[2 * i], pts[2 * i + 1], ox, oy);
+  out[2 * i] = ox;
+  out[2 * i + 1] = oy;
+}
+
+__global__ void project_kernel(const double* __restrict__ cams, int C, const double* __restrict__ p3d,
+                               double* __restrict__ out, int N) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * N) return;
+  const int c = i / N, n = i % N;
+  double u, v;
+  omni_project(cam_at(cams, c), p3d[3 * n], p3d[3 * n + 1], p3d[3 * n + 2], u, v);
+  out[2 * i] = u;
+  out[2 * i + 1] = v;
+}
+
+// CameraGroup.triangulate (cameras.py:593-637): optional undistort, >= 2 views.
+template <int MAXC>
+__global__ void triangulate_kernel(const double* __restrict__ cams, int C, const double* __restrict__ pts, int N,
+                                   int undistort, double* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double ux[MAXC], uy[MAXC];
+  unsigned use = 0;
+  int cnt = 0;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    ux[c] = 0;
+    uy[c] = 0;
+    if (c < C) {
+      const double u = pts[2 * ((size_t)c * N + n)], v = pts[2 * ((size_t)c * N + n) + 1];
+      double x = u, y = v;
+      if (undistort) omni_undistort(cam_at(cams, c), u, v, x, y);
+      ux[c] = x;
+      uy[c] = y;
+      if (!(x != x)) {
+        use |= 1u << c;
+        ++cnt;
+      }
+    }
+  }
+  double r[3] = {NAN, NAN, NAN};
+  if (cnt >= 2) dlt_point<MAXC>(cams, C, ux, uy, use, r);
+  out[3 * n] = r[0];
+  out[3 * n + 1] = r[1];
+  out[3 * n + 2] = r[2];
+}
+
+// CameraGroup.reprojection_error (cameras.py:746-783).
+__global__ void reproj_kernel(const double* __restrict__ cams, int C, const double* __restrict__ p3d,
+                              const double* __restrict__ p2d, int N, int mean, double* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const double X = p3d[3 * n], Y = p3d[3 * n + 1], Z = p3d[3 * n + 2];
+  double sum = 0.0, cnt = 0.0;
+  for (int c = 0; c < C; ++c) {
+    double u, v;
+    omni_project(cam_at(cams, c), X, Y, Z, u, v);
+    const size_t o = 2 * ((size_t)c * N + n);
+    const double ex = p2d[o] - u, ey = p2d[o + 1] - v;
+    if (!mean) {
+      out[o] = ex;
+      out[o + 1] = ey;
+    } else {
+      const double nr = sqrt(ex * ex + ey * ey);
+      if (!(nr != nr)) {
+        sum = sum + nr;
+        cnt = cnt + 1.0;
+      }
+    }
+  }
+  if (mean) out[n] = (cnt < 1.5) ? NAN : sum / cnt;
+}
+
+// triangulate_ransac -> triangulate_possible (cameras.py:639-743), n_possible = 1.
+// One wave per point; lanes walk the itertools.product order (bit m-1-i of the
+// subset index = "camera position i dropped") 64 subsets at a time and stop at
+// the first chunk holding an error < threshold, which reproduces the serial
+// early exit exactly; otherwise the first strict minimum below 200 wins.
+template <int MAXC>
+__global__ __launch_bounds__(64) void ransac_kernel(const double* __restrict__ cams, int C,
+                                                    const double* __restrict__ pts, int N, int min_cams,
+                                                    double threshold, double* __restrict__ out_p3d,
+                                                    uint8_t* __restrict__ out_picked, double* __restrict__ out_p2d,
+                                                    double* __restrict__ out_err) {
+  const int n = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (n >= N) return;
+  double raw_u[MAXC], raw_v[MAXC], ux[MAXC], uy[MAXC];
+  int pos2cam[MAXC];
+  int m = 0;
+  unsigned und_ok = 0;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    raw_u[c] = raw_v[c] = ux[c] = uy[c] = 0;
+    if (c < C) {
+      const size_t o = 2 * ((size_t)c * N + n);
+      raw_u[c] = pts[o];
+      raw_v[c] = pts[o + 1];
+      if (!(raw_u[c] != raw_u[c])) {
+        omni_undistort(cam_at(cams, c), raw_u[c], raw_v[c], ux[c], uy[c]);
+        if (!(ux[c] != ux[c])) und_ok |= 1u << c;
+        pos2cam[m] = c;
+        ++m;
+      }
+    }
+  }
+  const int nsub = 1 << m;
+  int chosen = -1;
+  double best_err = 200.0;
+  int best_s = 0x7fffffff;
+  if (m >= 2) {
+    for (int base = 0; base < nsub; base += 64) {
+      const int s = base + lane;
+      double err = NAN;
+      if (s < nsub) {
+        unsigned use = 0;
+        int k = 0;
+        for (int i = 0; i < m; ++i)
+          if (!((s >> (m - 1 - i)) & 1)) {
+            use |= 1u << pos2cam[i];
+            ++k;
+          }
+        if (!(k < min_cams && k != m) && k >= 2) {
+          double p[3] = {NAN, NAN, NAN};
+          if (__popc(use & und_ok) >= 2) dlt_point<MAXC>(cams, C, ux, uy, use & und_ok, p);
+          double sum = 0.0, cnt = 0.0;
+          for (int c = 0; c < C; ++c) {
+            if (!((use >> c) & 1u)) continue;
+            double u, v;
+            omni_project(cam_at(cams, c), p[0], p[1], p[2], u, v);
+            const double ex = raw_u[c] - u, ey = raw_v[c] - v;
+            const double nr = sqrt(ex * ex + ey * ey);
+            if (!(nr != nr)) {
+              sum = sum + nr;
+              cnt = cnt + 1.0;
+            }
+          }
+          err = (cnt < 1.5) ? NAN : sum / cnt;
+        }
+      }
+      // first subset (smallest s) in this chunk with err < threshold
+      const bool hit = err < threshold;
+      const unsigned long long hits = __ballot(hit);
+      if (hits) {
+        chosen = base + __ffsll((long long)hits) - 1;
+        break;
+      }
+      // running strict minimum, ties keep the earlier subset
+      double e = (err < 200.0) ? err : INFINITY;
+      int es = (err < 200.0) ? s : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double e2 = __shfl_xor(e, o, 64);
+        const int s2 = __shfl_xor(es, o, 64);
+        if (e2 < e || (e2 == e && s2 < es)) {
+          e = e2;
+          es = s2;
+        }
+      }
+      if (es != 0x7fffffff && (e < best_err || (e == best_err && es < best_s))) {
+        best_err = e;
+        best_s = es;
+      }
+    }
+    if (chosen < 0 && best_s != 0x7fffffff) chosen = best_s;
+  }
+  if (lane != 0) return;
+  double p[3] = {NAN, NAN, NAN};
+  double err = 0.0;
+  unsigned use = 0;
+  if (chosen >= 0) {
+    for (int i = 0; i < m; ++i)
+      if (!((chosen >> (m - 1 - i)) & 1)) use |= 1u << pos2cam[i];
+    if (__popc(use & und_ok) >= 2) dlt_point<MAXC>(cams, C, ux, uy, use & und_ok, p);
+    double sum = 0.0, cnt = 0.0;
+    for (int c = 0; c < C; ++c) {
+      if (!((use >> c) & 1u)) continue;
+      double u, v;
+      omni_project(cam_at(cams, c), p[0], p[1], p[2], u, v);
+      const double ex = raw_u[c] - u, ey = raw_v[c] - v;
+      const double nr = sqrt(ex * ex + ey * ey);
+      if (!(nr != nr)) {
+        sum = sum + nr;
+        cnt = cnt + 1.0;
+      }
+    }
+    err = (cnt < 1.5) ? NAN : sum / cnt;
+  }
+  out_p3d[3 * n] = p[0];
+  out_p3d[3 * n + 1] = p[1];
+  out_p3d[3 * n + 2] = p[2];
+  out_err[n] = err;
+  for (int c = 0; c < C; ++c) {
+    const bool on = (use >> c) & 1u;
+    out_picked[(size_t)c * N + n] = on ? 1 : 0;
+    out_p2d[2 * ((size_t)c * N + n)] = on ? raw_u[c] : NAN;
+    out_p2d[2 * ((size_t)c * N + n) + 1] = on ? raw_v[c] : NAN;
+  }
+}
+
+// mvpose inhomogeneous DLT (multicam_toolbox.py:433-486): X = pinv(A[:, :3]) A[:, 3], P = -X.
+template <int MAXC>
+__global__ void pinv_dlt_kernel(const double* __restrict__ cams, int C, const double* __restrict__ und,
+                                const uint8_t* __restrict__ use_mask, int N, double* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  double a[3][2 * MAXC], b[2 * MAXC];
+  int cnt = 0;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    bool on = false;
+    double x = 0, y = 0;
+    if (c < C) {
+      on = use_mask[(size_t)n * C + c] != 0;
+      x = und[2 * ((size_t)c * N + n)];
+      y = und[2 * ((size_t)c * N + n) + 1];
+    }
+    if (on) {
+      ++cnt;
+      const CamParams& cp = cam_at(cams, c);
+      const double P0[4] = {cp.R[0], cp.R[1], cp.R[2], cp.t[0]};
+      const double P1[4] = {cp.R[3], cp.R[4], cp.R[5], cp.t[1]};
+      const double P2[4] = {cp.R[6], cp.R[7], cp.R[8], cp.t[2]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        a[k][2 * c] = x * P2[k] - P0[k];
+        a[k][2 * c + 1] = y * P2[k] - P1[k];
+      }
+      b[2 * c] = x * P2[3] - P0[3];
+      b[2 * c + 1] = y * P2[3] - P1[3];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) a[k][2 * c] = a[k][2 * c + 1] = 0.0;
+      b[2 * c] = b[2 * c + 1] = 0.0;
+    }
+  }
+  if (cnt < 2) {
+    out[3 * n] = out[3 * n + 1] = out[3 * n + 2] = NAN;
+    return;
+  }
+  double V[3][3], sig[3];
+  jacobi_svd<2 * MAXC, 3>(a, V, sig);
+  const double smax = fmax(fmax(sig[0], sig[1]), sig[2]);
+  double X[3] = {0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (sig[j] > 1e-15 * smax) {
+      double ub = 0;
+#pragma unroll
+      for (int i = 0; i < 2 * MAXC; ++i) ub += a[j][i] * b[i];
+      const double w = ub / (sig[j] * sig[j]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) X[k] += V[j][k] * w;
+    }
+  }
+  out[3 * n] = -X[0];
+  out[3 * n + 1] = -X[1];
+  out[3 * n + 2] = -X[2];
+}
+
+// ------------------------------------------------------------------ Viterbi (filter_pose.py:48-186)
+// scipy log_ndtr (Faddeeva form): x < -1: log(erfcx(-t)/2) - t^2, else log1p(-erfc(t)/2), t = x/sqrt(2),
+// erfc(t) = exp(-t^2) erfcx(t) (t >= 0) or 2 - exp(-t^2) erfcx(-t).
+__device__ __forceinline__ double log_ndtr_d(double x) {
+  const double t = x * 0.70710678118654752440;
+  if (x < -1.0) return log(erfcx(-t) / 2) - t * t;
+  const double e = (t < 0) ? (2. - exp(-t * t) * erfcx(-t)) : exp(-t * t) * erfcx(t);
+  return log1p(-e / 2);
+}
+
+// log(Phi((d+2)/s) - Phi((d-2)/s)) evaluated as scipy's logsumexp(b=[1,-1]) does, clamped at -100.
+__device__ __forceinline__ double trans_logprob(double d, double thres) {
+  const double hi = log_ndtr_d((d + 2) / thres);
+  const double lo = log_ndtr_d((d - 2) / thres);
+  double r;
+  if (hi > lo) {
+    r = log1p(-exp(lo - hi)) + hi;
+  } else if (hi == lo) {
+    r = -INFINITY;
+  } else {
+    r = NAN;
+  }
+  if (r < -100) r = -100;
+  return r;
+}
+
+// One thread per chain (animal, camera, joint): kp (A,F,C,J,3) -> filtered (A,F,C,J,3).
+__global__ void viterbi_kernel(const double* __restrict__ kp, int A, int F, int C, int J, double score_thr,
+                               int n_back, double thres_dist, int8_t* __restrict__ back, double* __restrict__ out) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= A * C * J) return;
+  const int j = ch % J, c = (ch / J) % C, a = ch / (J * C);
+  auto at = [&](int f) -> const double* { return kp + ((((size_t)a * F + f) * C + c) * J + j) * 3; };
+  auto valid = [&](int f) -> bool {
+    const double* p = at(f);
+    const bool masked = p[2] < score_thr;  // points_full[scores < thr] = NaN
+    return !masked && !(p[0] != p[0]);
+  };
+  // particles of frame i: (x, y, score * 2^-jj) for valid frames i-jj, jj < n_back
+  auto particles = [&](int i, double (&px)[8], double (&py)[8], double (&ps)[8]) -> int {
+    int s = 0;
+    double w = 1.0;
+    for (int jj = 0; jj < n_back && jj < 8; ++jj) {
+      if (i - jj < 0) break;
+      if (valid(i - jj)) {
+        const double* p = at(i - jj);
+        px[s] = p[0];
+        py[s] = p[1];
+        ps[s] = p[2] * w;
+        ++s;
+      }
+      w = w * 0.5;
+    }
+    if (s == 0) {
+      px[0] = -1;
+      py[0] = -1;
+      ps[0] = 0.001;
+      s = 1;
+    }
+    return s;
+  };
+  int8_t* bk = back + (size_t)ch * F * 8;
+  double ax[8], ay[8], as[8], bx[8], by[8], bs[8];
+  double Tp[8], Tc[8];
+  int va = particles(0, ax, ay, as);
+  for (int p = 0; p < va; ++p) Tp[p] = log(as[p]);
+  const double lmiss = log(0.001);
+  for (int i = 1; i < F; ++i) {
+    const int vb = particles(i, bx, by, bs);
+    for (int q = 0; q < vb; ++q) {
+      double best = -INFINITY;
+      int arg = 0;
+      for (int p = 0; p < va; ++p) {
+        double P;
+        if (bx[q] == -1 || ax[p] == -1) {
+          P = lmiss;
+        } else {
+          const double dx = ax[p] - bx[q], dy = ay[p] - by[q];
+          P = trans_logprob(sqrt(dx * dx + dy * dy), thres_dist);
+        }
+        const double v = Tp[p] + P;
+        // np.max / np.argmax semantics: first maximum, a NaN wins and sticks
+        if (p == 0) {
+          best = v;
+          arg = 0;
+        } else if (!(best != best) && ((v != v) || v > best)) {
+          best = v;
+          arg = p;
+        }
+      }
+      Tc[q] = best + log(bs[q]);
+      bk[(size_t)i * 8 + q] = (int8_t)arg;
+    }
+    for (int q = 0; q < vb; ++q) {
+      Tp[q] = Tc[q];
+      ax[q] = bx[q];
+      ay[q] = by[q];
+      as[q] = bs[q];
+    }
+    va = vb;
+  }
+  // backtrack from the first argmax of the last frame
+  int cur = 0;
+  for (int p = 1; p < va; ++p)
+    if (Tp[p] > Tp[cur]) cur = p;
+  for (int i = F - 1; i >= 0; --i) {
+    double px[8], py[8], ps[8];
+    particles(i, px, py, ps);
+    double* o = out + ((((size_t)a * F + i) * C + c) * J + j) * 3;
+    o[0] = px[cur];
+    o[1] = py[cur];
+    o[2] = ps[cur];
+    if (i > 0) cur = bk[(size_t)i * 8 + cur];
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+int omnidir_undistort(const double* cams, int C, const double* pts, double* out, int N, hipStream_t s) {
+  const int tot = C * N;
+  if (tot <= 0) return 0;
+  hipLaunchKernelGGL(undistort_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, cams, C, pts, out, N);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int omnidir_project(const double* cams, int C, const double* p3d, double* out, int N, hipStream_t s) {
+  const int tot = C * N;
+  if (tot <= 0) return 0;
+  hipLaunchKernelGGL(project_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, cams, C, p3d, out, N);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int triangulate_dlt(const double* cams, int C, const double* pts, int N, int undistort, double* out, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (C <= 8)
+    hipLaunchKernelGGL(triangulate_kernel<8>, dim3((N + 63) / 64), dim3(64), 0, s, cams, C, pts, N, undistort, out);
+  else if (C <= 16)
+    hipLaunchKernelGGL(triangulate_kernel<16>, dim3((N + 63) / 64), dim3(64), 0, s, cams, C, pts, N, undistort, out);
+  else
+    return -2;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int reprojection_error(const double* cams, int C, const double* p3d, const double* p2d, int N, int mean, double* out,
+                       hipStream_t s) {
+  if (N <= 0) return 0;
+  hipLaunchKernelGGL(reproj_kernel, dim3((N + 127) / 128), dim3(128), 0, s, cams, C, p3d, p2d, N, mean, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int triangulate_ransac(const double* cams, int C, const double* pts, int N, int min_cams, double threshold,
+                       double* p3d, uint8_t* picked, double* p2d, double* err, hipStream_t s) {
+  if (N <= 0) return 0;
+  if (C <= 8)
+    hipLaunchKernelGGL(ransac_kernel<8>, dim3(N), dim3(64), 0, s, cams, C, pts, N, min_cams, threshold, p3d, picked,
+                       p2d, err);
+  else if (C <= 16)
+    hipLaunchKernelGGL(ransac_kernel<16>, dim3(N), dim3(64), 0, s, cams, C, pts, N, min_cams, threshold, p3d, picked,
+                       p2d, err);
+  else
+    return -2;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int triangulate_pinv(const double* cams, int C, const double* und, const uint8_t* use, int N, double* out,
+                     hipStream_t s) {
+  if (N <= 0) return 0;
+  if (C <= 8)
+    hipLaunchKernelGGL(pinv_dlt_kernel<8>, dim3((N + 63) / 64), dim3(64), 0, s, cams, C, und, use, N, out);
+  else if (C <= 16)
+    hipLaunchKernelGGL(pinv_dlt_kernel<16>, dim3((N + 63) / 64), dim3(64), 0, s, cams, C, und, use, N, out);
+  else
+    return -2;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int viterbi_filter(const double* kp, int A, int F, int C, int J, double score_thr, int n_back, double thres_dist,
+                   int8_t* back_scratch, double* out, hipStream_t s) {
+  const int chains = A * C * J;
+  if (chains <= 0 || F <= 0) return 0;
+  if (n_back > 8 || n_back < 1) return -2;
+  hipLaunchKernelGGL(viterbi_kernel, dim3((chains + 63) / 64), dim3(64), 0, s, kp, A, F, C, J, score_thr, n_back,
+                     thres_dist, back_scratch, out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace mq

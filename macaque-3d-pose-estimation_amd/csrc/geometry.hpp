@@ -1,0 +1,18 @@
+// Internal launchers of the float64 geometry kernels (geometry.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mq {
+int omnidir_undistort(const double* cams, int C, const double* pts, double* out, int N, hipStream_t s);
+int omnidir_project(const double* cams, int C, const double* p3d, double* out, int N, hipStream_t s);
+int triangulate_dlt(const double* cams, int C, const double* pts, int N, int undistort, double* out, hipStream_t s);
+int reprojection_error(const double* cams, int C, const double* p3d, const double* p2d, int N, int mean, double* out,
+                       hipStream_t s);
+int triangulate_ransac(const double* cams, int C, const double* pts, int N, int min_cams, double threshold,
+                       double* p3d, uint8_t* picked, double* p2d, double* err, hipStream_t s);
+int triangulate_pinv(const double* cams, int C, const double* und, const uint8_t* use, int N, double* out,
+                     hipStream_t s);
+int viterbi_filter(const double* kp, int A, int F, int C, int J, double score_thr, int n_back, double thres_dist,
+                   int8_t* back_scratch, double* out, hipStream_t s);
+}  // namespace mq

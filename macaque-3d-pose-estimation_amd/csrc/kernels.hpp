@@ -1,0 +1,51 @@
+// Internal launcher declarations of libmq_hip (not part of the public C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mq {
+
+enum GemmEpilogue {
+  EPI_BF16 = 0,       // C bf16 = acc + bias
+  EPI_GELU_BF16 = 1,  // C bf16 = gelu_erf(acc + bias)
+  EPI_RESID_F32 = 2,  // C f32 += acc + bias            (residual stream)
+  EPI_POS_F32 = 3,    // C f32 = acc + bias + aux[m % aux_rows][n]   (patch embed + pos_embed)
+  EPI_F32 = 4,        // C f32 = acc + bias
+  EPI_NCHW_F32 = 5,   // C f32 [m / aux_rows][n][m % aux_rows] = acc + bias (1x1 conv -> NCHW)
+};
+
+struct GemmArgs {
+  const unsigned short* A;  // [M][lda] bf16, K-contiguous
+  const unsigned short* W;  // [N][ldw] bf16, K-contiguous
+  void* C;
+  const float* bias;        // [N] or null
+  const float* aux;         // epilogue side input
+  int M, N, K;
+  int lda, ldw, ldc;
+  int aux_rows;
+};
+
+int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
+
+// ViT ops (vit_ops.hip)
+int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
+                       float eps, hipStream_t s);
+int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
+                   hipStream_t s);
+int patch_im2col(const float* crops, unsigned short* A, int n_crops, int flip_copies, int img_h, int img_w,
+                 int patch, int pad, hipStream_t s);
+int deconv_col2im_bn_relu(const unsigned short* cols, const float* scale, const float* shift, unsigned short* out,
+                          int n_img, int in_h, int in_w, int ch, hipStream_t s);
+int convert_f32_bf16(const float* src, unsigned short* dst, int64_t n, hipStream_t s);
+int deconv_weight_pack(const float* w, unsigned short* dst, int cin, int cout, hipStream_t s);
+
+// image ops (imgproc.hip)
+int crop_udp(const uint8_t* frames, int64_t frame_stride, int img_h, int img_w, const float* boxes,
+             const int32_t* box_frame, int n, float* crops, float* center, float* scale, hipStream_t s);
+int flip_average(const float* hm_all, float* avg, int n, int joints, int h, int w, const int32_t* flip_idx,
+                 hipStream_t s);
+int udp_decode(const float* avg, int n, int joints, int h, int w, const float* center, const float* scale,
+               int in_w, int in_h, float* work, double* kp_img, float* score, int32_t* argmax, float* kp_hm,
+               hipStream_t s);
+
+}  // namespace mq

@@ -1,0 +1,356 @@
+// ViT-side kernels for gfx950: LayerNorm, fused global attention (192 tokens,
+// K/V staged whole in LDS), patch im2col (+ flip-test copy), deconv col2im with
+// the eval BatchNorm + ReLU fused, and weight packing.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace mq {
+
+// ---------------------------------------------------------------- LayerNorm
+// One wave per row: fp32 residual stream in, bf16 normalised out (eps 1e-6).
+template <int MAXIT>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
+                                                         const float* __restrict__ b, bf16_t* __restrict__ y,
+                                                         int rows, int dim, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (size_t)row * dim;
+  float4 v[MAXIT];
+  float s = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    const int i = it * 256 + lane * 4;
+    if (i < dim) {
+      v[it] = *reinterpret_cast<const float4*>(xr + i);
+      s += (v[it].x + v[it].y) + (v[it].z + v[it].w);
+    } else {
+      v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const float mean = wave_sum(s) / (float)dim;
+  float q = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    const int i = it * 256 + lane * 4;
+    if (i < dim) {
+      float a0 = v[it].x - mean, a1 = v[it].y - mean, a2 = v[it].z - mean, a3 = v[it].w - mean;
+      q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)dim + eps);
+  bf16_t* yr = y + (size_t)row * dim;
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    const int i = it * 256 + lane * 4;
+    if (i < dim) {
+      const float4 gg = *reinterpret_cast<const float4*>(g + i);
+      const float4 bb = *reinterpret_cast<const float4*>(b + i);
+      uint2 o;
+      o.x = pack_bf16x2((v[it].x - mean) * rstd * gg.x + bb.x, (v[it].y - mean) * rstd * gg.y + bb.y);
+      o.y = pack_bf16x2((v[it].z - mean) * rstd * gg.z + bb.z, (v[it].w - mean) * rstd * gg.w + bb.w);
+      *reinterpret_cast<uint2*>(yr + i) = o;
+    }
+  }
+}
+
+int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
+                       float eps, hipStream_t s) {
+  if (dim % 4 || dim > 2048) return -1;
+  dim3 grid((rows + 3) / 4), block(256);
+  if (dim <= 1280)
+    hipLaunchKernelGGL(layernorm_kernel<5>, grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<8>, grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------- attention
+// One workgroup per (image, head).  K is staged row-major and V transposed in LDS
+// (T x DH each, <= 30 KB bf16 at T=192, DH=80).  Each wave takes 16-query blocks:
+//   S^T = K Q^T with v_mfma_f32_16x16x16_bf16 (query on the lane, tokens in regs),
+//   softmax over the 192 tokens = in-register reduction + 2 cross-lane steps,
+//   O = P V with v_mfma_f32_16x16x32_bf16; the accumulator S^T is re-used as the
+//   A operand of PV without going through LDS (k-slot permutation matched in V).
+template <int DH>
+__global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                         int T, int D, int H, float scale_log2) {
+  constexpr int KS = DH + 4;       // K row stride (elements)
+  constexpr int NKS = DH / 16;     // k-steps of QK^T
+  constexpr int MAXT = 192;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
+  const int VS = T + 8;  // Vt row stride
+  bf16_t* Vt = Ks + MAXT * KS;
+
+  const int img = blockIdx.x / H, h = blockIdx.x % H;
+  const size_t row0 = (size_t)img * T;
+  const int ld = 3 * D;
+  // stage K and V^T
+  for (int c = threadIdx.x; c < T * (DH / 8); c += blockDim.x) {
+    const int t = c / (DH / 8), ch = c % (DH / 8);
+    const bf16_t* src = qkv + (row0 + t) * ld + h * DH + ch * 8;
+    const uint4 kv = *reinterpret_cast<const uint4*>(src + D);
+    const uint4 vv = *reinterpret_cast<const uint4*>(src + 2 * D);
+    uint2* kd = reinterpret_cast<uint2*>(Ks + t * KS + ch * 8);
+    kd[0] = make_uint2(kv.x, kv.y);
+    kd[1] = make_uint2(kv.z, kv.w);
+    const unsigned vw[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      Vt[(ch * 8 + 2 * e) * VS + t] = (bf16_t)(vw[e] & 0xffff);
+      Vt[(ch * 8 + 2 * e + 1) * VS + t] = (bf16_t)(vw[e] >> 16);
+    }
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int ntb = T / 16;
+  for (int qb = wave; qb < T / 16; qb += 4) {
+    const int q = qb * 16 + l16;
+    short4v qf[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      qf[ks] = *reinterpret_cast<const short4v*>(qkv + (row0 + q) * ld + h * DH + ks * 16 + 4 * g);
+    f32x4 S[MAXT / 16];
+#pragma unroll
+    for (int tb = 0; tb < MAXT / 16; ++tb) {
+      S[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (tb < ntb) {
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const short4v kf = *reinterpret_cast<const short4v*>(Ks + (tb * 16 + l16) * KS + ks * 16 + 4 * g);
+          S[tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[ks], S[tb], 0, 0, 0);
+        }
+      }
+    }
+    // softmax over tokens for query q (column l16): values spread over regs and lanes g
+    float m = -INFINITY;
+#pragma unroll
+    for (int tb = 0; tb < MAXT / 16; ++tb)
+      if (tb < ntb) m = fmaxf(m, fmaxf(fmaxf(S[tb][0], S[tb][1]), fmaxf(S[tb][2], S[tb][3])));
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float mb = m * scale_log2;
+    float lsum = 0.f;
+#pragma unroll
+    for (int tb = 0; tb < MAXT / 16; ++tb) {
+      if (tb < ntb) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = exp2f(S[tb][e] * scale_log2 - mb);
+          S[tb][e] = p;
+          lsum += p;
+        }
+      }
+    }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+
+    f32x4 O[NKS];
+#pragma unroll
+    for (int dt = 0; dt < NKS; ++dt) O[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kst = 0; kst < MAXT / 32; ++kst) {
+      if (kst < T / 32) {
+        const int tb0 = 2 * kst;
+        bf16x8 pa;
+        pa[0] = (__bf16)S[tb0][0];
+        pa[1] = (__bf16)S[tb0][1];
+        pa[2] = (__bf16)S[tb0][2];
+        pa[3] = (__bf16)S[tb0][3];
+        pa[4] = (__bf16)S[tb0 + 1][0];
+        pa[5] = (__bf16)S[tb0 + 1][1];
+        pa[6] = (__bf16)S[tb0 + 1][2];
+        pa[7] = (__bf16)S[tb0 + 1][3];
+#pragma unroll
+        for (int dt = 0; dt < NKS; ++dt) {
+          const bf16_t* vrow = Vt + (dt * 16 + l16) * VS;
+          const uint2 v0 = *reinterpret_cast<const uint2*>(vrow + tb0 * 16 + 4 * g);
+          const uint2 v1 = *reinterpret_cast<const uint2*>(vrow + (tb0 + 1) * 16 + 4 * g);
+          const uint4 vv = make_uint4(v0.x, v0.y, v1.x, v1.y);
+          const bf16x8 vb = *reinterpret_cast<const bf16x8*>(&vv);
+          O[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, O[dt], 0, 0, 0);
+        }
+      }
+    }
+    // O C-layout: col = l16 -> d, row = 4g + e -> query; normaliser lives in lane (4g + e)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float inv = 1.0f / __shfl(lsum, 4 * g + e, 64);
+      const int qq = qb * 16 + 4 * g + e;
+      bf16_t* orow = out + (row0 + qq) * D + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = f32_to_bf16(O[dt][e] * inv);
+    }
+  }
+}
+
+int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
+                   hipStream_t s) {
+  const int dh = dim / heads;
+  if (tokens % 32 || tokens > 192 || dh * heads != dim) return -1;
+  const float scale_log2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
+  dim3 grid(n_img * heads), block(256);
+  if (dh == 80) {
+    const size_t lds = (192 * (80 + 4) + 80 * (tokens + 8)) * 2;
+    hipLaunchKernelGGL(attention_kernel<80>, grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+  } else if (dh == 64) {
+    const size_t lds = (192 * (64 + 4) + 64 * (tokens + 8)) * 2;
+    hipLaunchKernelGGL(attention_kernel<64>, grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+  } else {
+    return -2;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// ---------------------------------------------------------------- patch im2col
+// A[(f*T + t)][ci*P*P + ky*P + kx] = crop[f % n][ci][py*P + ky - pad][px*P + kx - pad]
+// (zero outside); forwards f >= n read the horizontally flipped crop (flip test).
+__global__ void patch_im2col_kernel(const float* __restrict__ crops, bf16_t* __restrict__ A, int n, int copies,
+                                    int IH, int IW, int P, int pad, int gh, int gw) {
+  const int K = 3 * P * P;
+  const int k8 = K / 8;
+  const int64_t total = (int64_t)n * copies * gh * gw * k8;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int kc = (int)(idx % k8);
+    const int64_t m = idx / k8;
+    const int t = (int)(m % (gh * gw));
+    const int f = (int)(m / (gh * gw));
+    const int src = f % n;
+    const bool flip = f >= n;
+    const int py = t / gw, px = t % gw;
+    const int k0 = kc * 8;
+    const int ci = k0 / (P * P);
+    const int ky = (k0 / P) % P;
+    const int kx0 = k0 % P;
+    const int y = py * P + ky - pad;
+    const float* plane = crops + ((int64_t)src * 3 + ci) * IH * IW;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      int x = px * P + kx0 + e - pad;
+      bool ok = (y >= 0) && (y < IH) && (x >= 0) && (x < IW);
+      int xs = flip ? (IW - 1 - x) : x;
+      v[e] = ok ? plane[(int64_t)y * IW + xs] : 0.f;
+    }
+    uint4 o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                         pack_bf16x2(v[6], v[7]));
+    *reinterpret_cast<uint4*>(A + m * K + k0) = o;
+  }
+}
+
+int patch_im2col(const float* crops, unsigned short* A, int n_crops, int flip_copies, int img_h, int img_w, int patch,
+                 int pad, hipStream_t s) {
+  if ((patch * patch) % 8) return -1;
+  const int gh = (img_h + 2 * pad - patch) / patch + 1;
+  const int gw = (img_w + 2 * pad - patch) / patch + 1;
+  const int64_t total = (int64_t)n_crops * flip_copies * gh * gw * (3 * patch * patch / 8);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(patch_im2col_kernel, dim3(blocks), dim3(256), 0, s, crops, A, n_crops, flip_copies, img_h, img_w,
+                     patch, pad, gh, gw);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------- deconv col2im
+// ConvTranspose2d(k4, s2, p1) as GEMM + gather: cols[(img,iy,ix)][(ky*4+kx)*C + co].
+// out[(img,oy,ox)][co] = relu(scale[co] * sum_{valid taps} cols + shift[co]),  NHWC bf16.
+__global__ void col2im_bn_relu_kernel(const bf16_t* __restrict__ cols, const float* __restrict__ scale,
+                                      const float* __restrict__ shift, bf16_t* __restrict__ out, int n, int IH,
+                                      int IW, int C) {
+  const int OH = IH * 2, OW = IW * 2;
+  const int c8 = C / 8;
+  const int64_t total = (int64_t)n * OH * OW * c8;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(idx % c8);
+    const int64_t pix = idx / c8;
+    const int ox = (int)(pix % OW);
+    const int oy = (int)((pix / OW) % OH);
+    const int img = (int)(pix / ((int64_t)OW * OH));
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    // oy = 2*iy - 1 + ky
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int ky = ((oy + 1) & 1) + 2 * a;
+      const int ty = oy + 1 - ky;
+      const int iy = ty >> 1;
+      if (iy < 0 || iy >= IH) continue;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int kx = ((ox + 1) & 1) + 2 * b;
+        const int tx = ox + 1 - kx;
+        const int ix = tx >> 1;
+        if (ix < 0 || ix >= IW) continue;
+        const bf16_t* src = cols + (((int64_t)img * IH + iy) * IW + ix) * (16 * C) + (ky * 4 + kx) * C + cc * 8;
+        const uint4 u = *reinterpret_cast<const uint4*>(src);
+        const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] += bf16_to_f32((bf16_t)(w[e] & 0xffff));
+          acc[2 * e + 1] += bf16_to_f32((bf16_t)(w[e] >> 16));
+        }
+      }
+    }
+    float r[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = cc * 8 + e;
+      r[e] = fmaxf(acc[e] * scale[c] + shift[c], 0.f);
+    }
+    uint4 o = make_uint4(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]), pack_bf16x2(r[4], r[5]),
+                         pack_bf16x2(r[6], r[7]));
+    *reinterpret_cast<uint4*>(out + pix * C + cc * 8) = o;
+  }
+}
+
+int deconv_col2im_bn_relu(const unsigned short* cols, const float* scale, const float* shift, unsigned short* out,
+                          int n_img, int in_h, int in_w, int ch, hipStream_t s) {
+  if (ch % 8) return -1;
+  const int64_t total = (int64_t)n_img * in_h * 2 * in_w * 2 * (ch / 8);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(col2im_bn_relu_kernel, dim3(blocks), dim3(256), 0, s, cols, scale, shift, out, n_img, in_h, in_w,
+                     ch);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+// ---------------------------------------------------------------- weight packing
+__global__ void f32_to_bf16_kernel(const float* __restrict__ src, bf16_t* __restrict__ dst, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = f32_to_bf16(src[i]);
+}
+
+int convert_f32_bf16(const float* src, unsigned short* dst, int64_t n, hipStream_t s) {
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(blocks), dim3(256), 0, s, src, dst, n);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// torch ConvTranspose2d weight [cin][cout][4][4] -> GEMM rows [(ky*4+kx)*cout + co][cin]
+__global__ void deconv_pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ dst, int cin, int cout) {
+  const int64_t total = (int64_t)cin * cout * 16;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cin);
+    const int64_t n = i / cin;
+    const int co = (int)(n % cout);
+    const int kk = (int)(n / cout);
+    dst[i] = f32_to_bf16(w[((int64_t)ci * cout + co) * 16 + kk]);
+  }
+}
+
+int deconv_weight_pack(const float* w, unsigned short* dst, int cin, int cout, hipStream_t s) {
+  const int64_t total = (int64_t)cin * cout * 16;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(deconv_pack_kernel, dim3(blocks), dim3(256), 0, s, w, dst, cin, cout);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace mq

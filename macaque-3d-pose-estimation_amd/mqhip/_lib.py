@@ -1,0 +1,130 @@
+"""ctypes binding of libmq_hip.so (include/mq_hip.h).
+
+The shared library is built in-tree (``macaque-3d-pose-estimation_amd/lib/``) by
+``__graft_entry__.build()`` / ``make -C macaque-3d-pose-estimation_amd/csrc``.
+There is no CPU fallback: if the library or a GPU is missing, every product call
+raises ``MqError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmq_hip.so"))
+
+EXPORTED = [
+    "mq_abi_version", "mq_last_error", "mq_create", "mq_destroy",
+    "mq_vitpose_create", "mq_vitpose_destroy", "mq_vitpose_set_param", "mq_vitpose_finalize",
+    "mq_vitpose_set_graph", "mq_vitpose_timing", "mq_vitpose_timing_result", "mq_crop_udp", "mq_vitpose_forward", "mq_decode_udp", "mq_topdown",
+    "mq_omnidir_undistort", "mq_omnidir_project", "mq_triangulate_dlt", "mq_reproj_error",
+    "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_viterbi_filter",
+]
+
+
+class MqError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+vp = C.c_void_p
+i32 = C.c_int
+i64 = C.c_int64
+f64 = C.c_double
+
+_SIGS = {
+    "mq_abi_version": (i32, []),
+    "mq_last_error": (C.c_char_p, []),
+    "mq_create": (i32, [i32, C.POINTER(vp)]),
+    "mq_destroy": (i32, [vp]),
+    "mq_vitpose_create": (i32, [vp, i32, i32, i32, i32, i32, C.POINTER(vp)]),
+    "mq_vitpose_destroy": (i32, [vp]),
+    "mq_vitpose_set_param": (i32, [vp, C.c_char_p, vp, i64, i32]),
+    "mq_vitpose_finalize": (i32, [vp]),
+    "mq_vitpose_set_graph": (i32, [vp, i32]),
+    "mq_vitpose_timing": (i32, [vp, i32]),
+    "mq_vitpose_timing_result": (i32, [vp, C.POINTER(f64), C.POINTER(i32), C.POINTER(i64)]),
+    "mq_crop_udp": (i32, [vp, vp, i64, i32, i32, vp, vp, i32, vp, vp, vp, vp]),
+    "mq_vitpose_forward": (i32, [vp, vp, i32, i32, vp, vp]),
+    "mq_decode_udp": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "mq_topdown": (i32, [vp, vp, i64, i32, i32, vp, vp, i32, i32, vp, vp, vp, vp, vp]),
+    "mq_omnidir_undistort": (i32, [vp, vp, i32, vp, i32, vp, vp]),
+    "mq_omnidir_project": (i32, [vp, vp, i32, vp, i32, vp, vp]),
+    "mq_triangulate_dlt": (i32, [vp, vp, i32, vp, i32, i32, vp, vp]),
+    "mq_reproj_error": (i32, [vp, vp, i32, vp, vp, i32, i32, vp, vp]),
+    "mq_triangulate_ransac": (i32, [vp, vp, i32, vp, i32, i32, f64, vp, vp, vp, vp, vp]),
+    "mq_triangulate_pinv": (i32, [vp, vp, i32, vp, vp, i32, vp, vp]),
+    "mq_viterbi_filter": (i32, [vp, vp, i32, i32, i32, i32, f64, i32, f64, vp, vp]),
+}
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and return the ctypes library with every signature bound."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise MqError(f"libmq_hip.so not found at {path}: run __graft_entry__.build() "
+                          f"or `make -C macaque-3d-pose-estimation_amd/csrc` first")
+        lib = C.CDLL(path)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.mq_abi_version() != 1:
+            raise MqError("libmq_hip ABI version mismatch")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.mq_last_error().decode() if _lib is not None else "?"
+        raise MqError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Raw device/host pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Context:
+    """One mq_ctx per device (threading)."""
+
+    _per_device: dict = {}
+
+    def __init__(self, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise MqError("no HIP device visible: the MI355X path has no CPU fallback")
+        self.lib = load()
+        self.device = device
+        h = C.c_void_p()
+        check(self.lib.mq_create(device, C.byref(h)), "mq_create")
+        self.handle = h
+
+    @classmethod
+    def get(cls, device: int = 0) -> "Context":
+        ctx = cls._per_device.get(device)
+        if ctx is None:
+            ctx = cls(device)
+            cls._per_device[device] = ctx
+        return ctx
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None) is not None and _lib is not None:
+                _lib.mq_destroy(self.handle)
+        except Exception:
+            pass

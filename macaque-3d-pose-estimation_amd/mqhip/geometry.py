@@ -1,0 +1,260 @@
+"""Multi-view geometry on MI355X: the aniposelib ``CameraGroup`` surface used by step 4.
+
+Mirrors ``/root/reference/src/third_party/aniposelib/cameras.py`` (OmnidirCamera
+:429-555, CameraGroup :557-2017) for the calls step 4 makes
+(``src/pipeline/step4_aniposefiltering.py``:212-291): ``load``,
+``subset_cameras_names``, ``triangulate``, ``triangulate_ransac``,
+``reprojection_error``, ``project``, ``optim_points``.  Inputs/outputs are numpy
+float64 like the reference; the arithmetic runs in libmq_hip (float64 HIP kernels).
+Shape errors raise AssertionError and unknown camera names IndexError, as in the
+reference.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def rodrigues(rvec):
+    """cv2.Rodrigues(rvec) (host-side parameter packing only)."""
+    r = np.asarray(rvec, dtype=np.float64).ravel()
+    th = np.sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2])
+    if th < np.finfo(np.float64).eps:
+        return np.eye(3)
+    c, s = np.cos(th), np.sin(th)
+    c1 = 1.0 - c
+    it = 1.0 / th
+    x, y, z = r[0] * it, r[1] * it, r[2] * it
+    return np.array([[c + c1 * x * x, c1 * x * y - s * z, c1 * x * z + s * y],
+                     [c1 * x * y + s * z, c + c1 * y * y, c1 * y * z - s * x],
+                     [c1 * x * z - s * y, c1 * y * z + s * x, c + c1 * z * z]])
+
+
+class OmnidirCamera:
+    """Parameter holder with the OmnidirCamera field names (cameras.py:429-470)."""
+
+    def __init__(self, matrix=None, dist=None, size=None, rvec=None, tvec=None, xi=None, K=None, D=None,
+                 name=None):
+        self.matrix = np.eye(3) if matrix is None else np.asarray(matrix, dtype=np.float64)
+        self.dist = np.zeros(4) if dist is None else np.asarray(dist, dtype=np.float64).ravel()
+        self.size = size
+        self.rvec = np.zeros(3) if rvec is None else np.asarray(rvec, dtype=np.float64).ravel()
+        self.tvec = np.zeros(3) if tvec is None else np.asarray(tvec, dtype=np.float64).ravel()
+        self.xi = np.zeros(1) if xi is None else np.asarray(xi, dtype=np.float64).ravel()
+        self.K = np.zeros((3, 3)) if K is None else np.asarray(K, dtype=np.float64)
+        self.D = np.zeros(4) if D is None else np.asarray(D, dtype=np.float64).ravel()
+        self.name = None if name is None else str(name)
+
+    @staticmethod
+    def from_dict(d):
+        return OmnidirCamera(matrix=d.get("matrix"), dist=d.get("distortions"), size=d.get("size"),
+                             rvec=d.get("rotation", d.get("rvec")), tvec=d.get("translation", d.get("tvec")),
+                             xi=d.get("xi"), K=d.get("K"), D=d.get("D"), name=d.get("name"))
+
+    def get_name(self):
+        return self.name
+
+    def get_extrinsics_mat(self):
+        M = np.eye(4)
+        M[:3, :3] = rodrigues(self.rvec)
+        M[:3, 3] = self.tvec
+        return M
+
+    def param_row(self):
+        row = np.zeros(24)
+        row[0:6] = [self.K[0, 0], self.K[1, 1], self.K[0, 1], self.K[0, 2], self.K[1, 2], float(self.xi[0])]
+        row[6:10] = self.D[:4]
+        row[10:19] = rodrigues(self.rvec).ravel()
+        row[19:22] = self.tvec[:3]
+        return row
+
+
+class CameraGroup:
+    def __init__(self, cameras, metadata=None, device: int = 0):
+        self.cameras = list(cameras)
+        self.metadata = {} if metadata is None else metadata
+        self.device = device
+        self._cams_dev = None
+
+    # ------------------------------------------------------------------ construction
+    @staticmethod
+    def from_dicts(arr, device: int = 0):
+        return CameraGroup([OmnidirCamera.from_dict(d) for d in arr], device=device)
+
+    @staticmethod
+    def load(path, device: int = 0):
+        """cameras.py:1995-2013 (TOML calibration; omnidir cameras)."""
+        try:
+            import tomllib as _toml  # py >= 3.11
+        except ImportError:  # pragma: no cover - py3.10 image
+            import tomli as _toml
+        with open(path, "rb") as f:
+            master = _toml.load(f)
+        keys = sorted([k for k in master.keys() if k != "metadata"])
+        items = [master[k] for k in keys]
+        g = CameraGroup.from_dicts(items, device=device)
+        g.metadata = master.get("metadata", {})
+        return g
+
+    def get_names(self):
+        return [c.get_name() for c in self.cameras]
+
+    def subset_cameras(self, indices):
+        return CameraGroup([self.cameras[i] for i in indices], self.metadata, self.device)
+
+    def subset_cameras_names(self, names):
+        cur = self.get_names()
+        d = dict(zip(cur, range(len(cur))))
+        idx = []
+        for n in names:
+            if n not in d:
+                raise IndexError("name {} not part of camera names: {}".format(n, cur))
+            idx.append(d[n])
+        return self.subset_cameras(idx)
+
+    # ------------------------------------------------------------------ device plumbing
+    def _dev(self):
+        return torch.device("cuda", self.device)
+
+    def cams_tensor(self):
+        if self._cams_dev is None:
+            rows = np.stack([c.param_row() for c in self.cameras])
+            self._cams_dev = torch.from_numpy(rows).to(self._dev())
+        return self._cams_dev
+
+    def _ctx(self):
+        return _lib.Context.get(self.device)
+
+    def _to_dev(self, a):
+        return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(self._dev())
+
+    # ------------------------------------------------------------------ API
+    def project(self, points):
+        """Nx3 -> CxNx2 (cameras.py:573-584)."""
+        p = np.asarray(points, dtype=np.float64).reshape(-1, 3)
+        n, C = p.shape[0], len(self.cameras)
+        ctx = self._ctx()
+        out = torch.empty((C, n, 2), dtype=torch.float64, device=self._dev())
+        p_d = self._to_dev(p)  # keep device temporaries alive until the call is enqueued
+        _lib.check(ctx.lib.mq_omnidir_project(ctx.handle, _lib.ptr(self.cams_tensor()), C, _lib.ptr(p_d),
+                                              n, _lib.ptr(out), _lib.stream_ptr(self._dev())), "mq_omnidir_project")
+        return out.cpu().numpy()
+
+    def undistort_points(self, points):
+        pts = np.asarray(points, dtype=np.float64)
+        C = len(self.cameras)
+        assert pts.shape[0] == C
+        shape = pts.shape
+        flat = pts.reshape(C, -1, 2)
+        n = flat.shape[1]
+        ctx = self._ctx()
+        out = torch.empty((C, n, 2), dtype=torch.float64, device=self._dev())
+        flat_d = self._to_dev(flat)
+        _lib.check(ctx.lib.mq_omnidir_undistort(ctx.handle, _lib.ptr(self.cams_tensor()), C,
+                                                _lib.ptr(flat_d), n, _lib.ptr(out),
+                                                _lib.stream_ptr(self._dev())), "mq_omnidir_undistort")
+        return out.cpu().numpy().reshape(shape)
+
+    def triangulate(self, points, undistort=True, progress=False):
+        """CxNx2 -> Nx3 (cameras.py:593-637)."""
+        assert points.shape[0] == len(self.cameras), \
+            "Invalid points shape, first dim should be equal to" \
+            " number of cameras ({}), but shape is {}".format(len(self.cameras), points.shape)
+        one_point = False
+        if len(points.shape) == 2:
+            points = points.reshape(-1, 1, 2)
+            one_point = True
+        C, n, _ = points.shape
+        ctx = self._ctx()
+        out = torch.empty((n, 3), dtype=torch.float64, device=self._dev())
+        pts_d = self._to_dev(points)
+        _lib.check(ctx.lib.mq_triangulate_dlt(ctx.handle, _lib.ptr(self.cams_tensor()), C,
+                                              _lib.ptr(pts_d), n, 1 if undistort else 0, _lib.ptr(out),
+                                              _lib.stream_ptr(self._dev())), "mq_triangulate_dlt")
+        res = out.cpu().numpy()
+        return res[0] if one_point else res
+
+    def triangulate_ransac(self, points, undistort=True, min_cams=2, progress=False, threshold=0.5):
+        """CxNx2 -> (p3d Nx3, picked CxNx1, p2ds CxNx2, errors N) (cameras.py:639-743)."""
+        assert points.shape[0] == len(self.cameras), \
+            "Invalid points shape, first dim should be equal to" \
+            " number of cameras ({}), but shape is {}".format(len(self.cameras), points.shape)
+        if not undistort:
+            raise NotImplementedError("triangulate_ransac(undistort=False) is not on the reference's path")
+        C, n, _ = points.shape
+        ctx = self._ctx()
+        dev = self._dev()
+        p3d = torch.empty((n, 3), dtype=torch.float64, device=dev)
+        picked = torch.empty((C, n), dtype=torch.uint8, device=dev)
+        p2d = torch.empty((C, n, 2), dtype=torch.float64, device=dev)
+        err = torch.empty((n,), dtype=torch.float64, device=dev)
+        pts_d = self._to_dev(points)
+        _lib.check(ctx.lib.mq_triangulate_ransac(ctx.handle, _lib.ptr(self.cams_tensor()), C,
+                                                 _lib.ptr(pts_d), n, int(min_cams), float(threshold),
+                                                 _lib.ptr(p3d), _lib.ptr(picked), _lib.ptr(p2d), _lib.ptr(err),
+                                                 _lib.stream_ptr(dev)), "mq_triangulate_ransac")
+        return (p3d.cpu().numpy(), picked.cpu().numpy().astype(bool).reshape(C, n, 1), p2d.cpu().numpy(),
+                err.cpu().numpy())
+
+    def reprojection_error(self, p3ds, p2ds, mean=False):
+        """cameras.py:746-783."""
+        one_point = False
+        if len(p3ds.shape) == 1 and len(p2ds.shape) == 2:
+            p3ds = p3ds.reshape(1, 3)
+            p2ds = p2ds.reshape(-1, 1, 2)
+            one_point = True
+        C, n, _ = p2ds.shape
+        assert p3ds.shape == (n, 3), \
+            "shapes of 2D and 3D points are not consistent: 2D={}, 3D={}".format(p2ds.shape, p3ds.shape)
+        ctx = self._ctx()
+        dev = self._dev()
+        out = torch.empty((n,) if mean else (C, n, 2), dtype=torch.float64, device=dev)
+        p3_d, p2_d = self._to_dev(p3ds), self._to_dev(p2ds)
+        _lib.check(ctx.lib.mq_reproj_error(ctx.handle, _lib.ptr(self.cams_tensor()), C, _lib.ptr(p3_d),
+                                           _lib.ptr(p2_d), n, 1 if mean else 0, _lib.ptr(out),
+                                           _lib.stream_ptr(dev)), "mq_reproj_error")
+        errors = out.cpu().numpy()
+        if one_point:
+            errors = float(errors[0]) if mean else errors.reshape(-1, 2)
+        return errors
+
+    def optim_points(self, points, p3ds, constraints=(), constraints_weak=(), scale_smooth=4, scale_length=2,
+                     scale_length_weak=0.5, reproj_error_threshold=15, reproj_loss='soft_l1', n_deriv_smooth=1,
+                     scores=None, verbose=False):
+        """cameras.py:1116-1190 on the GPU (see mqhip.optim)."""
+        from .optim import optim_points_gpu
+        return optim_points_gpu(self, points, p3ds, constraints=constraints, constraints_weak=constraints_weak,
+                                scale_smooth=scale_smooth, scale_length=scale_length,
+                                scale_length_weak=scale_length_weak, reproj_error_threshold=reproj_error_threshold,
+                                reproj_loss=reproj_loss, n_deriv_smooth=n_deriv_smooth, verbose=verbose)
+
+
+def triangulate_pinv(cams: CameraGroup, und, frame_use):
+    """multicam_toolbox.triangulatePoints on the GPU: und (C,N,2) undistorted, frame_use (N,C) bool."""
+    und = np.asarray(und, dtype=np.float64)
+    C, n, _ = und.shape
+    ctx = cams._ctx()
+    dev = cams._dev()
+    use = torch.from_numpy(np.ascontiguousarray(frame_use, dtype=np.uint8)).to(dev)
+    out = torch.empty((n, 3), dtype=torch.float64, device=dev)
+    und_d = cams._to_dev(und)
+    _lib.check(ctx.lib.mq_triangulate_pinv(ctx.handle, _lib.ptr(cams.cams_tensor()), C, _lib.ptr(und_d),
+                                           _lib.ptr(use), n, _lib.ptr(out), _lib.stream_ptr(dev)),
+               "mq_triangulate_pinv")
+    return out.cpu().numpy()
+
+
+def viterbi_filter(kp2d, score_threshold=0.3, n_back=3, offset_threshold=25, device: int = 0):
+    """Batched filter_pose_viterbi over kp2d (A,F,C,J,3) -> filtered (A,F,C,J,3) (step4:142-167)."""
+    kp = np.ascontiguousarray(kp2d, dtype=np.float64)
+    A, F, C, J, _ = kp.shape
+    ctx = _lib.Context.get(device)
+    dev = torch.device("cuda", device)
+    src = torch.from_numpy(kp).to(dev)
+    out = torch.empty_like(src)
+    _lib.check(ctx.lib.mq_viterbi_filter(ctx.handle, _lib.ptr(src), A, F, C, J, float(score_threshold), int(n_back),
+                                         float(offset_threshold), _lib.ptr(out), _lib.stream_ptr(dev)),
+               "mq_viterbi_filter")
+    return out.cpu().numpy()

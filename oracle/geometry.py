@@ -1,0 +1,437 @@
+"""ORACLE (test infrastructure only): float64 restatement of the anipose / mvpose
+geometry on the hot path.
+
+Sources restated (all under /root/reference):
+* ``src/third_party/aniposelib/cameras.py``:20-32 (triangulate_simple),
+  498-516 (OmnidirCamera.undistort_points / project), 593-637 (triangulate),
+  639-743 (triangulate_possible / triangulate_ransac), 746-783 (reprojection_error),
+  1116-1190 (optim_points), 1560-1620 (_error_fun_triangulation),
+  1670-1697 (_initialize_params_triangulation), 1714-1793 (_jac_sparsity_triangulation),
+  129-145 (medfilt_data / interpolate_data).
+* ``src/third_party/aniposelib/utils.py``:9-15 (make_M).
+* ``src/utils/multicam_toolbox.py``:393-486 (undistortPoints / triangulatePoints).
+* cv2.omnidir.projectPoints / undistortPoints / cv2.Rodrigues (opencv-contrib 4.11,
+  not installed; restated from the published Mei-model algorithm -- see DESIGN.md,
+  "parity unpinned" for the undistort final step).
+"""
+from __future__ import annotations
+
+import itertools
+
+import numpy as np
+from scipy import optimize, signal
+from scipy.sparse import dok_matrix
+
+
+# ----------------------------------------------------------------------------- cameras
+
+def rodrigues(rvec):
+    """cv2.Rodrigues(rvec) -> 3x3 (the theta < DBL_EPSILON branch returns I)."""
+    r = np.asarray(rvec, dtype=np.float64).ravel()
+    th = np.sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2])
+    if th < np.finfo(np.float64).eps:
+        return np.eye(3)
+    c = np.cos(th)
+    s = np.sin(th)
+    c1 = 1.0 - c
+    it = 1.0 / th
+    x, y, z = r[0] * it, r[1] * it, r[2] * it
+    return np.array([[c + c1 * x * x, c1 * x * y - s * z, c1 * x * z + s * y],
+                     [c1 * x * y + s * z, c + c1 * y * y, c1 * y * z - s * x],
+                     [c1 * x * z - s * y, c1 * y * z + s * x, c + c1 * z * z]])
+
+
+def make_M(rvec, tvec):
+    """utils.py:9-15 -- 4x4 [R|t; 0 0 0 1]."""
+    out = np.zeros((4, 4))
+    out[:3, :3] = rodrigues(rvec)
+    out[:3, 3] = np.asarray(tvec, dtype=np.float64).ravel()
+    out[3, 3] = 1
+    return out
+
+
+class OmnidirCam:
+    """cameras.py:429-555 OmnidirCamera (only the hot-path methods)."""
+
+    def __init__(self, d):
+        self.name = str(d["name"])
+        self.K = np.asarray(d["K"], dtype=np.float64)
+        self.xi = float(np.ravel(d["xi"])[0])
+        self.D = np.asarray(d["D"], dtype=np.float64).ravel()[:4]
+        self.rvec = np.asarray(d["rvec"] if "rvec" in d else d["rotation"], dtype=np.float64).ravel()
+        self.tvec = np.asarray(d["tvec"] if "tvec" in d else d["translation"], dtype=np.float64).ravel()
+
+    def extrinsics_mat(self):
+        return make_M(self.rvec, self.tvec)
+
+    def undistort_points(self, pts):
+        """cameras.py:498-507 -> cv2.omnidir.undistortPoints(pts, K, D, xi, I).
+
+        Mei model: normalise with skew, 20 Gauss-Seidel fixed-point iterations
+        removing (k1,k2,p1,p2), lift to the unit sphere, R = I, then the pinhole
+        reprojection (Xs/Zs) -- the form consistent with the [R|t] DLT of
+        cameras.py:20-32 (unpinned against opencv-contrib 4.11).
+        """
+        shape = pts.shape
+        p = np.asarray(pts, dtype=np.float64).reshape(-1, 2)
+        fx, fy, cx, cy, s = self.K[0, 0], self.K[1, 1], self.K[0, 2], self.K[1, 2], self.K[0, 1]
+        k1, k2, p1, p2 = self.D
+        xi = self.xi
+        ppx = (p[:, 0] * fy - cx * fy - s * (p[:, 1] - cy)) / (fx * fy)
+        ppy = (p[:, 1] - cy) / fy
+        x = ppx.copy()
+        y = ppy.copy()
+        for _ in range(20):
+            r2 = x * x + y * y
+            r4 = r2 * r2
+            x = (ppx - 2 * p1 * x * y - p2 * (r2 + 2 * x * x)) / (1 + k1 * r2 + k2 * r4)
+            y = (ppy - 2 * p2 * x * y - p1 * (r2 + 2 * y * y)) / (1 + k1 * r2 + k2 * r4)
+        r2 = x * x + y * y
+        a = r2 + 1
+        b = 2 * xi * r2
+        cc = r2 * xi * xi - 1
+        Zs = (-b + np.sqrt(b * b - 4 * a * cc)) / (2 * a)
+        Xw = x * (Zs + xi)
+        Yw = y * (Zs + xi)
+        nrm = np.sqrt(Xw * Xw + Yw * Yw + Zs * Zs)
+        Xs, Ys, Zn = Xw / nrm, Yw / nrm, Zs / nrm
+        out = np.stack([Xs / Zn, Ys / Zn], axis=-1)
+        return out.reshape(shape)
+
+    def project(self, p3d):
+        """cameras.py:509-516 -> cv2.omnidir.projectPoints(p, rvec, tvec, K, xi, D)."""
+        X = np.asarray(p3d, dtype=np.float64).reshape(-1, 3)
+        R = rodrigues(self.rvec)
+        t = self.tvec
+        Xc0 = R[0, 0] * X[:, 0] + R[0, 1] * X[:, 1] + R[0, 2] * X[:, 2] + t[0]
+        Xc1 = R[1, 0] * X[:, 0] + R[1, 1] * X[:, 1] + R[1, 2] * X[:, 2] + t[1]
+        Xc2 = R[2, 0] * X[:, 0] + R[2, 1] * X[:, 1] + R[2, 2] * X[:, 2] + t[2]
+        nrm = np.sqrt(Xc0 * Xc0 + Xc1 * Xc1 + Xc2 * Xc2)
+        xs, ys, zs = Xc0 / nrm, Xc1 / nrm, Xc2 / nrm
+        xu = xs / (zs + self.xi)
+        yu = ys / (zs + self.xi)
+        k1, k2, p1, p2 = self.D
+        r2 = xu * xu + yu * yu
+        r4 = r2 * r2
+        xd = xu * (1 + k1 * r2 + k2 * r4) + 2 * p1 * xu * yu + p2 * (r2 + 2 * xu * xu)
+        yd = yu * (1 + k1 * r2 + k2 * r4) + p1 * (r2 + 2 * yu * yu) + 2 * p2 * xu * yu
+        K = self.K
+        u = K[0, 0] * xd + K[0, 1] * yd + K[0, 2]
+        v = K[1, 1] * yd + K[1, 2]
+        return np.stack([u, v], axis=-1)
+
+    def reprojection_error(self, p3d, p2d):
+        """cameras.py:326-328 (Camera.reprojection_error)."""
+        proj = self.project(p3d).reshape(p2d.shape)
+        return p2d - proj
+
+
+def triangulate_simple(points, camera_mats):
+    """cameras.py:20-32 -- homogeneous DLT, last right-singular vector of the 2k x 4 system."""
+    num_cams = len(camera_mats)
+    A = np.zeros((num_cams * 2, 4))
+    for i in range(num_cams):
+        x, y = points[i]
+        mat = camera_mats[i]
+        A[i * 2] = x * mat[2] - mat[0]
+        A[i * 2 + 1] = y * mat[2] - mat[1]
+    u, s, vh = np.linalg.svd(A, full_matrices=True)
+    p3d = vh[-1]
+    return p3d[:3] / p3d[3]
+
+
+class CameraGroupOracle:
+    """cameras.py:557-783 CameraGroup hot-path methods."""
+
+    def __init__(self, cam_dicts):
+        self.cameras = [c if isinstance(c, OmnidirCam) else OmnidirCam(c) for c in cam_dicts]
+
+    def subset(self, idx):
+        g = CameraGroupOracle([])
+        g.cameras = [self.cameras[i] for i in idx]
+        return g
+
+    def project(self, p3d):
+        p3d = np.asarray(p3d, dtype=np.float64).reshape(-1, 3)
+        return np.stack([c.project(p3d) for c in self.cameras])
+
+    def undistort(self, points):
+        return np.stack([c.undistort_points(np.copy(points[i])) for i, c in enumerate(self.cameras)])
+
+    def triangulate(self, points, undistort=True):
+        """cameras.py:593-637."""
+        assert points.shape[0] == len(self.cameras)
+        one_point = False
+        if points.ndim == 2:
+            points = points.reshape(-1, 1, 2)
+            one_point = True
+        if undistort:
+            points = self.undistort(points)
+        n_cams, n_points, _ = points.shape
+        out = np.full((n_points, 3), np.nan)
+        cam_mats = np.array([c.extrinsics_mat() for c in self.cameras])
+        for ip in range(n_points):
+            subp = points[:, ip, :]
+            good = ~np.isnan(subp[:, 0])
+            if np.sum(good) >= 2:
+                out[ip] = triangulate_simple(subp[good], cam_mats[good])
+        if one_point:
+            out = out[0]
+        return out
+
+    def reprojection_error(self, p3ds, p2ds, mean=False):
+        """cameras.py:746-783."""
+        one_point = False
+        if p3ds.ndim == 1 and p2ds.ndim == 2:
+            p3ds = p3ds.reshape(1, 3)
+            p2ds = p2ds.reshape(-1, 1, 2)
+            one_point = True
+        n_cams, n_points, _ = p2ds.shape
+        assert p3ds.shape == (n_points, 3)
+        errors = np.empty((n_cams, n_points, 2))
+        for cnum, cam in enumerate(self.cameras):
+            errors[cnum] = cam.reprojection_error(p3ds, p2ds[cnum])
+        if mean:
+            errors_norm = np.linalg.norm(errors, axis=2)
+            good = ~np.isnan(errors_norm)
+            errors_norm[~good] = 0
+            denom = np.sum(good, axis=0).astype('float64')
+            denom[denom < 1.5] = np.nan
+            errors = np.sum(errors_norm, axis=0) / denom
+        if one_point:
+            if mean:
+                errors = float(errors[0])
+            else:
+                errors = errors.reshape(-1, 2)
+        return errors
+
+    def triangulate_possible(self, points, undistort=True, min_cams=2, threshold=0.5):
+        """cameras.py:639-722 for n_possible = 1 (the triangulate_ransac path).
+
+        Subsets come from ``itertools.product`` over ``[(cam, 0), None]`` for each
+        camera with a non-NaN point, in ascending camera order; the first subset
+        whose error drops below ``threshold`` ends the search (``best`` starts at 200).
+        """
+        n_cams, n_points, n_possible, _ = points.shape
+        assert n_cams == len(self.cameras)
+        out = np.full((n_points, 3), np.nan)
+        picked_vals = np.zeros((n_cams, n_points, n_possible), dtype=bool)
+        errors = np.zeros(n_points)
+        points_2d = np.full((n_cams, n_points, 2), np.nan)
+        for ip in range(n_points):
+            present = {}
+            for c in range(n_cams):
+                for k in range(n_possible):
+                    if not np.isnan(points[c, ip, k, 0]):
+                        present.setdefault(c, []).append((c, k))
+            for c in present:
+                present[c].append(None)
+            best_point = None
+            best_error = 200
+            n_cams_max = len(present)
+            for picked in itertools.product(*present.values()):
+                picked = [p for p in picked if p is not None]
+                if len(picked) < min_cams and len(picked) != n_cams_max:
+                    continue
+                cnums = [p[0] for p in picked]
+                xnums = [p[1] for p in picked]
+                pts = points[cnums, ip, xnums]
+                cc = self.subset(cnums)
+                if len(cnums) == 0:
+                    continue  # 0-camera subset: p3d NaN, err NaN -> never accepted
+                p3d = cc.triangulate(pts, undistort=undistort)
+                err = cc.reprojection_error(p3d, pts, mean=True)
+                if err < best_error:
+                    best_point = dict(error=err, point=p3d[:3], points=pts, picked=picked)
+                    best_error = err
+                    if best_error < threshold:
+                        break
+            if best_point is not None:
+                out[ip] = best_point['point']
+                cn = [p[0] for p in best_point['picked']]
+                xn = [p[1] for p in best_point['picked']]
+                picked_vals[cn, ip, xn] = True
+                errors[ip] = best_point['error']
+                points_2d[cn, ip] = best_point['points']
+        return out, picked_vals, points_2d, errors
+
+    def triangulate_ransac(self, points, undistort=True, min_cams=2):
+        """cameras.py:724-743."""
+        n_cams, n_points, _ = points.shape
+        return self.triangulate_possible(points.reshape(n_cams, n_points, 1, 2),
+                                         undistort=undistort, min_cams=min_cams)
+
+    # ------------------------------------------------------------------ optim_points
+    def _error_fun_triangulation(self, params, p2ds, constraints, constraints_weak,
+                                 scale_smooth, scale_length, scale_length_weak,
+                                 reproj_error_threshold, reproj_loss, n_deriv_smooth):
+        """cameras.py:1560-1620."""
+        n_cams, n_frames, n_joints, _ = p2ds.shape
+        n_3d = n_frames * n_joints * 3
+        n_c = len(constraints)
+        p3ds = params[:n_3d].reshape((n_frames, n_joints, 3))
+        jl = np.array(params[n_3d:n_3d + n_c])
+        jlw = np.array(params[n_3d + n_c:])
+        p3ds_flat = p3ds.reshape(-1, 3)
+        p2ds_flat = p2ds.reshape((n_cams, -1, 2))
+        errors = self.reprojection_error(p3ds_flat, p2ds_flat)
+        errors_reproj = errors[~np.isnan(p2ds_flat)]
+        rp = reproj_error_threshold
+        errors_reproj = np.abs(errors_reproj)
+        if reproj_loss == 'huber':
+            bad = errors_reproj > rp
+            errors_reproj[bad] = rp * (2 * np.sqrt(errors_reproj[bad] / rp) - 1)
+        elif reproj_loss == 'soft_l1':
+            errors_reproj = rp * 2 * (np.sqrt(1 + errors_reproj / rp) - 1)
+        errors_smooth = np.diff(p3ds, n=n_deriv_smooth, axis=0).ravel() * scale_smooth
+        el = np.empty((len(constraints), n_frames))
+        for cix, (a, b) in enumerate(constraints):
+            lengths = np.linalg.norm(p3ds[:, a] - p3ds[:, b], axis=1)
+            el[cix] = 100 * (lengths - jl[cix]) / jl[cix]
+        el = el.ravel() * scale_length
+        elw = np.empty((len(constraints_weak), n_frames))
+        for cix, (a, b) in enumerate(constraints_weak):
+            lengths = np.linalg.norm(p3ds[:, a] - p3ds[:, b], axis=1)
+            elw[cix] = 100 * (lengths - jlw[cix]) / jlw[cix]
+        elw = elw.ravel() * scale_length_weak
+        return np.hstack([errors_reproj, errors_smooth, el, elw])
+
+
+def medfilt_data(values, size=15):
+    """cameras.py:129-133."""
+    padsize = size + 5
+    vpad = np.pad(values, (padsize, padsize), mode='reflect')
+    vpadf = signal.medfilt(vpad, kernel_size=size)
+    return vpadf[padsize:-padsize]
+
+
+def interpolate_data(vals):
+    """cameras.py:135-145."""
+    nans = np.isnan(vals)
+    out = np.copy(vals)
+    try:
+        out[nans] = np.interp(nans.nonzero()[0], (~nans).nonzero()[0], vals[~nans])
+    except ValueError:
+        out[:] = 0
+    return out
+
+
+def initialize_params_triangulation(p3ds, constraints, constraints_weak):
+    """cameras.py:1670-1697."""
+    jl = np.empty(len(constraints))
+    jlw = np.empty(len(constraints_weak))
+    for cix, (a, b) in enumerate(constraints):
+        jl[cix] = np.median(np.linalg.norm(p3ds[:, a] - p3ds[:, b], axis=1))
+    for cix, (a, b) in enumerate(constraints_weak):
+        jlw[cix] = np.median(np.linalg.norm(p3ds[:, a] - p3ds[:, b], axis=1))
+    all_lengths = np.hstack([jl, jlw])
+    med = np.median(all_lengths)
+    if med == 0:
+        med = 1e-3
+    mad = np.median(np.abs(all_lengths - med))
+    jl[jl == 0] = med
+    jlw[jlw == 0] = med
+    jl[jl > med + mad * 5] = med
+    jlw[jlw > med + mad * 5] = med
+    return np.hstack([p3ds.ravel(), jl, jlw])
+
+
+def jac_sparsity_triangulation(p2ds, constraints, constraints_weak, n_deriv_smooth=1):
+    """cameras.py:1714-1793."""
+    n_cams, n_frames, n_joints, _ = p2ds.shape
+    n_c = len(constraints)
+    n_cw = len(constraints_weak)
+    p2ds_flat = p2ds.reshape((n_cams, -1, 2))
+    point_indices = np.zeros(p2ds_flat.shape, dtype='int32')
+    for i in range(p2ds_flat.shape[1]):
+        point_indices[:, i] = i
+    point_indices_3d = np.arange(n_frames * n_joints).reshape((n_frames, n_joints))
+    good = ~np.isnan(p2ds_flat)
+    n_errors_reproj = np.sum(good)
+    n_errors_smooth = (n_frames - n_deriv_smooth) * n_joints * 3
+    n_errors_lengths = n_c * n_frames
+    n_errors_lengths_weak = n_cw * n_frames
+    n_errors = n_errors_reproj + n_errors_smooth + n_errors_lengths + n_errors_lengths_weak
+    n_3d = n_frames * n_joints * 3
+    n_params = n_3d + n_c + n_cw
+    point_indices_good = point_indices[good]
+    A = dok_matrix((n_errors, n_params), dtype='int16')
+    ix_reproj = np.arange(n_errors_reproj)
+    for k in range(3):
+        A[ix_reproj, point_indices_good * 3 + k] = 1
+    frames = np.arange(n_frames - n_deriv_smooth)
+    for j in range(n_joints):
+        for n in range(n_deriv_smooth + 1):
+            pa = point_indices_3d[frames, j]
+            pb = point_indices_3d[frames + n, j]
+            for k in range(3):
+                A[n_errors_reproj + pa * 3 + k, pb * 3 + k] = 1
+    start = n_errors_reproj + n_errors_smooth
+    frames = np.arange(n_frames)
+    for cix, (a, b) in enumerate(constraints):
+        A[start + cix * n_frames + frames, n_3d + cix] = 1
+    for cix, (a, b) in enumerate(constraints):
+        pa = point_indices_3d[frames, a]
+        pb = point_indices_3d[frames, b]
+        for k in range(3):
+            A[start + cix * n_frames + frames, pa * 3 + k] = 1
+            A[start + cix * n_frames + frames, pb * 3 + k] = 1
+    start = n_errors_reproj + n_errors_smooth + n_errors_lengths
+    for cix, (a, b) in enumerate(constraints_weak):
+        A[start + cix * n_frames + frames, n_3d + n_c + cix] = 1
+    for cix, (a, b) in enumerate(constraints_weak):
+        pa = point_indices_3d[frames, a]
+        pb = point_indices_3d[frames, b]
+        for k in range(3):
+            A[start + cix * n_frames + frames, pa * 3 + k] = 1
+            A[start + cix * n_frames + frames, pb * 3 + k] = 1
+    return A
+
+
+def optim_points(cgroup, points, p3ds, constraints=(), constraints_weak=(), scale_smooth=4,
+                 scale_length=2, scale_length_weak=0.5, reproj_error_threshold=15,
+                 reproj_loss='soft_l1', n_deriv_smooth=1, ftol=1e-3, return_result=False):
+    """cameras.py:1116-1190 -- scipy TRF with a 2-point FD sparse Jacobian, loss 'linear'."""
+    n_cams, n_frames, n_joints, _ = points.shape
+    assert n_cams == len(cgroup.cameras)
+    constraints = np.array(constraints)
+    constraints_weak = np.array(constraints_weak)
+    p3ds_intp = np.apply_along_axis(interpolate_data, 0, p3ds)
+    p3ds_med = np.apply_along_axis(medfilt_data, 0, p3ds_intp, size=7)
+    default_smooth = 1.0 / np.mean(np.abs(np.diff(p3ds_med, axis=0)))
+    scale_smooth_full = scale_smooth * default_smooth
+    x0 = initialize_params_triangulation(p3ds_intp, constraints, constraints_weak)
+    x0[~np.isfinite(x0)] = 0
+    jac = jac_sparsity_triangulation(points, constraints, constraints_weak, n_deriv_smooth)
+    res = optimize.least_squares(
+        cgroup._error_fun_triangulation, x0=x0, jac_sparsity=jac, loss='linear', ftol=ftol,
+        args=(points, constraints, constraints_weak, scale_smooth_full, scale_length,
+              scale_length_weak, reproj_error_threshold, reproj_loss, n_deriv_smooth))
+    p3ds_new = res.x[:p3ds.size].reshape(p3ds.shape)
+    joint_len = res.x[p3ds.size:]
+    if return_result:
+        return p3ds_new, joint_len, res, scale_smooth_full, x0
+    return p3ds_new, joint_len
+
+
+# ----------------------------------------------------------------------------- mvpose DLT
+
+def mct_triangulate_points(pos_2d_undist, frame_use, pmat):
+    """multicam_toolbox.py:433-486 -- inhomogeneous DLT: X = pinv(A[:,:3]) A[:,3], P = -X."""
+    n_frame, n_cam = frame_use.shape
+    P = np.zeros((n_frame, 3))
+    U = pos_2d_undist
+    for i_frame in range(n_frame):
+        if np.sum(frame_use[i_frame, :]) < 2:
+            P[i_frame, :] = np.nan
+            continue
+        A = []
+        for i_cam in range(n_cam):
+            if frame_use[i_frame, i_cam]:
+                a1 = U[i_cam][i_frame, 0] * pmat[i_cam][2, :] - pmat[i_cam][0, :]
+                a2 = U[i_cam][i_frame, 1] * pmat[i_cam][2, :] - pmat[i_cam][1, :]
+                A.append(np.vstack((a1, a2)))
+        A = np.vstack(A)
+        X = np.matmul(np.linalg.pinv(A[:, :3]), A[:, 3])
+        P[i_frame, :] = -X
+    return P

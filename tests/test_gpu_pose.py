@@ -1,0 +1,154 @@
+"""GPU parity: crop, ViTPose forward (bf16 MFMA) and UDP decode of libmq_hip vs the oracle."""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+# bf16 heatmaps vs the fp32 oracle: max|dH| <= 2e-2 * max|H| per sample
+HM_TOL = 2e-2
+
+
+def _frames_and_boxes(n_views=3, seed=0):
+    from mqhip import synth
+    rng = np.random.default_rng(seed)
+    frames = rng.integers(0, 256, size=(n_views, 300, 400, 3), dtype=np.uint8)
+    boxes = []
+    frame_idx = []
+    for v in range(n_views):
+        for _ in range(3):
+            x1, y1 = rng.uniform(-40, 350), rng.uniform(-40, 250)
+            w, h = rng.uniform(10, 160), rng.uniform(10, 200)
+            boxes.append([x1, y1, x1 + w, y1 + h])
+            frame_idx.append(v)
+    return frames, np.array(boxes, dtype=np.float32), np.array(frame_idx, dtype=np.int32)
+
+
+def test_crop_bit_exact():
+    import torch
+    from mqhip.pose import crop_boxes
+    from oracle.crop import preprocess, topdown_crop
+    frames, boxes, fidx = _frames_and_boxes()
+    crops, center, scale = crop_boxes(torch.from_numpy(frames).cuda(), torch.from_numpy(boxes).cuda(),
+                                      torch.from_numpy(fidx).cuda())
+    crops, center, scale = crops.cpu().numpy(), center.cpu().numpy(), scale.cpu().numpy()
+    for i in range(len(boxes)):
+        c_u8, c, s = topdown_crop(frames[fidx[i]], boxes[i])
+        np.testing.assert_array_equal(center[i], c)
+        np.testing.assert_array_equal(scale[i], s)
+        np.testing.assert_array_equal(crops[i], preprocess(c_u8))
+
+
+def _peaky_heatmaps(n, J=17, seed=0):
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:64, 0:48]
+    hm = rng.normal(0, 0.02, (n, J, 64, 48)).astype(np.float32)
+    for i in range(n):
+        for k in range(J):
+            cx, cy = rng.uniform(-2, 49), rng.uniform(-2, 65)
+            hm[i, k] += np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * 2.0 ** 2)).astype(np.float32)
+    hm[0, 3] = -np.abs(hm[0, 3])  # max <= 0 -> loc -1 + wrap-around reads
+    hm[1, 0] = -np.abs(hm[1, 0])
+    return hm
+
+
+def test_decode_matches_oracle():
+    import torch
+    from mqhip.pose import decode_heatmaps
+    from oracle.decode import decode_batch, udp_decode
+    n = 6
+    hm = _peaky_heatmaps(n)
+    rng = np.random.default_rng(1)
+    center = rng.uniform(100, 1500, (n, 2)).astype(np.float32)
+    scale = rng.uniform(50, 400, (n, 2)).astype(np.float32)
+    kp, score, am, kp_hm = decode_heatmaps(torch.from_numpy(hm).cuda(), torch.from_numpy(center).cuda(),
+                                           torch.from_numpy(scale).cuda())
+    rkp, rsc, ram = decode_batch(hm, center, scale)
+    np.testing.assert_array_equal(am.cpu().numpy(), ram)          # bit-exact argmax
+    np.testing.assert_array_equal(score.cpu().numpy(), rsc)       # peak values
+    kp_hm = kp_hm.cpu().numpy()
+    for i in range(n):
+        from oracle.decode import refine_keypoints_dark_udp, get_heatmap_maximum
+        locs, vals, _ = get_heatmap_maximum(hm[i].copy())
+        ref = refine_keypoints_dark_udp(locs[None].copy(), hm[i].copy())[0]
+        np.testing.assert_allclose(kp_hm[i], ref, rtol=0, atol=2e-4)
+    np.testing.assert_allclose(kp.cpu().numpy(), rkp, rtol=0, atol=2e-2)
+
+
+def _run_vit(cfg_name, n_crops, seed=0):
+    import torch
+    from mqhip.pose import VitPoseHip
+    from mqhip.weights import CONFIGS, make_random_weights
+    from oracle.vitpose import forward_flip_test
+    cfg = CONFIGS[cfg_name]
+    w = make_random_weights(cfg, seed=seed, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed + 1)
+    crops = torch.randn((n_crops, 3, 256, 192), generator=g, device="cuda", dtype=torch.float32)
+    model = VitPoseHip(cfg, w, graph=False)
+    got = model.forward(crops, flip_test=True)
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        torch.backends.cuda.matmul.allow_tf32 = False
+        torch.backends.cudnn.allow_tf32 = False
+        ref, _, _ = forward_flip_test(crops, w, cfg)
+    return got.float().cpu().numpy(), ref.float().cpu().numpy()
+
+
+@pytest.mark.parametrize("cfg_name,n", [("tiny", 3), ("base", 2), ("huge", 2)])
+def test_vitpose_heatmaps_vs_fp32_oracle(cfg_name, n):
+    got, ref = _run_vit(cfg_name, n)
+    assert np.all(np.isfinite(got))
+    for i in range(n):
+        scale = np.abs(ref[i]).max()
+        err = np.abs(got[i] - ref[i]).max()
+        assert err <= HM_TOL * scale, f"{cfg_name} sample {i}: max|d|={err:.3e} vs {HM_TOL}*{scale:.3e}"
+
+
+def test_vitpose_graph_replay_matches_eager():
+    import torch
+    from mqhip.pose import VitPoseHip
+    from mqhip.weights import VIT_TINY, make_random_weights
+    w = make_random_weights(VIT_TINY, seed=3, device="cuda")
+    crops = torch.randn((4, 3, 256, 192), device="cuda")
+    eager = VitPoseHip(VIT_TINY, w, graph=False).forward(crops).clone()
+    model = VitPoseHip(VIT_TINY, w, graph=True)
+    out = torch.empty_like(eager)
+    for _ in range(3):
+        model.forward(crops, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
+
+
+def test_topdown_end_to_end_vs_oracle():
+    """crop -> ViT-tiny (flip) -> decode; argmax exact wherever the top-2 margin is clear."""
+    import torch
+    from mqhip.pose import VitPoseHip
+    from mqhip.weights import VIT_TINY, make_random_weights
+    from oracle.crop import preprocess, topdown_crop
+    from oracle.decode import decode_batch
+    from oracle.vitpose import forward_flip_test
+    frames, boxes, fidx = _frames_and_boxes(seed=4)
+    w = make_random_weights(VIT_TINY, seed=5, device="cuda")
+    model = VitPoseHip(VIT_TINY, w, graph=False)
+    kp, score, am = model.topdown(torch.from_numpy(frames).cuda(), torch.from_numpy(boxes).cuda(),
+                                  torch.from_numpy(fidx).cuda())
+    crops, cs, ss = [], [], []
+    for i in range(len(boxes)):
+        c_u8, c, s = topdown_crop(frames[fidx[i]], boxes[i])
+        crops.append(preprocess(c_u8))
+        cs.append(c)
+        ss.append(s)
+    x = torch.from_numpy(np.stack(crops)).cuda()
+    with torch.no_grad():
+        ref_hm, _, _ = forward_flip_test(x, w, VIT_TINY)
+    ref_hm = ref_hm.cpu().numpy()
+    rkp, rsc, ram = decode_batch(ref_hm, np.stack(cs), np.stack(ss))
+    am = am.cpu().numpy()
+    flat = ref_hm.reshape(ref_hm.shape[0], ref_hm.shape[1], -1)
+    top2 = np.sort(flat, axis=-1)[..., -2:]
+    margin = (top2[..., 1] - top2[..., 0]) / np.abs(flat).max(axis=-1)
+    clear = margin > 5e-2
+    assert clear.sum() > 0
+    np.testing.assert_array_equal(am[clear], ram[clear])
