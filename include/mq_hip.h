@@ -92,6 +92,13 @@ int mq_topdown(mq_vitpose* model, const uint8_t* frames, int64_t frame_stride, i
                const float* boxes, const int32_t* box_frame, int n, int flip_test, double* kp_img, float* score,
                int32_t* argmax, float* heatmaps, void* stream);
 
+/* bf16 MFMA GEMM building block used by the forward: C[M,N] = A[M,K] * W[N,K]^T + bias
+ * (A, W bf16 K-contiguous; leading dims in elements).  epilogue: 0 C bf16, 1 C bf16 with
+ * exact-erf GELU, 2 C f32 += (residual), 3 C f32 = . + aux[m % aux_rows][n] (pos_embed),
+ * 4 C f32, 5 C f32 scattered to [m / aux_rows][n][m % aux_rows] (NCHW).  bias/aux may be NULL. */
+int mq_gemm_bf16(mq_ctx* ctx, const void* A, const void* W, void* C, const float* bias, const float* aux, int M,
+                 int N, int K, int lda, int ldw, int ldc, int aux_rows, int epilogue, void* stream);
+
 /* ======================================================================= geometry
  * Replaces aniposelib CameraGroup (cameras.py:593-783), anipose filter_pose_viterbi
  * (filter_pose.py:48-186) and the mvpose DLT (multicam_toolbox.py:393-486).

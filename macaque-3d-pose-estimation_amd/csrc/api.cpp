@@ -596,6 +596,21 @@ int mq_topdown(mq_vitpose* m, const uint8_t* frames, int64_t frame_stride, int h
                        stream);
 }
 
+// ----------------------------------------------------------------------------- building blocks
+int mq_gemm_bf16(mq_ctx* ctx, const void* A, const void* W, void* C, const float* bias, const float* aux, int M,
+                 int N, int K, int lda, int ldw, int ldc, int aux_rows, int epilogue, void* stream) {
+  if (!ctx || !A || !W || !C) return fail("mq_gemm_bf16: null argument");
+  if (M <= 0 || N <= 0 || K <= 0) return fail("mq_gemm_bf16: bad sizes", -2);
+  if (epilogue < 0 || epilogue > 5) return fail("mq_gemm_bf16: bad epilogue", -2);
+  if ((epilogue == mq::EPI_POS_F32 || epilogue == mq::EPI_NCHW_F32) && (!aux_rows || (!aux && epilogue == 3)))
+    return fail("mq_gemm_bf16: epilogue needs aux", -2);
+  HIP_TRY(hipSetDevice(ctx->device));
+  mq::GemmArgs g{(const unsigned short*)A, (const unsigned short*)W, C, bias, aux, M, N, K, lda, ldw, ldc, aux_rows};
+  int rc = mq::gemm_bf16(g, epilogue, (hipStream_t)stream);
+  if (rc) return fail("mq_gemm_bf16: launch failed / unsupported shape (K % 32, lda/ldw % 8)", -6);
+  return 0;
+}
+
 // ----------------------------------------------------------------------------- geometry
 static int check_geo(mq_ctx* ctx, const void* cams, int C, int n) {
   if (!ctx) return fail("null ctx");

@@ -18,6 +18,8 @@
 
 namespace mq {
 
+bool g_gemm_force_small = false;
+
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int GEMM_THREADS = 256;
 constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand tile
@@ -143,9 +145,203 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
   }
 }
 
+// ============================================================================
+// 256x256 tile, BK = 32, 4-stage LDS ring (128 KiB), 512 threads = 8 waves (2 M x 4 N),
+// each wave 128 x 64 = 8 x 4 MFMA 16x16x32 tiles.  Every K-step issues the DMA of
+// the tile three steps ahead and waits only for the NEXT tile (counted vmcnt +
+// raw s_barrier: a __syncthreads() would drain every in-flight DMA).  Arithmetic
+// intensity 128 FLOP per staged byte (vs 64 for 128x128), ~3 K-steps (~3k cycles)
+// of latency cover.  The MFMA runs "swapped" (D = W * A^T): each lane then holds 4
+// consecutive output columns of one row, so the epilogue stores 8 B (bf16) or
+// 16 B (f32) per lane instead of scalar 2-byte stores.
+// LDS image: 64-byte rows, 16-byte chunk c of row r at slot c ^ ((r >> 1) & 3)
+// (ds_read_b128 conflict-free for the 16x16x32 fragment pattern).
+constexpr int B2M = 256, B2N = 256, B2K = 32, B2S = 4, B2T = 512;
+constexpr int B2_OP_BYTES = B2M * B2K * 2;       // 16 KiB per operand per stage
+constexpr int B2_STAGE_BYTES = 2 * B2_OP_BYTES;  // 32 KiB
+
+__device__ __forceinline__ int swz2(int row) { return (row >> 1) & 3; }
+
+// one 256x32 bf16 operand tile = 16 wave-instructions of 1 KiB; wave w issues 2 of them
+__device__ __forceinline__ void stage256(const bf16_t* __restrict__ g, int ld, int r0, int rmax, int k0,
+                                         char* lds_op, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rbase = (wave * 2 + i) * 16;
+    const int row = rbase + (lane >> 2);
+    const int chunk = (lane & 3) ^ swz2(row);
+    int grow = r0 + row;
+    grow = grow < rmax ? grow : rmax - 1;
+    const bf16_t* src = g + (size_t)grow * ld + k0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(src), MQ_LDS_LOCAL(lds_op + rbase * 64), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 frag256(const char* lds_op, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(lds_op + row * 64 + ((chunk ^ swz2(row)) << 4));
+}
+
+template <int N_IN_FLIGHT>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N_IN_FLIGHT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N_IN_FLIGHT == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int EPI>
+__global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // XCD-contiguous block ids, then grouped (8 M-tiles) ordering for L2 panel reuse
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles_m = (p.M + B2M - 1) / B2M;
+  const int tiles_n = (p.N + B2N - 1) / B2N;
+  constexpr int GROUP_M = 8;
+  const int per_group = GROUP_M * tiles_n;
+  const int grp = wid / per_group;
+  const int first_m = grp * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_g = wid - grp * per_group;
+  const int tm = first_m + in_g % gsize;
+  const int tn = in_g / gsize;
+  const int m0 = tm * B2M, n0 = tn * B2N;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / B2K;
+  // prologue: stages 0..2 in flight
+#pragma unroll
+  for (int st = 0; st < B2S - 1; ++st) {
+    if (st < nk) {
+      char* sb = smem + st * B2_STAGE_BYTES;
+      stage256(p.A, p.lda, m0, p.M, st * B2K, sb, wave, lane);
+      stage256(p.W, p.ldw, n0, p.N, st * B2K, sb + B2_OP_BYTES, wave, lane);
+    }
+  }
+  if (nk >= 3) wait_vm<8>();
+  else if (nk == 2) wait_vm<4>();
+  else wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+
+  const int frow = lane & 15;
+  const int fk = lane >> 4;
+  for (int t = 0; t < nk; ++t) {
+    if (t + 3 < nk) {
+      char* sb = smem + ((t + 3) & 3) * B2_STAGE_BYTES;
+      stage256(p.A, p.lda, m0, p.M, (t + 3) * B2K, sb, wave, lane);
+      stage256(p.W, p.ldw, n0, p.N, (t + 3) * B2K, sb + B2_OP_BYTES, wave, lane);
+    }
+    const char* As = smem + (t & 3) * B2_STAGE_BYTES;
+    const char* Bs = As + B2_OP_BYTES;
+    bf16x8 a[8], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = frag256(Bs, wn * 64 + j * 16 + frow, fk);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = frag256(As, wm * 128 + i * 16 + frow, fk);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // retire the next stage's DMA (loads issued after it stay in flight), then rendezvous
+    const int ahead = min(t + 3, nk - 1) - (t + 1);
+    if (ahead >= 2) wait_vm<8>();
+    else if (ahead == 1) wait_vm<4>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // epilogue: lane holds D[n][m] with m = l & 15 (col of D) and n = 4*(l >> 4) + e
+  const int mm = lane & 15;
+  const int nn = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm * 128 + i * 16 + mm;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + nn;
+      if (n >= p.N) continue;
+      float v[4];
+      const float4 bias = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[0] = acc[i][j][0] + bias.x;
+      v[1] = acc[i][j][1] + bias.y;
+      v[2] = acc[i][j][2] + bias.z;
+      v[3] = acc[i][j][3] + bias.w;
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+        if constexpr (EPI == EPI_GELU_BF16) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+        }
+        uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        *reinterpret_cast<uint2*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
+      } else if constexpr (EPI == EPI_RESID_F32) {
+        float4* c = reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n);
+        float4 x = *c;
+        x.x += v[0];
+        x.y += v[1];
+        x.z += v[2];
+        x.w += v[3];
+        *c = x;
+      } else if constexpr (EPI == EPI_POS_F32) {
+        const float4 ps = *reinterpret_cast<const float4*>(p.aux + (size_t)(m % p.aux_rows) * p.N + n);
+        *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) =
+            make_float4(v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w);
+      } else if constexpr (EPI == EPI_F32) {
+        *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
+static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
+  const int tiles = ((p.M + B2M - 1) / B2M) * ((p.N + B2N - 1) / B2N);
+  dim3 grid(tiles), block(B2T);
+  const size_t lds = (size_t)B2S * B2_STAGE_BYTES;
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL(gemm256_kernel<EPI_BF16>, grid, block, lds, stream, p); break;
+    case EPI_GELU_BF16: hipLaunchKernelGGL(gemm256_kernel<EPI_GELU_BF16>, grid, block, lds, stream, p); break;
+    case EPI_RESID_F32: hipLaunchKernelGGL(gemm256_kernel<EPI_RESID_F32>, grid, block, lds, stream, p); break;
+    case EPI_POS_F32: hipLaunchKernelGGL(gemm256_kernel<EPI_POS_F32>, grid, block, lds, stream, p); break;
+    case EPI_F32: hipLaunchKernelGGL(gemm256_kernel<EPI_F32>, grid, block, lds, stream, p); break;
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+static bool g_lds_attr_set = false;
+
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
-  if (p.K % BK != 0 || p.M <= 0 || p.N <= 0) return -1;
+  if (p.M <= 0 || p.N <= 0) return -1;
   if ((p.lda % 8) || (p.ldw % 8)) return -2;
+  const bool big = epi != EPI_NCHW_F32 && p.N >= 256 && p.M >= 256 && (p.N % 4) == 0 && (p.K % B2K) == 0 &&
+                   (p.ldc % 4) == 0 && !g_gemm_force_small;
+  if (big) {
+    if (!g_lds_attr_set) {
+      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_GELU_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_POS_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
+      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
+      g_lds_attr_set = true;
+    }
+    return gemm256(p, epi, stream);
+  }
+  if (p.K % BK != 0) return -1;
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   dim3 grid(tiles), block(GEMM_THREADS);
   const size_t lds = 4 * TILE_BYTES;

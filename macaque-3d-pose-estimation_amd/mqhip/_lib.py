@@ -18,7 +18,7 @@ EXPORTED = [
     "mq_abi_version", "mq_last_error", "mq_create", "mq_destroy",
     "mq_vitpose_create", "mq_vitpose_destroy", "mq_vitpose_set_param", "mq_vitpose_finalize",
     "mq_vitpose_set_graph", "mq_vitpose_timing", "mq_vitpose_timing_result", "mq_crop_udp", "mq_vitpose_forward", "mq_decode_udp", "mq_topdown",
-    "mq_omnidir_undistort", "mq_omnidir_project", "mq_triangulate_dlt", "mq_reproj_error",
+    "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_triangulate_dlt", "mq_reproj_error",
     "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_viterbi_filter",
 ]
 
@@ -51,6 +51,7 @@ _SIGS = {
     "mq_vitpose_forward": (i32, [vp, vp, i32, i32, vp, vp]),
     "mq_decode_udp": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, vp]),
     "mq_topdown": (i32, [vp, vp, i64, i32, i32, vp, vp, i32, i32, vp, vp, vp, vp, vp]),
+    "mq_gemm_bf16": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mq_omnidir_undistort": (i32, [vp, vp, i32, vp, i32, vp, vp]),
     "mq_omnidir_project": (i32, [vp, vp, i32, vp, i32, vp, vp]),
     "mq_triangulate_dlt": (i32, [vp, vp, i32, vp, i32, i32, vp, vp]),

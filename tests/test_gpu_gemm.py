@@ -1,0 +1,85 @@
+"""GPU numerics of the bf16 MFMA GEMM building block (mq_gemm_bf16) vs a PyTorch fp32 reference.
+
+Inputs are bf16; the reference multiplies the same bf16 values in fp32 (torch matmul
+with TF32 off), so only the accumulation order differs: tolerance 2e-3 relative to
+the row's |A||W| scale, plus bf16 output rounding where the epilogue emits bf16.
+"""
+import ctypes as C
+
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+
+def _run(M, N, K, epi, aux_rows=0, seed=0):
+    import torch
+    from mqhip import _lib
+    torch.backends.cuda.matmul.allow_tf32 = False
+    ctx = _lib.Context.get(0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    A = torch.randn((M, K), generator=g, device="cuda").to(torch.bfloat16)
+    W = (torch.randn((N, K), generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    bias = torch.randn((N,), generator=g, device="cuda")
+    ref = A.float() @ W.float().t() + bias
+    aux = None
+    if epi in (0, 1):
+        Cm = torch.empty((M, N), device="cuda", dtype=torch.bfloat16)
+    elif epi == 2:
+        Cm = torch.randn((M, N), generator=g, device="cuda")
+        ref = ref + Cm
+    elif epi == 3:
+        aux = torch.randn((aux_rows, N), generator=g, device="cuda")
+        ref = ref + aux[torch.arange(M, device="cuda") % aux_rows]
+        Cm = torch.empty((M, N), device="cuda")
+    elif epi == 4:
+        Cm = torch.empty((M, N), device="cuda")
+    else:
+        Cm = torch.empty((M // aux_rows, N, aux_rows), device="cuda")
+        ref = ref.view(M // aux_rows, aux_rows, N).permute(0, 2, 1)
+    if epi == 1:
+        ref = torch.nn.functional.gelu(ref)
+    rc = ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), _lib.ptr(bias), _lib.ptr(aux), M, N,
+                              K, K, K, N, aux_rows, epi, _lib.stream_ptr())
+    _lib.check(rc, "mq_gemm_bf16")
+    torch.cuda.synchronize()
+    scale = (A.float().abs() @ W.float().abs().t()).max().item() + 1.0
+    err = (Cm.float() - ref).abs().max().item()
+    return err, scale
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
+def test_gemm_256_path_all_epilogues(epi):
+    err, scale = _run(700, 512, 320, epi, aux_rows=192)
+    tol = 2e-3 * scale + (0.01 * scale if epi in (0, 1) else 0.0)
+    assert err <= tol, (err, tol)
+
+
+@pytest.mark.parametrize("M,N,K", [(12288, 1280, 1280), (1024, 3840, 1280), (512, 5120, 256)])
+def test_gemm_vit_shapes(M, N, K):
+    err, scale = _run(M, N, K, 4)
+    assert err <= 2e-3 * scale
+
+
+def test_gemm_small_path_nchw():
+    err, scale = _run(2 * 3072, 17, 256, 5, aux_rows=3072)
+    assert err <= 2e-3 * scale
+
+
+def test_gemm_small_path_narrow():
+    err, scale = _run(300, 128, 128, 4)
+    assert err <= 2e-3 * scale
+
+
+def test_gemm_rejects_bad_k():
+    import torch
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    A = torch.zeros((64, 40), device="cuda", dtype=torch.bfloat16)
+    W = torch.zeros((64, 40), device="cuda", dtype=torch.bfloat16)
+    Cm = torch.zeros((64, 64), device="cuda")
+    rc = ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), None, None, 64, 64, 40, 40, 40, 64,
+                              0, 4, _lib.stream_ptr())
+    assert rc != 0
