@@ -33,6 +33,11 @@ typedef struct mq_vitpose mq_vitpose;
 int mq_abi_version(void);
 const char* mq_last_error(void);
 
+/* Process-wide tuning knobs (for A/B measurement; defaults are the tuned values). */
+#define MQ_TUNE_GEMM_STAGES 1       /* LDS ring depth of the 256x256 GEMM: 4 (128 KiB) or 5 (160 KiB) */
+#define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 kernel */
+int mq_set_tuning(int key, int value);
+
 /* Bind a context to HIP device `device`. */
 int mq_create(int device, mq_ctx** out);
 int mq_destroy(mq_ctx* ctx);

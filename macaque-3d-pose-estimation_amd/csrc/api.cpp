@@ -125,6 +125,20 @@ extern "C" {
 
 int mq_abi_version(void) { return MQ_ABI_VERSION; }
 
+int mq_set_tuning(int key, int value) {
+  switch (key) {
+    case MQ_TUNE_GEMM_STAGES:
+      if (value != 4 && value != 5) return fail("mq_set_tuning: GEMM stages must be 4 or 5", -2);
+      mq::g_gemm_stages = value;
+      return 0;
+    case MQ_TUNE_GEMM_FORCE_SMALL:
+      mq::g_gemm_force_small = value != 0;
+      return 0;
+    default:
+      return fail("mq_set_tuning: unknown key", -2);
+  }
+}
+
 const char* mq_last_error(void) { return g_err.c_str(); }
 
 int mq_create(int device, mq_ctx** out) {

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
 // 16 B (f32) per lane instead of scalar 2-byte stores.
 // LDS image: 64-byte rows, 16-byte chunk c of row r at slot c ^ ((r >> 1) & 3)
 // (ds_read_b128 conflict-free for the 16x16x32 fragment pattern).
-constexpr int B2M = 256, B2N = 256, B2K = 32, B2S = 4, B2T = 512;
+constexpr int B2M = 256, B2N = 256, B2K = 32, B2T = 512;
 constexpr int B2_OP_BYTES = B2M * B2K * 2;       // 16 KiB per operand per stage
 constexpr int B2_STAGE_BYTES = 2 * B2_OP_BYTES;  // 32 KiB
 
@@ -183,35 +183,95 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds_op, int row, int chunk
 
 template <int N_IN_FLIGHT>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N_IN_FLIGHT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  if constexpr (N_IN_FLIGHT == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N_IN_FLIGHT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N_IN_FLIGHT == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int EPI>
-__global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-
-  // XCD-contiguous block ids, then grouped (8 M-tiles) ordering for L2 panel reuse
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int q = nwg >> 3, r = nwg & 7;
-  const int wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tiles_m = (p.M + B2M - 1) / B2M;
-  const int tiles_n = (p.N + B2N - 1) / B2N;
+// Tile -> (m0, n0): grouped ordering (8 M-tiles per group) so the tiles an XCD works
+// on concurrently share A and W panels in its L2.
+__device__ __forceinline__ void tile_coords(int wid, int tiles_m, int tiles_n, int& m0, int& n0) {
   constexpr int GROUP_M = 8;
   const int per_group = GROUP_M * tiles_n;
   const int grp = wid / per_group;
   const int first_m = grp * GROUP_M;
   const int gsize = min(tiles_m - first_m, GROUP_M);
   const int in_g = wid - grp * per_group;
-  const int tm = first_m + in_g % gsize;
-  const int tn = in_g / gsize;
-  const int m0 = tm * B2M, n0 = tn * B2N;
+  m0 = (first_m + in_g % gsize) * B2M;
+  n0 = (in_g / gsize) * B2N;
+}
+
+// Persistent: one 512-thread block per CU walks its tiles; the DMA stream and the
+// fragment pipeline run straight across tile boundaries (the first stages of the
+// next tile are in flight while the current tile's epilogue stores drain).
+template <int EPI, int NS>
+__global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int frow = lane & 15;
+  const int fk = lane >> 4;
+
+  // tiles of this XCD = a contiguous range; its blocks take them round-robin
+  const int nt = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int nbx = (G - xcd + 7) >> 3;  // blocks on this XCD
+  const int xb = bid >> 3;
+  const int q = nt >> 3, r = nt & 7;
+  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int len = q + (xcd < r ? 1 : 0);
+  const int my_tiles = xb < len ? (len - xb + nbx - 1) / nbx : 0;
+  const int nk = p.K / B2K;
+  const int total = my_tiles * nk;
+  if (total == 0) return;
+
+  // DMA issue cursor: (tile, k) of the next stage to load and this lane's source rows
+  // for that tile (recomputed only when the cursor moves to the next tile).  Past the
+  // end the cursor stays on the last stage: extra DMAs re-load it into a dead buffer,
+  // which keeps every wait count uniform.
+  int iss_t = 0, iss_k = 0, iss_slot = 0;
+  const bf16_t* pa[2];
+  const bf16_t* pw[2];
+  auto set_tile_ptrs = [&](int ti) {
+    int m0, n0;
+    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wave * 2 + i) * 16 + (lane >> 2);
+      const int chunk = (lane & 3) ^ swz2(row);
+      const int ga = min(m0 + row, p.M - 1), gw = min(n0 + row, p.N - 1);
+      pa[i] = p.A + (size_t)ga * p.lda + chunk * 8;
+      pw[i] = p.W + (size_t)gw * p.ldw + chunk * 8;
+    }
+  };
+  set_tile_ptrs(0);
+  auto issue_a = [&]() {
+    char* sb = smem + iss_slot * B2_STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pa[i] + iss_k * B2K),
+                                       MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+  };
+  auto issue_w_and_advance = [&]() {
+    char* sb = smem + iss_slot * B2_STAGE_BYTES + B2_OP_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pw[i] + iss_k * B2K),
+                                       MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+    iss_slot = iss_slot + 1 == NS ? 0 : iss_slot + 1;
+    if (iss_k + 1 < nk) {
+      ++iss_k;
+    } else if (iss_t + 1 < my_tiles) {
+      ++iss_t;
+      iss_k = 0;
+      set_tile_ptrs(iss_t);
+    }
+  };
+  auto stage_ptr = [&](int g) { return smem + (g % NS) * B2_STAGE_BYTES; };
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -219,111 +279,157 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K / B2K;
-  // prologue: stages 0..2 in flight
+  // prologue: stages 0 .. NS-2 in flight; stage NS-1 is issued by the first K-step
 #pragma unroll
-  for (int st = 0; st < B2S - 1; ++st) {
-    if (st < nk) {
-      char* sb = smem + st * B2_STAGE_BYTES;
-      stage256(p.A, p.lda, m0, p.M, st * B2K, sb, wave, lane);
-      stage256(p.W, p.ldw, n0, p.N, st * B2K, sb + B2_OP_BYTES, wave, lane);
-    }
+  for (int st = 0; st < NS - 1; ++st) {
+    issue_a();
+    issue_w_and_advance();
   }
-  if (nk >= 3) wait_vm<8>();
-  else if (nk == 2) wait_vm<4>();
-  else wait_vm<0>();
+  wait_vm<4 * (NS - 3)>();  // stages 0 and 1 landed (this wave)
   __builtin_amdgcn_s_barrier();
 
-  const int frow = lane & 15;
-  const int fk = lane >> 4;
-  for (int t = 0; t < nk; ++t) {
-    if (t + 3 < nk) {
-      char* sb = smem + ((t + 3) & 3) * B2_STAGE_BYTES;
-      stage256(p.A, p.lda, m0, p.M, (t + 3) * B2K, sb, wave, lane);
-      stage256(p.W, p.ldw, n0, p.N, (t + 3) * B2K, sb + B2_OP_BYTES, wave, lane);
-    }
-    const char* As = smem + (t & 3) * B2_STAGE_BYTES;
-    const char* Bs = As + B2_OP_BYTES;
-    bf16x8 a[8], b[4];
+  bf16x8 a[8], b0[4], b1[4];
+  {
+    const char* As = stage_ptr(0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = frag256(Bs, wn * 64 + j * 16 + frow, fk);
+    for (int j = 0; j < 4; ++j) b0[j] = frag256(As + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
 #pragma unroll
     for (int i = 0; i < 8; ++i) a[i] = frag256(As, wm * 128 + i * 16 + frow, fk);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    // retire the next stage's DMA (loads issued after it stay in flight), then rendezvous
-    const int ahead = min(t + 3, nk - 1) - (t + 1);
-    if (ahead >= 2) wait_vm<8>();
-    else if (ahead == 1) wait_vm<4>();
-    else wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
   }
 
-  // epilogue: lane holds D[n][m] with m = l & 15 (col of D) and n = 4*(l >> 4) + e
-  const int mm = lane & 15;
-  const int nn = 4 * (lane >> 4);
+  auto epilogue = [&](int ti) {
+    int m0, n0;
+    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+    // lane holds D[n][m] with m = l & 15 (col of D) and n = 4 * (l >> 4) + e
+    const int mm = lane & 15;
+    const int nn = 4 * (lane >> 4);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + mm;
-    if (m >= p.M) continue;
+    for (int i = 0; i < 8; ++i) {
+      const int m = m0 + wm * 128 + i * 16 + mm;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + nn;
-      if (n >= p.N) continue;
-      float v[4];
-      const float4 bias = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-      v[0] = acc[i][j][0] + bias.x;
-      v[1] = acc[i][j][1] + bias.y;
-      v[2] = acc[i][j][2] + bias.z;
-      v[3] = acc[i][j][3] + bias.w;
-      if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-        if constexpr (EPI == EPI_GELU_BF16) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + nn;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (m >= p.M || n >= p.N) continue;
+        if (p.bias) {
+          const float4 bias = *reinterpret_cast<const float4*>(p.bias + n);
+          v[0] += bias.x;
+          v[1] += bias.y;
+          v[2] += bias.z;
+          v[3] += bias.w;
         }
-        uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        *reinterpret_cast<uint2*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
-      } else if constexpr (EPI == EPI_RESID_F32) {
-        float4* c = reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n);
-        float4 x = *c;
-        x.x += v[0];
-        x.y += v[1];
-        x.z += v[2];
-        x.w += v[3];
-        *c = x;
-      } else if constexpr (EPI == EPI_POS_F32) {
-        const float4 ps = *reinterpret_cast<const float4*>(p.aux + (size_t)(m % p.aux_rows) * p.N + n);
-        *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) =
-            make_float4(v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w);
-      } else if constexpr (EPI == EPI_F32) {
-        *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+          if constexpr (EPI == EPI_GELU_BF16) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+          }
+          uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+          *reinterpret_cast<uint2*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
+        } else if constexpr (EPI == EPI_RESID_F32) {
+          float4* c = reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n);
+          float4 x = *c;
+          x.x += v[0];
+          x.y += v[1];
+          x.z += v[2];
+          x.w += v[3];
+          *c = x;
+        } else if constexpr (EPI == EPI_POS_F32) {
+          const float4 ps = *reinterpret_cast<const float4*>(p.aux + (size_t)(m % p.aux_rows) * p.N + n);
+          *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) =
+              make_float4(v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w);
+        } else if constexpr (EPI == EPI_F32) {
+          *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+        }
       }
     }
+  };
+
+  // One K-step of 32 MFMAs per wave.  The DMA of stage g+NS-1 (into the buffer stage
+  // g-1 used) is spread over the two MFMA halves; the next step's fragments are read
+  // one MFMA half ahead of their use; at the end stage g+2 is retired (later stages
+  // stay in flight) and the block rendezvous once.
+  auto kstep = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
+    const char* An = stage_ptr(g + 1);  // past the end: harmless reads of a dead buffer
+    issue_a();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bn[j] = frag256(An + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
+    issue_w_and_advance();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int i = 4; i < 8; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+    wait_vm<4 * (NS - 3)>();  // stage g+2 landed; g+3 .. g+NS-1 stay in flight
+    __builtin_amdgcn_s_barrier();
+    const int ti = g / nk;
+    if (g - ti * nk == nk - 1) epilogue(ti);
+  };
+  int g = 0;
+  for (; g + 1 < total; g += 2) {
+    kstep(g, b0, b1);
+    kstep(g + 1, b1, b0);
   }
+  if (g < total) kstep(g, b0, b1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the block
+}
+
+static int g_num_cus = 0;
+
+int g_gemm_stages = 4;  // tuning knob (mq_set_tuning(MQ_TUNE_GEMM_STAGES, 4|5))
+
+template <int EPI, int NS>
+static void launch256(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
+  static bool attr = false;
+  const int lds = NS * B2_STAGE_BYTES;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm256_kernel<EPI, NS>), grid, dim3(B2T), lds, stream, p, tiles_m, tiles_n);
+}
+
+template <int EPI>
+static void launch256s(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
+  if (g_gemm_stages == 5)
+    launch256<EPI, 5>(grid, stream, p, tiles_m, tiles_n);
+  else
+    launch256<EPI, 4>(grid, stream, p, tiles_m, tiles_n);
 }
 
 static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
-  const int tiles = ((p.M + B2M - 1) / B2M) * ((p.N + B2N - 1) / B2N);
-  dim3 grid(tiles), block(B2T);
-  const size_t lds = (size_t)B2S * B2_STAGE_BYTES;
+  if (!g_num_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
+      g_num_cus = 256;
+  }
+  const int tiles_m = (p.M + B2M - 1) / B2M, tiles_n = (p.N + B2N - 1) / B2N;
+  const int tiles = tiles_m * tiles_n;
+  dim3 grid(tiles < g_num_cus ? tiles : g_num_cus);
   switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL(gemm256_kernel<EPI_BF16>, grid, block, lds, stream, p); break;
-    case EPI_GELU_BF16: hipLaunchKernelGGL(gemm256_kernel<EPI_GELU_BF16>, grid, block, lds, stream, p); break;
-    case EPI_RESID_F32: hipLaunchKernelGGL(gemm256_kernel<EPI_RESID_F32>, grid, block, lds, stream, p); break;
-    case EPI_POS_F32: hipLaunchKernelGGL(gemm256_kernel<EPI_POS_F32>, grid, block, lds, stream, p); break;
-    case EPI_F32: hipLaunchKernelGGL(gemm256_kernel<EPI_F32>, grid, block, lds, stream, p); break;
+    case EPI_BF16: launch256s<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_GELU_BF16: launch256s<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RESID_F32: launch256s<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_POS_F32: launch256s<EPI_POS_F32>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_F32: launch256s<EPI_F32>(grid, stream, p, tiles_m, tiles_n); break;
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
-
-static bool g_lds_attr_set = false;
 
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return -1;
@@ -331,14 +437,6 @@ int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   const bool big = epi != EPI_NCHW_F32 && p.N >= 256 && p.M >= 256 && (p.N % 4) == 0 && (p.K % B2K) == 0 &&
                    (p.ldc % 4) == 0 && !g_gemm_force_small;
   if (big) {
-    if (!g_lds_attr_set) {
-      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_GELU_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_RESID_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_POS_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
-      (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, B2S * B2_STAGE_BYTES);
-      g_lds_attr_set = true;
-    }
     return gemm256(p, epi, stream);
   }
   if (p.K % BK != 0) return -1;

@@ -26,6 +26,8 @@ struct GemmArgs {
 };
 
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
+extern int g_gemm_stages;
+extern bool g_gemm_force_small;
 
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,

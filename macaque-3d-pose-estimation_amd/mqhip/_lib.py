@@ -15,7 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmq_hip.so"))
 
 EXPORTED = [
-    "mq_abi_version", "mq_last_error", "mq_create", "mq_destroy",
+    "mq_abi_version", "mq_last_error", "mq_set_tuning", "mq_create", "mq_destroy",
     "mq_vitpose_create", "mq_vitpose_destroy", "mq_vitpose_set_param", "mq_vitpose_finalize",
     "mq_vitpose_set_graph", "mq_vitpose_timing", "mq_vitpose_timing_result", "mq_crop_udp", "mq_vitpose_forward", "mq_decode_udp", "mq_topdown",
     "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_triangulate_dlt", "mq_reproj_error",
@@ -38,6 +38,7 @@ f64 = C.c_double
 _SIGS = {
     "mq_abi_version": (i32, []),
     "mq_last_error": (C.c_char_p, []),
+    "mq_set_tuning": (i32, [i32, i32]),
     "mq_create": (i32, [i32, C.POINTER(vp)]),
     "mq_destroy": (i32, [vp]),
     "mq_vitpose_create": (i32, [vp, i32, i32, i32, i32, i32, C.POINTER(vp)]),

@@ -1,0 +1,75 @@
+"""Time the ViT GEMM shapes through mq_gemm_bf16 (hipEvents on the launch stream).
+
+python tools/gemm_probe.py [--iters N] [--shape fc1|fc2|qkv|proj|dc1|dc2|all]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "macaque-3d-pose-estimation_amd"))
+
+SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
+    "qkv": (12288, 3840, 1280, 0),
+    "proj": (12288, 1280, 1280, 2),
+    "fc1": (12288, 5120, 1280, 1),
+    "fc2": (12288, 1280, 5120, 2),
+    "dc1": (12288, 4096, 1280, 0),
+    "dc2": (49152, 4096, 256, 0),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--shape", default="all")
+    ap.add_argument("--variants", default="4,5,small", help="GEMM variants to A/B in this process")
+    args = ap.parse_args()
+    import torch
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    names = list(SHAPES) if args.shape == "all" else args.shape.split(",")
+    res = {}
+    variants = args.variants.split(",")
+    for rnd in range(2):
+      for var in variants:
+        if var == "small":
+            ctx.lib.mq_set_tuning(2, 1)
+        else:
+            ctx.lib.mq_set_tuning(2, 0)
+            ctx.lib.mq_set_tuning(1, int(var))
+        for name in names:
+            res[f"{name}/{var}/r{rnd}"] = bench_one(ctx, _lib, torch, name, args.iters)
+            print(f"{name} v={var} r={rnd}", res[f"{name}/{var}/r{rnd}"], flush=True)
+    print(json.dumps(res))
+
+
+def bench_one(ctx, _lib, torch, name, iters):
+    if True:
+        M, N, K, epi = SHAPES[name]
+        A = (torch.rand((M, K), device="cuda") * 2 - 1).to(torch.bfloat16)
+        W = ((torch.rand((N, K), device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+        bias = torch.zeros((N,), device="cuda")
+        Cm = torch.zeros((M, N), device="cuda", dtype=torch.bfloat16 if epi in (0, 1) else torch.float32)
+        s = _lib.stream_ptr()
+
+        def run():
+            _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), _lib.ptr(bias), None,
+                                            M, N, K, K, K, N, 0, epi, s), name)
+        for _ in range(3):
+            run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / iters
+        tf = 2 * M * N * K / (ms * 1e-3) / 1e12
+        return {"M": M, "N": N, "K": K, "ms": round(ms, 4), "tflops": round(tf, 1)}
+
+
+if __name__ == "__main__":
+    main()
