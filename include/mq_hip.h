@@ -36,6 +36,8 @@ const char* mq_last_error(void);
 /* Process-wide tuning knobs (for A/B measurement; defaults are the tuned values). */
 #define MQ_TUNE_GEMM_STAGES 1       /* LDS ring depth of the 256x256 GEMM: 4 (128 KiB) or 5 (160 KiB) */
 #define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 kernel */
+#define MQ_TUNE_GEMM_ABLATE 3       /* timing ablations of the f32-epilogue 256 GEMM (WRONG results):
+                                       1 no steady-state DMA, 2 no barrier, 3 both, 7 + no LDS reads */
 int mq_set_tuning(int key, int value);
 
 /* Bind a context to HIP device `device`. */

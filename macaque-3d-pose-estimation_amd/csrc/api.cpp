@@ -131,6 +131,11 @@ int mq_set_tuning(int key, int value) {
       if (value != 4 && value != 5) return fail("mq_set_tuning: GEMM stages must be 4 or 5", -2);
       mq::g_gemm_stages = value;
       return 0;
+    case MQ_TUNE_GEMM_ABLATE:
+      if (value != 0 && value != 1 && value != 2 && value != 3 && value != 7)
+        return fail("mq_set_tuning: ablation must be 0, 1, 2, 3 or 7", -2);
+      mq::g_gemm_ablate = value;
+      return 0;
     case MQ_TUNE_GEMM_FORCE_SMALL:
       mq::g_gemm_force_small = value != 0;
       return 0;

@@ -183,7 +183,9 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds_op, int row, int chunk
 
 template <int N_IN_FLIGHT>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N_IN_FLIGHT == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  if constexpr (N_IN_FLIGHT == 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+  else if constexpr (N_IN_FLIGHT == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+  else if constexpr (N_IN_FLIGHT == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else if constexpr (N_IN_FLIGHT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else if constexpr (N_IN_FLIGHT == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -205,7 +207,9 @@ __device__ __forceinline__ void tile_coords(int wid, int tiles_m, int tiles_n, i
 // Persistent: one 512-thread block per CU walks its tiles; the DMA stream and the
 // fragment pipeline run straight across tile boundaries (the first stages of the
 // next tile are in flight while the current tile's epilogue stores drain).
-template <int EPI, int NS>
+// ABL (timing ablations only, outputs are wrong when non-zero): bit0 no steady-state
+// DMA, bit1 no per-step barrier, bit2 no fragment re-reads.
+template <int EPI, int NS, int ABL = 0>
 __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -349,9 +353,10 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
   // g-1 used) is spread over the two MFMA halves; the next step's fragments are read
   // one MFMA half ahead of their use; at the end stage g+2 is retired (later stages
   // stay in flight) and the block rendezvous once.
+  bool stores_pending = false;
   auto kstep = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
     const char* An = stage_ptr(g + 1);  // past the end: harmless reads of a dead buffer
-    issue_a();
+    if constexpr (!(ABL & 1)) issue_a();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -359,11 +364,16 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(ABL & 4)) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+      for (int i = 0; i < 4; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bn[j] = frag256(An + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
-    issue_w_and_advance();
+      for (int j = 0; j < 4; ++j) bn[j] = frag256(An + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bn[j] = bc[j];
+    }
+    if constexpr (!(ABL & 1)) issue_w_and_advance();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 4; i < 8; ++i)
@@ -371,12 +381,28 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(ABL & 4)) {
 #pragma unroll
-    for (int i = 4; i < 8; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
-    wait_vm<4 * (NS - 3)>();  // stage g+2 landed; g+3 .. g+NS-1 stay in flight
-    __builtin_amdgcn_s_barrier();
+      for (int i = 4; i < 8; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+    }
+    // stage g+2 landed; g+3 .. g+NS-1 in flight.  Right after a full tile's epilogue its
+    // 32 stores per wave sit between those DMAs in the in-order vmcnt queue: let them
+    // drain behind this step instead of stalling the MFMAs on them.
+    if constexpr (!(ABL & 1)) {
+      if (stores_pending)
+        wait_vm<4 * (NS - 3) + 32>();
+      else
+        wait_vm<4 * (NS - 3)>();
+    }
+    stores_pending = false;
+    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();
     const int ti = g / nk;
-    if (g - ti * nk == nk - 1) epilogue(ti);
+    if (g - ti * nk == nk - 1) {
+      epilogue(ti);
+      int m0, n0;
+      tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+      stores_pending = (m0 + B2M <= p.M) && (n0 + B2N <= p.N);
+    }
   };
   int g = 0;
   for (; g + 1 < total; g += 2) {
@@ -390,24 +416,35 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
 static int g_num_cus = 0;
 
 int g_gemm_stages = 4;  // tuning knob (mq_set_tuning(MQ_TUNE_GEMM_STAGES, 4|5))
+int g_gemm_ablate = 0;  // timing ablation knob (MQ_TUNE_GEMM_ABLATE)
 
-template <int EPI, int NS>
+template <int EPI, int NS, int ABL>
 static void launch256(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   const int lds = NS * B2_STAGE_BYTES;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<EPI, NS>), grid, dim3(B2T), lds, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm256_kernel<EPI, NS, ABL>), grid, dim3(B2T), lds, stream, p, tiles_m, tiles_n);
 }
 
 template <int EPI>
 static void launch256s(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
+  if constexpr (EPI == EPI_F32) {  // ablations are compiled for the plain-f32 epilogue only
+    switch (g_gemm_ablate) {
+      case 1: launch256<EPI, 4, 1>(grid, stream, p, tiles_m, tiles_n); return;
+      case 2: launch256<EPI, 4, 2>(grid, stream, p, tiles_m, tiles_n); return;
+      case 3: launch256<EPI, 4, 3>(grid, stream, p, tiles_m, tiles_n); return;
+      case 7: launch256<EPI, 4, 7>(grid, stream, p, tiles_m, tiles_n); return;
+      default: break;
+    }
+  }
   if (g_gemm_stages == 5)
-    launch256<EPI, 5>(grid, stream, p, tiles_m, tiles_n);
+    launch256<EPI, 5, 0>(grid, stream, p, tiles_m, tiles_n);
   else
-    launch256<EPI, 4>(grid, stream, p, tiles_m, tiles_n);
+    launch256<EPI, 4, 0>(grid, stream, p, tiles_m, tiles_n);
 }
 
 static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {

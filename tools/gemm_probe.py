@@ -17,6 +17,7 @@ SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
     "fc2": (12288, 1280, 5120, 2),
     "dc1": (12288, 4096, 1280, 0),
     "dc2": (49152, 4096, 256, 0),
+    "f32": (12288, 1280, 5120, 4),   # fc2 shape, plain f32 epilogue (ablation target)
 }
 
 
@@ -34,8 +35,13 @@ def main():
     variants = args.variants.split(",")
     for rnd in range(2):
       for var in variants:
+        ctx.lib.mq_set_tuning(3, 0)
         if var == "small":
             ctx.lib.mq_set_tuning(2, 1)
+        elif var.startswith("abl"):
+            ctx.lib.mq_set_tuning(2, 0)
+            ctx.lib.mq_set_tuning(1, 4)
+            ctx.lib.mq_set_tuning(3, int(var[3:]))
         else:
             ctx.lib.mq_set_tuning(2, 0)
             ctx.lib.mq_set_tuning(1, int(var))
