@@ -30,6 +30,23 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
+// Exact-erf GELU with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below
+// the bf16 rounding of the output): one v_rcp, one v_exp and a degree-5 Horner chain
+// instead of the library erff (the GELU epilogue was 20 % of the fc1 GEMM).
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
+  float poly = 1.061405429f;
+  poly = poly * t - 1.453152027f;
+  poly = poly * t + 1.421413741f;
+  poly = poly * t - 0.284496736f;
+  poly = poly * t + 0.254829592f;
+  poly = poly * t;
+  const float erf_abs = 1.0f - poly * __expf(-z * z);
+  const float erf_v = copysignf(erf_abs, x);
+  return 0.5f * x * (1.0f + erf_v);
+}
+
 // Issue the DMA of one 128x64 bf16 tile (rows [r0, r0+128) of a K-contiguous
 // matrix with leading dimension ld, columns [k0, k0+64)) into LDS.
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int ld, int r0, int rmax, int k0,
@@ -184,6 +201,8 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds_op, int row, int chunk
 template <int N_IN_FLIGHT>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N_IN_FLIGHT == 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+  else if constexpr (N_IN_FLIGHT == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else if constexpr (N_IN_FLIGHT == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
   else if constexpr (N_IN_FLIGHT == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
   else if constexpr (N_IN_FLIGHT == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   else if constexpr (N_IN_FLIGHT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -307,6 +326,52 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     // lane holds D[n][m] with m = l & 15 (col of D) and n = 4 * (l >> 4) + e
     const int mm = lane & 15;
     const int nn = 4 * (lane >> 4);
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+      // pack to bf16, then pair tiles (j, j+1): v_permlane16_swap gives every lane 8
+      // consecutive columns (even 16-lane groups: tile j, odd groups: tile j+1) -> one
+      // 16-byte store per lane per pair instead of two 8-byte stores.
+      const bool odd = (lane >> 4) & 1;
+      const int nbase = 4 * (lane >> 4) - (odd ? 4 : 0);
+      // all bias loads before the first store: a load behind a store would wait for it
+      float4 bias[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + nn;
+        bias[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int m = m0 + wm * 128 + i * 16 + mm;
+#pragma unroll
+        for (int jp = 0; jp < 4; jp += 2) {
+          unsigned pk[2][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = jp + h;
+            const int n = n0 + wn * 64 + j * 16 + nn;
+            (void)n;
+            float v[4] = {acc[i][j][0] + bias[j].x, acc[i][j][1] + bias[j].y, acc[i][j][2] + bias[j].z,
+                          acc[i][j][3] + bias[j].w};
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI == EPI_GELU_BF16) {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+            }
+            pk[h][0] = pack_bf16x2(v[0], v[1]);
+            pk[h][1] = pack_bf16x2(v[2], v[3]);
+          }
+          const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+          // even lanes: [own tile j | neighbour's tile j]; odd: [neighbour's j+1 | own j+1]
+          const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+          const int j = jp + (odd ? 1 : 0);
+          const int n = n0 + wn * 64 + j * 16 + nbase;
+          if (m < p.M && n < p.N)
+            *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int m = m0 + wm * 128 + i * 16 + mm;
@@ -323,14 +388,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
           v[2] += bias.z;
           v[3] += bias.w;
         }
-        if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-          if constexpr (EPI == EPI_GELU_BF16) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
-          }
-          uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-          *reinterpret_cast<uint2*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
-        } else if constexpr (EPI == EPI_RESID_F32) {
+        if constexpr (EPI == EPI_RESID_F32) {
           float4* c = reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n);
           float4 x = *c;
           x.x += v[0];
@@ -349,10 +407,6 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     }
   };
 
-  // One K-step of 32 MFMAs per wave.  The DMA of stage g+NS-1 (into the buffer stage
-  // g-1 used) is spread over the two MFMA halves; the next step's fragments are read
-  // one MFMA half ahead of their use; at the end stage g+2 is retired (later stages
-  // stay in flight) and the block rendezvous once.
   bool stores_pending = false;
   auto kstep = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
     const char* An = stage_ptr(g + 1);  // past the end: harmless reads of a dead buffer
@@ -389,8 +443,10 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     // 32 stores per wave sit between those DMAs in the in-order vmcnt queue: let them
     // drain behind this step instead of stalling the MFMAs on them.
     if constexpr (!(ABL & 1)) {
+      // >= this many VMEM ops of a full tile's epilogue are younger than stage g+2's DMA
+      constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
       if (stores_pending)
-        wait_vm<4 * (NS - 3) + 32>();
+        wait_vm<4 * (NS - 3) + EPI_OPS>();
       else
         wait_vm<4 * (NS - 3)>();
     }

@@ -18,6 +18,10 @@ SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
     "dc1": (12288, 4096, 1280, 0),
     "dc2": (49152, 4096, 256, 0),
     "f32": (12288, 1280, 5120, 4),   # fc2 shape, plain f32 epilogue (ablation target)
+    "fc1_f32": (12288, 5120, 1280, 4),
+    "fc1_bf16": (12288, 5120, 1280, 0),
+    "n5120_k5120": (12288, 5120, 5120, 0),
+    "m8192": (8192, 5120, 1280, 0),
 }
 
 
