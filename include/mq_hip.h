@@ -38,6 +38,7 @@ const char* mq_last_error(void);
 #define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 kernel */
 #define MQ_TUNE_GEMM_ABLATE 3       /* timing ablations of the f32-epilogue 256 GEMM (WRONG results):
                                        1 no steady-state DMA, 2 no barrier, 3 both, 7 + no LDS reads */
+#define MQ_TUNE_OPTIM_PCG_ITERS 4   /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
 int mq_set_tuning(int key, int value);
 
 /* Bind a context to HIP device `device`. */
@@ -141,6 +142,23 @@ int mq_triangulate_pinv(mq_ctx* ctx, const double* cams, int n_cams, const doubl
  * owned by the context.  score_threshold 0.3, n_back 3, offset_threshold 25 in step 4. */
 int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int n_animals, int n_frames, int n_cams, int n_joints,
                       double score_threshold, int n_back, double offset_threshold, double* out, void* stream);
+
+/* CameraGroup.optim_points (cameras.py:1116-1190) and optim_points_jointlenfix (:1192-1415) for
+ * B animals at once.  Replaces scipy least_squares(trf, 2-point sparse Jacobian) with
+ * Levenberg-Marquardt on the analytic Jacobian, PCG inner solves.
+ *   p2d  device (B, C, F, J, 2) float64, NaN = missing coordinate
+ *   x    device (B, F*J*3 + n_strong + n_weak) in/out: [p3d, strong lengths, weak lengths]
+ *        (the reference's _initialize_params_triangulation layout, :1670-1697)
+ *   constraints host int32 (n_strong + n_weak, 2) joint pairs; scale_smooth_full host (B)
+ *   reproj_loss 0 linear, 1 soft_l1 (reference default), 2 huber
+ *   fix_lengths 1: lengths are constants (jointlenfix variant), only p3d is optimised
+ *   max_iter LM iterations (reference: unbounded / max_nfev 15), ftol scipy-style on accepted steps
+ *   stats host (B, 4): initial cost, final cost, LM iterations, status (1 ftol, 2 max_iter, 3 damping). */
+int mq_optim_points(mq_ctx* ctx, const double* cams, int n_cams, const double* p2d, double* x, int n_animals,
+                    int n_frames, int n_joints, const int32_t* constraints, int n_strong, int n_weak,
+                    const double* scale_smooth_full, double scale_length, double scale_length_weak,
+                    double reproj_error_threshold, int reproj_loss, int n_deriv_smooth, int fix_lengths,
+                    int max_iter, double ftol, double* stats, void* stream);
 
 #ifdef __cplusplus
 }

@@ -68,6 +68,7 @@ struct mq_ctx {
   int device = 0;
   DevBuf scratch;  // geometry scratch (Viterbi back-pointers)
   DevBuf decode_work;
+  DevBuf optim_ws;
 };
 
 struct ParamSlot {
@@ -138,6 +139,10 @@ int mq_set_tuning(int key, int value) {
       return 0;
     case MQ_TUNE_GEMM_FORCE_SMALL:
       mq::g_gemm_force_small = value != 0;
+      return 0;
+    case MQ_TUNE_OPTIM_PCG_ITERS:
+      if (value < 1 || value > 128) return fail("mq_set_tuning: PCG iterations must be in [1, 128]", -2);
+      mq::g_optim_pcg_iters = value;
       return 0;
     default:
       return fail("mq_set_tuning: unknown key", -2);
@@ -697,6 +702,32 @@ int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int A, int F, int C, int J,
   if (ctx->scratch.ensure((size_t)A * C * J * F * 8)) return fail("viterbi scratch alloc failed", -5);
   K_TRY(mq::viterbi_filter(kp, A, F, C, J, score_threshold, n_back, offset_threshold, ctx->scratch.as<int8_t>(), out,
                            (hipStream_t)stream));
+  return 0;
+}
+
+int mq_optim_points(mq_ctx* ctx, const double* cams, int C, const double* p2d, double* x, int B, int F, int J,
+                    const int32_t* constraints, int n_strong, int n_weak, const double* scale_smooth_full,
+                    double scale_length, double scale_length_weak, double reproj_error_threshold, int reproj_loss,
+                    int n_deriv_smooth, int fix_lengths, int max_iter, double ftol, double* stats, void* stream) {
+  if (!ctx || !cams || !p2d || !x || !scale_smooth_full || !stats) return fail("mq_optim_points: null argument");
+  if (B < 0 || F < 0 || J < 0 || n_strong < 0 || n_weak < 0) return fail("mq_optim_points: negative size", -2);
+  if ((int64_t)B * F * J == 0) return 0;
+  if (C < 1 || C > 16) return fail("mq_optim_points: 1 <= cameras <= 16", -2);
+  if (J > 32 || n_strong + n_weak > 64) return fail("mq_optim_points: at most 32 joints and 64 constraints", -2);
+  if (n_deriv_smooth < 1 || n_deriv_smooth > 3) return fail("mq_optim_points: n_deriv_smooth must be 1..3", -2);
+  if (reproj_loss < 0 || reproj_loss > 2) return fail("mq_optim_points: loss must be 0 linear, 1 soft_l1, 2 huber", -2);
+  if (!(reproj_error_threshold > 0)) return fail("mq_optim_points: reproj_error_threshold must be > 0", -2);
+  if (n_strong + n_weak > 0 && !constraints) return fail("mq_optim_points: null constraints");
+  for (int k = 0; k < 2 * (n_strong + n_weak); ++k)
+    if (constraints[k] < 0 || constraints[k] >= J) return fail("mq_optim_points: constraint joint out of range", -2);
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (ctx->optim_ws.ensure(mq::optim_workspace_bytes(B, F, J, n_strong + n_weak)))
+    return fail("optim workspace alloc failed", -5);
+  const int rc = mq::optim_points(cams, C, p2d, x, B, F, J, constraints, n_strong, n_weak, scale_smooth_full,
+                                  scale_length, scale_length_weak, reproj_error_threshold, reproj_loss,
+                                  n_deriv_smooth, fix_lengths, max_iter, ftol, ctx->optim_ws.p, stats,
+                                  (hipStream_t)stream);
+  if (rc != 0) return fail("mq_optim_points: solver failed (" + std::to_string(rc) + ")", -6);
   return 0;
 }
 

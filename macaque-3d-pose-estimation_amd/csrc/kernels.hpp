@@ -51,4 +51,12 @@ int udp_decode(const float* avg, int n, int joints, int h, int w, const float* c
                int in_w, int in_h, float* work, double* kp_img, float* score, int32_t* argmax, float* kp_hm,
                hipStream_t s);
 
+// optim_points (optim.hip)
+extern int g_optim_pcg_iters;
+size_t optim_workspace_bytes(int B, int F, int J, int NL);
+int optim_points(const double* cams, int C, const double* p2d, double* x, int B, int F, int J, const int* cons_host,
+                 int n_strong, int n_weak, const double* ssf_host, double scale_length, double scale_length_weak,
+                 double rp, int loss, int n_deriv, int fix_lengths, int max_iter, double ftol, void* ws,
+                 double* stats, hipStream_t s);
+
 }  // namespace mq

@@ -1,0 +1,723 @@
+// optim_points on the GPU (row a16): the aniposelib bundle-style refinement of
+// 3D keypoints, cameras.py:1116-1190 (objective :1560-1620, parameter layout
+// :1670-1697) and the fixed-length variant :1192-1415.
+//
+// Objective (identical residual set to the reference, per animal b):
+//   x = [p3d (F*J*3), L (n_strong + n_weak)]
+//   reprojection   r = rho(|p2d - project(X)|) per non-NaN coordinate
+//                  (rho = soft_l1 2 rp (sqrt(1+|e|/rp)-1), huber, or |e|)
+//   smoothness     r = ssf * diff^n(p3d over frames)         (np.diff order n)
+//   lengths        r = s * 100 (|Xa - Xb| - L) / L           (s = strong / weak scale)
+//
+// Solver (MI355X-native, replaces scipy TRF + 2-point finite differences):
+// Levenberg-Marquardt on the analytic Jacobian.  The normal matrix is never
+// formed globally: it is applied as
+//   H p = R_fj p_fj (3x3 reprojection blocks) + J_len^T (J_len p) + ssf^2 (D^T D (x) I) p + lam diag(H) p
+// and each LM step is solved by preconditioned conjugate gradients.  The
+// preconditioner is exact for everything except the cross-joint length
+// couplings: one block-banded (3x3 blocks, bandwidth n) Cholesky per joint
+// series over frames, plus a diagonal for the length variables.
+//
+// Determinism: every reduction is a fixed-order per-block / per-series sum, so
+// results are bitwise reproducible run to run.
+#include <algorithm>
+#include <vector>
+
+#include "common.hpp"
+
+namespace mq {
+namespace {
+
+constexpr int OPT_MAXJ = 32;
+constexpr int OPT_MAXL = 64;
+constexpr int OPT_MAXN = 3;
+constexpr int OPT_MAXC = 16;
+constexpr int OPT_MAXIT = 128;  // PCG iterations per LM step (upper bound)
+constexpr int OPT_THREADS = 128;
+
+struct OptDims {
+  int B, C, F, J, NL, nS, fix, n, loss;
+  int NX, NV;
+  double rp, s_len, s_len_weak, tol2;
+  double c[OPT_MAXN + 1];
+};
+
+struct OptBufs {
+  const double* cams;
+  const double* p2d;
+  const int* cons;    // [NL][2]
+  const double* ssf;  // [B]
+  const double* ctl;  // [B][2]: lambda, accept flag
+  double *g, *diag, *R, *lenJ, *costF, *cost;
+  double *d, *r, *z, *P0, *P1, *q, *fac, *pinvL, *rzJ, *pq, *pqF, *qLf;
+};
+
+__device__ __forceinline__ const CamParams& cam_at(const double* cams, int c) {
+  return *reinterpret_cast<const CamParams*>(cams + 24 * c);
+}
+
+__device__ __forceinline__ double dtd(int f, int g, int F, int n, const double* c) {
+  const int lo = max(0, max(f, g) - n), hi = min(min(f, g), F - 1 - n);
+  double s = 0;
+  for (int i = lo; i <= hi; ++i) s += c[f - i] * c[g - i];
+  return s;
+}
+
+// r = rho(|e|) and dr/de (cameras.py:1581-1590: abs first, then the loss).
+__device__ __forceinline__ void reproj_loss(double e, double rp, int loss, double& r, double& dr) {
+  const double a = fabs(e), sg = e < 0 ? -1.0 : 1.0;
+  if (loss == 1) {
+    const double s = sqrt(1 + a / rp);
+    r = rp * 2 * (s - 1);
+    dr = sg / s;
+  } else if (loss == 2 && a > rp) {
+    r = rp * (2 * sqrt(a / rp) - 1);
+    dr = sg * sqrt(rp / a);
+  } else {
+    r = a;
+    dr = sg;
+  }
+}
+
+// cv2.omnidir.projectPoints (same arithmetic as geometry.hip omni_project) plus
+// the analytic d(u,v)/dX.
+__device__ __forceinline__ void project_jac(const CamParams& cp, const double* X, double& u, double& v, double* Ju,
+                                            double* Jv) {
+  const double* R = cp.R;
+  const double x0 = R[0] * X[0] + R[1] * X[1] + R[2] * X[2] + cp.t[0];
+  const double x1 = R[3] * X[0] + R[4] * X[1] + R[5] * X[2] + cp.t[1];
+  const double x2 = R[6] * X[0] + R[7] * X[1] + R[8] * X[2] + cp.t[2];
+  const double nrm = sqrt(x0 * x0 + x1 * x1 + x2 * x2);
+  const double xs = x0 / nrm, ys = x1 / nrm, zs = x2 / nrm;
+  const double xu = xs / (zs + cp.xi), yu = ys / (zs + cp.xi);
+  const double r2 = xu * xu + yu * yu;
+  const double r4 = r2 * r2;
+  const double rad = 1 + cp.k1 * r2 + cp.k2 * r4;
+  const double xd = xu * rad + 2 * cp.p1 * xu * yu + cp.p2 * (r2 + 2 * xu * xu);
+  const double yd = yu * rad + cp.p1 * (r2 + 2 * yu * yu) + 2 * cp.p2 * xu * yu;
+  u = cp.fx * xd + cp.skew * yd + cp.cx;
+  v = cp.fy * yd + cp.cy;
+  // xu = x0 / w, yu = x1 / w with w = x2 + xi |Xc|
+  const double w = x2 + cp.xi * nrm;
+  const double dw[3] = {cp.xi * x0 / nrm, cp.xi * x1 / nrm, 1 + cp.xi * x2 / nrm};
+  const double drad = 2 * (cp.k1 + 2 * cp.k2 * r2);
+  const double a11 = rad + xu * drad * xu + 2 * cp.p1 * yu + 6 * cp.p2 * xu;
+  const double a12 = xu * drad * yu + 2 * cp.p1 * xu + 2 * cp.p2 * yu;
+  const double a21 = yu * drad * xu + 2 * cp.p1 * xu + 2 * cp.p2 * yu;
+  const double a22 = rad + yu * drad * yu + 6 * cp.p1 * yu + 2 * cp.p2 * xu;
+  double gxu[3], gyu[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    gxu[i] = ((i == 0 ? 1.0 : 0.0) - xu * dw[i]) / w;
+    gyu[i] = ((i == 1 ? 1.0 : 0.0) - yu * dw[i]) / w;
+  }
+#pragma unroll
+  for (int jx = 0; jx < 3; ++jx) {
+    const double Gx = gxu[0] * R[jx] + gxu[1] * R[3 + jx] + gxu[2] * R[6 + jx];
+    const double Gy = gyu[0] * R[jx] + gyu[1] * R[3 + jx] + gyu[2] * R[6 + jx];
+    const double dxd = a11 * Gx + a12 * Gy, dyd = a21 * Gx + a22 * Gy;
+    Ju[jx] = cp.fx * dxd + cp.skew * dyd;
+    Jv[jx] = cp.fy * dyd;
+  }
+}
+
+__device__ double block_sum(double v, double* red) {
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int s = OPT_THREADS / 2; s > 0; s >>= 1) {
+    if (t < s) red[t] += red[t + s];
+    __syncthreads();
+  }
+  const double out = red[0];
+  __syncthreads();
+  return out;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Residuals, cost and (mode 0) the Gauss-Newton pieces for one (frame, animal).
+__global__ void __launch_bounds__(OPT_THREADS) optim_eval_kernel(OptDims D, OptBufs Bf, const double* __restrict__ x,
+                                                                  int mode) {
+  const int f = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int J = D.J, J3 = J * 3, F = D.F, n = D.n;
+  __shared__ double sx[OPT_MAXJ * 3];
+  __shared__ double slen[OPT_MAXL][5];
+  __shared__ double ssg[OPT_MAXJ * 3], ssd[OPT_MAXJ * 3];
+  __shared__ double red[OPT_THREADS];
+  const double* xb = x + (size_t)b * D.NV;
+  if (t < J3) sx[t] = xb[(size_t)f * J3 + t];
+  __syncthreads();
+  double cost = 0;
+  const double ssf = Bf.ssf[b];
+  if (t < D.NL) {  // joint-length residuals (cameras.py:1600-1616)
+    const int a = Bf.cons[2 * t], c2 = Bf.cons[2 * t + 1];
+    const double L = xb[D.NX + t];
+    const double s = t < D.nS ? D.s_len : D.s_len_weak;
+    const double dx = sx[3 * a] - sx[3 * c2], dy = sx[3 * a + 1] - sx[3 * c2 + 1], dz = sx[3 * a + 2] - sx[3 * c2 + 2];
+    const double nr = sqrt(dx * dx + dy * dy + dz * dz);
+    const double r = 100 * (nr - L) / L * s;
+    cost += r * r;
+    const double k = nr > 0 ? s * 100 / L / nr : 0.0;
+    slen[t][0] = k * dx;
+    slen[t][1] = k * dy;
+    slen[t][2] = k * dz;
+    slen[t][3] = -s * 100 * nr / (L * L);
+    slen[t][4] = r;
+    if (mode == 0) {
+      double* o = Bf.lenJ + (((size_t)b * F + f) * D.NL + t) * 5;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) o[i] = slen[t][i];
+    }
+  }
+  if (t < J3 && F > n) {  // temporal smoothness (np.diff order n over frames)
+    auto row = [&](int i) {
+      double s = 0;
+      for (int m = 0; m <= n; ++m) s += D.c[m] * xb[(size_t)(i + m) * J3 + t];
+      return s * ssf;
+    };
+    if (f <= F - 1 - n) {
+      const double rs = row(f);
+      cost += rs * rs;
+    }
+    if (mode == 0) {
+      double gs = 0;
+      for (int i = max(0, f - n); i <= min(f, F - 1 - n); ++i) gs += D.c[f - i] * ssf * row(i);
+      ssg[t] = gs;
+      ssd[t] = ssf * ssf * dtd(f, f, F, n, D.c);
+    }
+  } else if (t < J3) {
+    ssg[t] = 0;
+    ssd[t] = 0;
+  }
+  __syncthreads();
+  if (t < J) {  // reprojection, one thread per joint over all cameras
+    double Rm[6] = {0, 0, 0, 0, 0, 0}, gr[3] = {0, 0, 0};
+    const double X[3] = {sx[3 * t], sx[3 * t + 1], sx[3 * t + 2]};
+    for (int c = 0; c < D.C; ++c) {
+      const double* pp = Bf.p2d + ((((size_t)b * D.C + c) * F + f) * J + t) * 2;
+      const double px = pp[0], py = pp[1];
+      if (isnan(px) && isnan(py)) continue;
+      double u, v, Ju[3], Jv[3];
+      project_jac(cam_at(Bf.cams, c), X, u, v, Ju, Jv);
+#pragma unroll
+      for (int comp = 0; comp < 2; ++comp) {
+        const double obs = comp ? py : px;
+        if (isnan(obs)) continue;
+        double r, dr;
+        reproj_loss(obs - (comp ? v : u), D.rp, D.loss, r, dr);
+        cost += r * r;
+        const double* Jp = comp ? Jv : Ju;
+        const double j0 = -dr * Jp[0], j1 = -dr * Jp[1], j2 = -dr * Jp[2];
+        Rm[0] += j0 * j0;
+        Rm[1] += j0 * j1;
+        Rm[2] += j0 * j2;
+        Rm[3] += j1 * j1;
+        Rm[4] += j1 * j2;
+        Rm[5] += j2 * j2;
+        gr[0] += j0 * r;
+        gr[1] += j1 * r;
+        gr[2] += j2 * r;
+      }
+    }
+    if (mode == 0) {
+      double dg[3] = {Rm[0], Rm[3], Rm[5]};
+      for (int k = 0; k < D.NL; ++k) {
+        const int a = Bf.cons[2 * k], c2 = Bf.cons[2 * k + 1];
+        const double sgn = (a == t) ? 1.0 : (c2 == t ? -1.0 : 0.0);
+        if (sgn == 0.0) continue;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          gr[i] += sgn * slen[k][i] * slen[k][4];
+          dg[i] += slen[k][i] * slen[k][i];
+        }
+      }
+      double* Ro = Bf.R + (((size_t)b * F + f) * J + t) * 6;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Ro[i] = Rm[i];
+      const size_t o = (size_t)b * D.NV + (size_t)f * J3 + 3 * t;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        Bf.g[o + i] = gr[i] + ssg[3 * t + i];
+        Bf.diag[o + i] = dg[i] + ssd[3 * t + i];
+      }
+    }
+  }
+  const double tot = block_sum(cost, red);
+  if (t == 0) Bf.costF[(size_t)b * F + f] = tot;
+}
+
+// cost[b] = sum_f costF (fixed order); mode 0 also reduces the length-variable gradient and diagonal.
+__global__ void __launch_bounds__(OPT_THREADS) optim_reduce_kernel(OptDims D, OptBufs Bf, double* cost_out, int mode) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  __shared__ double red[OPT_THREADS];
+  double s = 0;
+  for (int f = t; f < D.F; f += OPT_THREADS) s += Bf.costF[(size_t)b * D.F + f];
+  const double tot = block_sum(s, red);
+  if (t == 0) cost_out[b] = 0.5 * tot;  // scipy's cost convention
+  if (mode == 0 && !D.fix && t < D.NL) {
+    double gL = 0, E = 0;
+    for (int f = 0; f < D.F; ++f) {
+      const double* l = Bf.lenJ + (((size_t)b * D.F + f) * D.NL + t) * 5;
+      gL += l[4] * l[3];
+      E += l[3] * l[3];
+    }
+    Bf.g[(size_t)b * D.NV + D.NX + t] = gL;
+    Bf.diag[(size_t)b * D.NV + D.NX + t] = E;
+  }
+}
+
+__device__ __forceinline__ double damp_of(double dg) { return fmax(dg, 1e-12); }
+
+// Block-banded Cholesky of the per-joint preconditioner (thread per (animal, joint)).
+// fac[((b*J + j)*F + f)*36]: [0..8] inverse of L_ff, [9d .. 9d+8] L_{f,f-d} (d = 1..n).
+__global__ void optim_factor_kernel(OptDims D, OptBufs Bf) {
+  const int b = blockIdx.x, j = threadIdx.x;
+  const int F = D.F, J = D.J, n = D.n;
+  const double lam = Bf.ctl[2 * b];
+  if (j == J) {
+    if (!D.fix)
+      for (int k = 0; k < D.NL; ++k) {
+        const double E = Bf.diag[(size_t)b * D.NV + D.NX + k];
+        Bf.pinvL[(size_t)b * OPT_MAXL + k] = 1.0 / (E + lam * damp_of(E) + 1e-300);
+      }
+    return;
+  }
+  if (j > J) return;
+  const double ssf = Bf.ssf[b];
+  const double s2 = F > n ? ssf * ssf : 0.0;
+  double* fb = Bf.fac + ((size_t)b * J + j) * F * 36;
+  for (int f = 0; f < F; ++f) {
+    const double* Rm = Bf.R + (((size_t)b * F + f) * J + j) * 6;
+    double A[3][3] = {{Rm[0], Rm[1], Rm[2]}, {Rm[1], Rm[3], Rm[4]}, {Rm[2], Rm[4], Rm[5]}};
+    for (int k = 0; k < D.NL; ++k) {
+      const int a = Bf.cons[2 * k], c2 = Bf.cons[2 * k + 1];
+      if (a != j && c2 != j) continue;
+      const double* l = Bf.lenJ + (((size_t)b * F + f) * D.NL + k) * 5;
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) A[r][c] += l[r] * l[c];
+    }
+    const double sd = s2 * dtd(f, f, F, n, D.c);
+    for (int i = 0; i < 3; ++i) {
+      const double dg = Bf.diag[(size_t)b * D.NV + (size_t)f * J * 3 + 3 * j + i];
+      A[i][i] += sd + lam * damp_of(dg);
+    }
+    double* cur = fb + (size_t)f * 36;
+    for (int d = n; d >= 1; --d) {
+      const int i = f - d;
+      if (i < 0) {
+        for (int e = 0; e < 9; ++e) cur[9 * d + e] = 0;
+        continue;
+      }
+      double M[3][3];
+      const double off = s2 * dtd(f, i, F, n, D.c);
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) M[r][c] = (r == c) ? off : 0.0;
+      for (int e = d + 1; e <= n; ++e) {
+        if (f - e < 0) break;
+        const double* Lf = cur + 9 * e;                                 // L_{f, f-e}
+        const double* Li = fb + (size_t)i * 36 + 9 * (e - d);          // L_{i, f-e}
+        for (int r = 0; r < 3; ++r)
+          for (int c = 0; c < 3; ++c)
+            M[r][c] -= Lf[3 * r] * Li[3 * c] + Lf[3 * r + 1] * Li[3 * c + 1] + Lf[3 * r + 2] * Li[3 * c + 2];
+      }
+      const double* Ii = fb + (size_t)i * 36;  // inv(L_ii) (lower)
+      // L_{f,i} = M L_ii^{-T}:  (M Ii^T)[r][c] = sum_k M[r][k] Ii[c][k]
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+          cur[9 * d + 3 * r + c] = M[r][0] * Ii[3 * c] + M[r][1] * Ii[3 * c + 1] + M[r][2] * Ii[3 * c + 2];
+    }
+    for (int d = 1; d <= n; ++d) {
+      if (f - d < 0) break;
+      const double* Lf = cur + 9 * d;
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+          A[r][c] -= Lf[3 * r] * Lf[3 * c] + Lf[3 * r + 1] * Lf[3 * c + 1] + Lf[3 * r + 2] * Lf[3 * c + 2];
+    }
+    // 3x3 Cholesky and its inverse
+    const double l00 = sqrt(fmax(A[0][0], 1e-300));
+    const double l10 = A[1][0] / l00, l20 = A[2][0] / l00;
+    const double l11 = sqrt(fmax(A[1][1] - l10 * l10, 1e-300));
+    const double l21 = (A[2][1] - l20 * l10) / l11;
+    const double l22 = sqrt(fmax(A[2][2] - l20 * l20 - l21 * l21, 1e-300));
+    const double i00 = 1 / l00, i11 = 1 / l11, i22 = 1 / l22;
+    const double i10 = -l10 * i00 * i11;
+    const double i21 = -l21 * i11 * i22;
+    const double i20 = -(l20 * i00 + l21 * i10) * i22;
+    const double inv[9] = {i00, 0, 0, i10, i11, 0, i20, i21, i22};
+    for (int e = 0; e < 9; ++e) cur[e] = inv[e];
+  }
+}
+
+__device__ __forceinline__ double rz_at(const OptDims& D, const OptBufs& Bf, int b, int it) {
+  const double* p = Bf.rzJ + ((size_t)b * (OPT_MAXIT + 1) + it) * (D.J + 1);
+  double s = 0;
+  for (int j = 0; j <= D.J; ++j) s += p[j];
+  return s;
+}
+
+__device__ __forceinline__ bool pcg_done(const OptDims& D, const OptBufs& Bf, int b, int it) {
+  const double r0 = rz_at(D, Bf, b, 0);
+  if (!(r0 > 0)) return true;
+  if (it == 0) return false;
+  const double ri = rz_at(D, Bf, b, it);
+  return !(ri > D.tol2 * r0);
+}
+
+// z = M^-1 r for one joint series (and the length diagonal for j == J); it < 0: init (d = 0, r = -g),
+// else first d += alpha p_it, r -= alpha q_it.  Writes the series' r.z partial to rzJ[it + 1].
+__global__ void optim_precond_kernel(OptDims D, OptBufs Bf, int it) {
+  const int b = blockIdx.x, j = threadIdx.x;
+  const int F = D.F, J = D.J, n = D.n, J3 = 3 * J;
+  if (j > J) return;
+  double alpha = 0;
+  const double* P = (it & 1) ? Bf.P1 : Bf.P0;
+  if (it >= 0) {
+    if (pcg_done(D, Bf, b, it)) return;
+    const double pq = Bf.pq[(size_t)b * (OPT_MAXIT + 1) + it];
+    if (!(pq > 0)) return;
+    alpha = rz_at(D, Bf, b, it) / pq;
+  }
+  const size_t base = (size_t)b * D.NV;
+  double rz = 0;
+  if (j == J) {
+    if (!D.fix)
+      for (int k = 0; k < D.NL; ++k) {
+        const size_t o = base + D.NX + k;
+        double r;
+        if (it < 0) {
+          Bf.d[o] = 0;
+          r = -Bf.g[o];
+        } else {
+          Bf.d[o] += alpha * P[o];
+          r = Bf.r[o] - alpha * Bf.q[o];
+        }
+        Bf.r[o] = r;
+        const double z = r * Bf.pinvL[(size_t)b * OPT_MAXL + k];
+        Bf.z[o] = z;
+        rz += r * z;
+      }
+  } else {
+    const double* fb = Bf.fac + ((size_t)b * J + j) * F * 36;
+    for (int f = 0; f < F; ++f) {  // forward: L y = r
+      const size_t o = base + (size_t)f * J3 + 3 * j;
+      double r[3];
+      for (int i = 0; i < 3; ++i) {
+        if (it < 0) {
+          Bf.d[o + i] = 0;
+          r[i] = -Bf.g[o + i];
+        } else {
+          Bf.d[o + i] += alpha * P[o + i];
+          r[i] = Bf.r[o + i] - alpha * Bf.q[o + i];
+        }
+        Bf.r[o + i] = r[i];
+      }
+      double w[3] = {r[0], r[1], r[2]};
+      const double* cur = fb + (size_t)f * 36;
+      for (int d = 1; d <= n && f - d >= 0; ++d) {
+        const double* y = Bf.z + base + (size_t)(f - d) * J3 + 3 * j;
+        const double* Lf = cur + 9 * d;
+        for (int i = 0; i < 3; ++i) w[i] -= Lf[3 * i] * y[0] + Lf[3 * i + 1] * y[1] + Lf[3 * i + 2] * y[2];
+      }
+      double* y = Bf.z + o;
+      y[0] = cur[0] * w[0];
+      y[1] = cur[3] * w[0] + cur[4] * w[1];
+      y[2] = cur[6] * w[0] + cur[7] * w[1] + cur[8] * w[2];
+    }
+    for (int f = F - 1; f >= 0; --f) {  // backward: L^T z = y
+      const size_t o = base + (size_t)f * J3 + 3 * j;
+      double w[3] = {Bf.z[o], Bf.z[o + 1], Bf.z[o + 2]};
+      for (int d = 1; d <= n && f + d < F; ++d) {
+        const double* zz = Bf.z + base + (size_t)(f + d) * J3 + 3 * j;
+        const double* Ld = fb + (size_t)(f + d) * 36 + 9 * d;  // L_{f+d, f}
+        for (int i = 0; i < 3; ++i) w[i] -= Ld[i] * zz[0] + Ld[3 + i] * zz[1] + Ld[6 + i] * zz[2];
+      }
+      const double* I = fb + (size_t)f * 36;  // z = I^T w
+      const double z0 = I[0] * w[0] + I[3] * w[1] + I[6] * w[2];
+      const double z1 = I[4] * w[1] + I[7] * w[2];
+      const double z2 = I[8] * w[2];
+      Bf.z[o] = z0;
+      Bf.z[o + 1] = z1;
+      Bf.z[o + 2] = z2;
+      rz += Bf.r[o] * z0 + Bf.r[o + 1] * z1 + Bf.r[o + 2] * z2;
+    }
+  }
+  Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
+}
+
+// q = (H + lam diag(H)) p_it with p_it = z + beta p_{it-1} (computed here, written to P[it & 1]).
+__global__ void __launch_bounds__(OPT_THREADS) optim_matvec_kernel(OptDims D, OptBufs Bf, int it) {
+  const int f = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int F = D.F, J = D.J, J3 = 3 * J, n = D.n;
+  if (pcg_done(D, Bf, b, it)) return;
+  __shared__ double sp[2 * OPT_MAXN + 1][OPT_MAXJ * 3];
+  __shared__ double spL[OPT_MAXL], stk[OPT_MAXL];
+  __shared__ double red[OPT_THREADS];
+  const double beta = it == 0 ? 0.0 : rz_at(D, Bf, b, it) / rz_at(D, Bf, b, it - 1);
+  double* Pc = (it & 1) ? Bf.P1 : Bf.P0;
+  const double* Pp = (it & 1) ? Bf.P0 : Bf.P1;
+  const size_t base = (size_t)b * D.NV;
+  const double lam = Bf.ctl[2 * b];
+  if (t < J3) {
+    for (int df = -n; df <= n; ++df) {
+      const int ff = f + df;
+      if (ff < 0 || ff >= F) continue;
+      const size_t o = base + (size_t)ff * J3 + t;
+      const double p = it == 0 ? Bf.z[o] : Bf.z[o] + beta * Pp[o];
+      sp[df + n][t] = p;
+      if (df == 0) Pc[o] = p;
+    }
+  }
+  if (t < D.NL) {
+    double p = 0;
+    if (!D.fix) {
+      const size_t o = base + D.NX + t;
+      p = it == 0 ? Bf.z[o] : Bf.z[o] + beta * Pp[o];
+      if (f == 0) Pc[o] = p;
+    }
+    spL[t] = p;
+  }
+  __syncthreads();
+  const double* p0 = sp[n];
+  if (t < D.NL) {
+    const double* l = Bf.lenJ + (((size_t)b * F + f) * D.NL + t) * 5;
+    const int a = Bf.cons[2 * t], c2 = Bf.cons[2 * t + 1];
+    const double tk = l[0] * (p0[3 * a] - p0[3 * c2]) + l[1] * (p0[3 * a + 1] - p0[3 * c2 + 1]) +
+                      l[2] * (p0[3 * a + 2] - p0[3 * c2 + 2]) + l[3] * spL[t];
+    stk[t] = tk;
+    if (!D.fix) Bf.qLf[((size_t)b * F + f) * D.NL + t] = l[3] * tk;
+  }
+  __syncthreads();
+  double pq = 0;
+  if (t < J3) {
+    const int j = t / 3, comp = t % 3;
+    const double* Rm = Bf.R + (((size_t)b * F + f) * J + j) * 6;
+    const int ix[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+    double q = Rm[ix[comp][0]] * p0[3 * j] + Rm[ix[comp][1]] * p0[3 * j + 1] + Rm[ix[comp][2]] * p0[3 * j + 2];
+    for (int k = 0; k < D.NL; ++k) {
+      const int a = Bf.cons[2 * k], c2 = Bf.cons[2 * k + 1];
+      if (a != j && c2 != j) continue;
+      const double gk = Bf.lenJ[(((size_t)b * F + f) * D.NL + k) * 5 + comp];
+      q += (a == j ? gk : -gk) * stk[k];
+    }
+    if (F > n) {
+      const double s2 = Bf.ssf[b] * Bf.ssf[b];
+      for (int df = -n; df <= n; ++df) {
+        const int ff = f + df;
+        if (ff < 0 || ff >= F) continue;
+        q += s2 * dtd(f, ff, F, n, D.c) * sp[df + n][t];
+      }
+    }
+    const size_t o = base + (size_t)f * J3 + t;
+    q += lam * damp_of(Bf.diag[o]) * p0[t];
+    Bf.q[o] = q;
+    pq = p0[t] * q;
+  }
+  const double tot = block_sum(pq, red);
+  if (t == 0) Bf.pqF[(size_t)b * F + f] = tot;
+}
+
+// Length part of q and the full p.q (fixed-order reductions over frames).
+__global__ void __launch_bounds__(OPT_THREADS) optim_reduce_pq_kernel(OptDims D, OptBufs Bf, int it) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (pcg_done(D, Bf, b, it)) return;
+  __shared__ double red[OPT_THREADS];
+  const double* P = (it & 1) ? Bf.P1 : Bf.P0;
+  const size_t base = (size_t)b * D.NV;
+  double s = 0;
+  for (int f = t; f < D.F; f += OPT_THREADS) s += Bf.pqF[(size_t)b * D.F + f];
+  if (!D.fix && t < D.NL) {
+    double qL = 0;
+    for (int f = 0; f < D.F; ++f) qL += Bf.qLf[((size_t)b * D.F + f) * D.NL + t];
+    const size_t o = base + D.NX + t;
+    qL += Bf.ctl[2 * b] * damp_of(Bf.diag[o]) * P[o];
+    Bf.q[o] = qL;
+    s += P[o] * qL;
+  }
+  const double tot = block_sum(s, red);
+  if (t == 0) Bf.pq[(size_t)b * (OPT_MAXIT + 1) + it] = tot;
+}
+
+__global__ void optim_axpy_kernel(const double* x, const double* d, double* xt, int NX, int NV, int B, int fix) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)B * NV) return;
+  const int k = (int)(i % NV);
+  xt[i] = (fix && k >= NX) ? x[i] : x[i] + d[i];
+}
+
+__global__ void optim_accept_kernel(double* x, const double* xt, const double* ctl, int NV, int B) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)B * NV) return;
+  if (ctl[2 * (i / NV) + 1] != 0.0) x[i] = xt[i];
+}
+
+}  // namespace
+
+int g_optim_pcg_iters = 40;
+
+size_t optim_workspace_bytes(int B, int F, int J, int NL) {
+  const size_t NV = (size_t)F * J * 3 + NL;
+  size_t n = 0;
+  n += (size_t)B * NV * 9;                       // g diag d r z P0 P1 q xt
+  n += (size_t)B * F * J * 6;                    // R
+  n += (size_t)B * F * NL * 5;                   // lenJ
+  n += (size_t)B * F * 2;                        // costF pqF
+  n += (size_t)B * F * NL;                       // qLf
+  n += (size_t)B * J * F * 36 + (size_t)B * OPT_MAXL;  // fac pinvL
+  n += (size_t)B * (OPT_MAXIT + 1) * (J + 2);    // rzJ, pq
+  n += (size_t)B * 4;                            // cost, cost_t, ctl(2)
+  n += (size_t)NL + 2 + B;                       // constraint pairs (int32), ssf
+  return n * sizeof(double);
+}
+
+// Host driver.  x: device (B, NV) in/out.  cons/ssf/stats: host.  ws: device workspace of
+// optim_workspace_bytes().  stats[b*4 + {0,1,2,3}] = initial cost, final cost, LM iterations, status
+// (1 ftol, 2 max_iter, 3 damping overflow).
+int optim_points(const double* cams, int C, const double* p2d, double* x, int B, int F, int J, const int* cons_host,
+                 int n_strong, int n_weak, const double* ssf_host, double scale_length, double scale_length_weak,
+                 double rp, int loss, int n_deriv, int fix_lengths, int max_iter, double ftol, void* ws,
+                 double* stats, hipStream_t s) {
+  const int NL = n_strong + n_weak;
+  if (B <= 0 || F <= 0 || J <= 0) return 0;
+  if (J > OPT_MAXJ || NL > OPT_MAXL || C > OPT_MAXC || C < 1 || n_deriv < 1 || n_deriv > OPT_MAXN) return -2;
+  OptDims D{};
+  D.B = B;
+  D.C = C;
+  D.F = F;
+  D.J = J;
+  D.NL = NL;
+  D.nS = n_strong;
+  D.fix = fix_lengths;
+  D.n = n_deriv;
+  D.loss = loss;
+  D.NX = F * J * 3;
+  D.NV = D.NX + NL;
+  D.rp = rp;
+  D.s_len = scale_length;
+  D.s_len_weak = scale_length_weak;
+  D.tol2 = 1e-10;
+  {  // np.diff(., n) coefficients: (-1)^(n-m) C(n, m)
+    int binom = 1;
+    for (int m = 0; m <= n_deriv; ++m) {
+      D.c[m] = (((n_deriv - m) & 1) ? -1.0 : 1.0) * binom;
+      binom = binom * (n_deriv - m) / (m + 1);
+    }
+  }
+  const size_t NVB = (size_t)B * D.NV;
+  double* w = static_cast<double*>(ws);
+  OptBufs Bf{};
+  auto take = [&](size_t cnt) {
+    double* p = w;
+    w += cnt;
+    return p;
+  };
+  Bf.g = take(NVB);
+  Bf.diag = take(NVB);
+  Bf.d = take(NVB);
+  Bf.r = take(NVB);
+  Bf.z = take(NVB);
+  Bf.P0 = take(NVB);
+  Bf.P1 = take(NVB);
+  Bf.q = take(NVB);
+  double* xt = take(NVB);
+  Bf.R = take((size_t)B * F * J * 6);
+  Bf.lenJ = take((size_t)B * F * NL * 5);
+  Bf.costF = take((size_t)B * F);
+  Bf.pqF = take((size_t)B * F);
+  Bf.qLf = take((size_t)B * F * NL);
+  Bf.fac = take((size_t)B * J * F * 36);
+  Bf.pinvL = take((size_t)B * OPT_MAXL);
+  Bf.rzJ = take((size_t)B * (OPT_MAXIT + 1) * (J + 1));
+  Bf.pq = take((size_t)B * (OPT_MAXIT + 1));
+  Bf.cost = take(B);
+  double* cost_t = take(B);
+  double* ctl = take(2 * (size_t)B);
+  Bf.ctl = ctl;
+  Bf.cams = cams;
+  Bf.p2d = p2d;
+  // small host-side inputs go to the device through the workspace tail
+  int* cons_d = reinterpret_cast<int*>(take((NL * 2 + 1) / 2 + 1));
+  double* ssf_d = take(B);
+  Bf.cons = cons_d;
+  Bf.ssf = ssf_d;
+  if (hipMemcpyAsync(cons_d, cons_host, sizeof(int) * 2 * NL, hipMemcpyHostToDevice, s) != hipSuccess) return -3;
+  if (hipMemcpyAsync(ssf_d, ssf_host, sizeof(double) * B, hipMemcpyHostToDevice, s) != hipSuccess) return -3;
+
+  const int npcg = std::max(1, std::min(g_optim_pcg_iters, OPT_MAXIT));
+  const dim3 gridFB(F, B);
+  const int ew_blocks = (int)((NVB + 255) / 256);
+  std::vector<double> lam(B, 1e-3), cost(B), costt(B), hctl(2 * B, 0.0);
+  std::vector<int> active(B, 1), iters(B, 0), status(B, 2);
+
+  auto eval = [&](const double* xx, int mode, double* out) {
+    hipLaunchKernelGGL(optim_eval_kernel, gridFB, dim3(OPT_THREADS), 0, s, D, Bf, xx, mode);
+    hipLaunchKernelGGL(optim_reduce_kernel, dim3(B), dim3(OPT_THREADS), 0, s, D, Bf, out, mode);
+  };
+  eval(x, 0, Bf.cost);
+  if (hipMemcpyAsync(cost.data(), Bf.cost, sizeof(double) * B, hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
+  if (hipStreamSynchronize(s) != hipSuccess) return -3;
+  for (int b = 0; b < B; ++b) {
+    stats[4 * b + 0] = cost[b];
+    if (!(cost[b] > 0)) {  // already exact (or NaN input): nothing to do
+      active[b] = 0;
+      status[b] = 1;
+    }
+  }
+  for (int iter = 0; iter < max_iter; ++iter) {
+    bool any = false;
+    for (int b = 0; b < B; ++b) any |= active[b] != 0;
+    if (!any) break;
+    for (int b = 0; b < B; ++b) {
+      hctl[2 * b] = lam[b];
+      hctl[2 * b + 1] = 0;
+    }
+    if (hipMemcpyAsync(ctl, hctl.data(), sizeof(double) * 2 * B, hipMemcpyHostToDevice, s) != hipSuccess) return -3;
+    (void)hipMemsetAsync(Bf.rzJ, 0, sizeof(double) * (size_t)B * (OPT_MAXIT + 1) * (J + 2), s);
+    hipLaunchKernelGGL(optim_factor_kernel, dim3(B), dim3(64), 0, s, D, Bf);
+    hipLaunchKernelGGL(optim_precond_kernel, dim3(B), dim3(64), 0, s, D, Bf, -1);
+    for (int it = 0; it < npcg; ++it) {
+      hipLaunchKernelGGL(optim_matvec_kernel, gridFB, dim3(OPT_THREADS), 0, s, D, Bf, it);
+      hipLaunchKernelGGL(optim_reduce_pq_kernel, dim3(B), dim3(OPT_THREADS), 0, s, D, Bf, it);
+      hipLaunchKernelGGL(optim_precond_kernel, dim3(B), dim3(64), 0, s, D, Bf, it);
+    }
+    hipLaunchKernelGGL(optim_axpy_kernel, dim3(ew_blocks), dim3(256), 0, s, x, Bf.d, xt, D.NX, D.NV, B, D.fix);
+    eval(xt, 1, cost_t);
+    if (hipMemcpyAsync(costt.data(), cost_t, sizeof(double) * B, hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
+    if (hipStreamSynchronize(s) != hipSuccess) return -3;
+    bool accepted_any = false;
+    for (int b = 0; b < B; ++b) {
+      if (!active[b]) continue;
+      iters[b]++;
+      if (costt[b] < cost[b]) {  // accept
+        const double dF = cost[b] - costt[b];
+        hctl[2 * b + 1] = 1;
+        accepted_any = true;
+        if (dF < ftol * cost[b]) {  // scipy's ftol test on an accepted step
+          active[b] = 0;
+          status[b] = 1;
+        }
+        cost[b] = costt[b];
+        lam[b] = std::max(lam[b] / 3.0, 1e-12);
+      } else {
+        lam[b] *= 4.0;
+        if (lam[b] > 1e12) {
+          active[b] = 0;
+          status[b] = 3;
+        }
+      }
+    }
+    if (accepted_any) {
+      if (hipMemcpyAsync(ctl, hctl.data(), sizeof(double) * 2 * B, hipMemcpyHostToDevice, s) != hipSuccess) return -3;
+      hipLaunchKernelGGL(optim_accept_kernel, dim3(ew_blocks), dim3(256), 0, s, x, xt, ctl, D.NV, B);
+      eval(x, 0, Bf.cost);
+    }
+  }
+  if (hipStreamSynchronize(s) != hipSuccess) return -3;
+  for (int b = 0; b < B; ++b) {
+    stats[4 * b + 1] = cost[b];
+    stats[4 * b + 2] = iters[b];
+    stats[4 * b + 3] = status[b];
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+}  // namespace mq

@@ -46,6 +46,15 @@ class OmnidirCamera:
         self.K = np.zeros((3, 3)) if K is None else np.asarray(K, dtype=np.float64)
         self.D = np.zeros(4) if D is None else np.asarray(D, dtype=np.float64).ravel()
         self.name = None if name is None else str(name)
+        self.R = None  # explicit rotation (from_projection); otherwise rodrigues(rvec)
+
+    @staticmethod
+    def from_projection(P, name=None):
+        """A camera whose extrinsics are the given 3x4 [R|t] (multicam_toolbox pmat)."""
+        P = np.asarray(P, dtype=np.float64)
+        cam = OmnidirCamera(tvec=P[:, 3], name=name)
+        cam.R = P[:, :3].copy()
+        return cam
 
     @staticmethod
     def from_dict(d):
@@ -58,7 +67,7 @@ class OmnidirCamera:
 
     def get_extrinsics_mat(self):
         M = np.eye(4)
-        M[:3, :3] = rodrigues(self.rvec)
+        M[:3, :3] = rodrigues(self.rvec) if self.R is None else self.R
         M[:3, 3] = self.tvec
         return M
 
@@ -66,7 +75,7 @@ class OmnidirCamera:
         row = np.zeros(24)
         row[0:6] = [self.K[0, 0], self.K[1, 1], self.K[0, 1], self.K[0, 2], self.K[1, 2], float(self.xi[0])]
         row[6:10] = self.D[:4]
-        row[10:19] = rodrigues(self.rvec).ravel()
+        row[10:19] = (rodrigues(self.rvec) if self.R is None else self.R).ravel()
         row[19:22] = self.tvec[:3]
         return row
 
@@ -228,7 +237,22 @@ class CameraGroup:
         return optim_points_gpu(self, points, p3ds, constraints=constraints, constraints_weak=constraints_weak,
                                 scale_smooth=scale_smooth, scale_length=scale_length,
                                 scale_length_weak=scale_length_weak, reproj_error_threshold=reproj_error_threshold,
-                                reproj_loss=reproj_loss, n_deriv_smooth=n_deriv_smooth, verbose=verbose)
+                                reproj_loss=reproj_loss, n_deriv_smooth=n_deriv_smooth, scores=scores,
+                                verbose=verbose)
+
+    def optim_points_jointlenfix(self, points, p3ds, joint_len, constraints=(), constraints_weak=(), scale_smooth=4,
+                                 scale_length=2, scale_length_weak=0.5, reproj_error_threshold=15,
+                                 reproj_loss='soft_l1', n_deriv_smooth=1, scores=None, verbose=False):
+        """cameras.py:1192-1415: lengths fixed to joint_len, p3d only; the reference caps scipy at
+        max_nfev=15, mirrored here as at most 15 Levenberg-Marquardt steps."""
+        from .optim import optim_points_gpu
+        joint_len = np.asarray(joint_len, dtype=np.float64).ravel()
+        p3, _ = optim_points_gpu(self, points, p3ds, constraints=constraints, constraints_weak=constraints_weak,
+                                 scale_smooth=scale_smooth, scale_length=scale_length,
+                                 scale_length_weak=scale_length_weak, reproj_error_threshold=reproj_error_threshold,
+                                 reproj_loss=reproj_loss, n_deriv_smooth=n_deriv_smooth, scores=scores,
+                                 verbose=verbose, joint_len=joint_len, max_iter=15)
+        return p3, joint_len
 
 
 def triangulate_pinv(cams: CameraGroup, und, frame_use):

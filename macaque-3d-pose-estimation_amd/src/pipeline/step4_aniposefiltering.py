@@ -1,0 +1,225 @@
+"""Step 4 -- 2D Viterbi filtering + anipose 3D lift, on MI355X (row a18 glue).
+
+Mirrors ``src/pipeline/step4_aniposefiltering.py`` of the reference: same
+``proc(data_name, results_dir_root, config_path, n_kp, redo)`` entry point, same
+files in and out (``kp2d.pickle`` -> ``kp2d_f.pickle``, ``calibration.toml``,
+``config.toml``, ``joint_len.npy``, ``kp3d.pickle`` / ``kp3d_fxdJointLen.pickle``)
+and the same numbers, but batched MI355X-first:
+
+* the Viterbi filter runs every (animal, camera, joint) chain in one launch
+  (reference: a spawn pool per animal x camera, step4:145-167);
+* initial triangulation / RANSAC / reprojection errors run over all animals'
+  points in one launch each (reference: per animal, per point);
+* optim_points refines all animals in one batched LM solve (reference: scipy
+  per animal).
+
+Calibration: if the reference's ``cam_intrinsic.h5`` / ``cam_extrinsic_optim.h5``
+sit next to ``config_path`` and h5py is importable, ``calibration.toml`` is
+rebuilt from them as in step4:101-138; otherwise an existing
+``<result_dir>/calibration.toml`` is used.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import yaml
+
+from mqhip import io as mqio
+from mqhip.geometry import CameraGroup, viterbi_filter
+
+BODYPARTS = ['nose', 'left_eye', 'right_eye', 'left_ear', 'right_ear',
+             'left_shoulder', 'right_shoulder', 'left_elbow', 'right_elbow',
+             'left_wrist', 'right_wrist', 'left_hip', 'right_hip',
+             'left_knee', 'right_knee', 'left_ankle', 'right_ankle']
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+CONFIG_TMPL = os.path.join(_HERE, "..", "..", "configs", "config_tmpl.toml")
+
+# step4:142-147 -- the filter settings are hard-coded there, not read from the TOML
+FILTER_CONFIG = {"filter": {"score_threshold": 0.3, "n_back": 3, "offset_threshold": 25, "multiprocessing": True}}
+
+
+def load_constraints(config, bodyparts, key='constraints'):
+    """step4:40-49: bodypart-name pairs -> index pairs (AssertionError on unknown names)."""
+    names = config['triangulation'].get(key, [])
+    idx = {b: i for i, b in enumerate(bodyparts)}
+    out = []
+    for a, b in names:
+        assert a in idx, 'Bodypart {} from constraints not found in list of bodyparts'.format(a)
+        assert b in idx, 'Bodypart {} from constraints not found in list of bodyparts'.format(b)
+        out.append([idx[a], idx[b]])
+    return out
+
+
+def _median_valid(p3, ix):
+    pts = p3[:, ix]
+    pts = pts[~np.isnan(pts[:, 0])]
+    return np.median(pts, axis=0)
+
+
+def correct_coordinate_frame(config, all_points_3d, bodyparts):
+    """step4:51-87: rotate/translate into the frame named by triangulation.reference_point / axes."""
+    bp = {b: i for i, b in enumerate(bodyparts)}
+    axis_of = {'x': 0, 'y': 1, 'z': 2}
+    ref = config['triangulation']['reference_point']
+    (ad, al, ar), (bd, bl, br) = config['triangulation']['axes'][:2]
+    a_dir, b_dir = axis_of[ad], axis_of[bd]
+    c_dir = [i for i in range(3) if i not in (a_dir, b_dir)][0]
+    a_vec = _median_valid(all_points_3d, bp[ar]) - _median_valid(all_points_3d, bp[al])
+    b_raw = _median_valid(all_points_3d, bp[br]) - _median_valid(all_points_3d, bp[bl])
+    b_vec = b_raw - a_vec * np.dot(b_raw, a_vec) / np.dot(a_vec, a_vec)
+    M = np.zeros((3, 3))
+    M[a_dir], M[b_dir] = a_vec, b_vec
+    M[c_dir] = np.cross(a_vec, b_vec) if (a_dir, b_dir) in [(0, 1), (2, 0), (1, 2)] else np.cross(b_vec, a_vec)
+    M /= np.linalg.norm(M, axis=1)[:, None]
+    adj = all_points_3d.dot(M.T)
+    center = _median_valid(adj, bp[ref])
+    return adj - center, M, center
+
+
+def write_calibration(config_path, result_dir, cam_ids):
+    """step4:101-138: calibration.toml from the h5 intrinsics/extrinsics (needs h5py)."""
+    import h5py  # absent in this image; only reached when the h5 files exist
+    base = os.path.dirname(config_path)
+    calib = {}
+    with h5py.File(os.path.join(base, 'cam_intrinsic.h5'), 'r') as f:
+        for i, k in enumerate(cam_ids):
+            mtx = f[k]['mtx'][()]
+            mtx[:2, :] /= 2
+            calib[f'cam_{i}'] = {
+                'name': k, 'size': [2048, 1536], 'matrix': mtx.tolist(),
+                'distortions': f[k]['dist'][()].ravel().tolist(), 'xi': f[k]['xi'][()].ravel().tolist(),
+                'K': f[k]['K'][()].tolist(), 'D': f[k]['D'][()].ravel().tolist(),
+                'fisheye': False, 'omnidir': True}
+    with h5py.File(os.path.join(base, 'cam_extrinsic_optim.h5'), 'r') as f:
+        for i, k in enumerate(cam_ids):
+            calib[f'cam_{i}']['rotation'] = f[k]['rvec'][()].ravel().tolist()
+            calib[f'cam_{i}']['translation'] = f[k]['tvec'][()].ravel().tolist()
+    mqio.dump_toml(calib, os.path.join(result_dir, 'calibration.toml'))
+
+
+def filter_2d(kp2d, filter_config=FILTER_CONFIG, device: int = 0):
+    """step4:140-170: kp2d (A,F,C,J,3) -> kp2d_f (F,J,A,3,C) (filtered points + Viterbi scores)."""
+    fc = filter_config['filter']
+    out = viterbi_filter(kp2d, score_threshold=fc['score_threshold'], n_back=fc['n_back'],
+                         offset_threshold=fc['offset_threshold'], device=device)
+    return np.ascontiguousarray(out.transpose(1, 3, 0, 4, 2))
+
+
+def reconstruct_3d(kp2d_f, cgroup, config, bodyparts=BODYPARTS, joint_len_median=None, verbose=False):
+    """step4:185-331 for all animals at once.  kp2d_f (F,J,A,3,C) ->
+    (kp3d (A,F,J,3), S (A,F,J), E (A,F,J), joint_len list)."""
+    tri = config['triangulation']
+    n_frame, n_kp, n_animal, _, n_cam = kp2d_f.shape
+    kp = np.array(kp2d_f.transpose((2, 4, 0, 1, 3)), dtype=np.float64)   # (A,C,F,J,3)
+    pts_raw = kp[..., :2].copy()
+    scores = kp[..., 2].copy()
+    pts_raw[scores < tri['score_threshold']] = np.nan
+    kp3d = np.zeros((n_animal, n_frame, n_kp, 3))
+    S = np.zeros((n_animal, n_frame, n_kp))
+    E = np.zeros((n_animal, n_frame, n_kp))
+    joint_len = []
+    # (C, A*F*J, 2): every animal's points in one launch; per-point results are independent
+    flat = np.ascontiguousarray(pts_raw.transpose(1, 0, 2, 3, 4).reshape(n_cam, -1, 2))
+    good = ~np.isnan(pts_raw[..., 0])                                     # (A,C,F,J)
+    if tri['optim']:
+        cons = load_constraints(config, bodyparts)
+        weak = load_constraints(config, bodyparts, 'constraints_weak')
+        if tri['ransac']:
+            init = cgroup.triangulate_ransac(flat)[0]
+        else:
+            init = cgroup.triangulate(flat)
+        init = init.reshape(n_animal, n_frame, n_kp, 3)
+        p3 = init.copy()
+        run = [a for a in range(n_animal) if np.sum(np.isfinite(init[a, :, :, 0])) >= 20]
+        for a in range(n_animal):
+            if a not in run:
+                print("warning: not enough 3D points to run optimization")
+        if run:
+            from mqhip.optim import optim_points_batch
+            jl_fix = None if joint_len_median is None else np.asarray(joint_len_median, dtype=np.float64)
+            res, jls = optim_points_batch(
+                cgroup, pts_raw[run], init[run], cons, weak, scale_smooth=tri['scale_smooth'],
+                scale_length=tri['scale_length'], scale_length_weak=tri['scale_length_weak'],
+                reproj_error_threshold=tri['reproj_error_threshold'], n_deriv_smooth=tri['n_deriv_smooth'],
+                joint_len=jl_fix, max_iter=200 if jl_fix is None else 15, verbose=verbose)
+            for i, a in enumerate(run):
+                p3[a] = res[i]
+                joint_len.append(jls[i] if jl_fix is None else jl_fix)
+        p3_flat = np.ascontiguousarray(p3.reshape(-1, 3))
+        err = cgroup.reprojection_error(p3_flat, flat, mean=True).reshape(n_animal, n_frame, n_kp)
+        num_cams = good.sum(axis=1).astype(float)                         # (A,F,J)
+        sc = scores.copy()
+        sc[~good] = 2
+        s3 = sc.min(axis=1)
+        s3[num_cams < 1] = np.nan
+        err[num_cams < 1] = np.nan
+    else:
+        if tri['ransac']:
+            p3, picked, p2s, err = cgroup.triangulate_ransac(flat, min_cams=3)
+            p2s = p2s.reshape(n_cam, n_animal, n_frame, n_kp, 2).transpose(1, 0, 2, 3, 4)
+            good = ~np.isnan(p2s[..., 0])
+            num_cams = picked.reshape(n_cam, n_animal, n_frame, n_kp).sum(axis=0).astype(float)
+        else:
+            p3 = cgroup.triangulate(flat)
+            err = cgroup.reprojection_error(p3, flat, mean=True)
+            num_cams = good.sum(axis=1).astype(float)
+        p3 = p3.reshape(n_animal, n_frame, n_kp, 3)
+        err = np.asarray(err, dtype=np.float64).reshape(n_animal, n_frame, n_kp)
+        sc = scores.copy()
+        sc[~good] = 2
+        s3 = sc.min(axis=1)
+        s3[num_cams < 2] = np.nan
+        err[num_cams < 2] = np.nan
+    for a in range(n_animal):
+        if 'reference_point' in tri and 'axes' in tri:
+            kp3d[a] = correct_coordinate_frame(config, p3[a], bodyparts)[0]
+        else:
+            kp3d[a] = p3[a]
+        S[a] = s3[a]
+        E[a] = err[a]
+    return kp3d, S, E, joint_len
+
+
+def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int = 0, verbose=False):
+    """step4_aniposefiltering.proc (step4:89)."""
+    result_dir = results_dir_root + '/' + data_name
+    fixed = os.path.exists(os.path.dirname(config_path) + '/joint_len.npy')
+    out_name = 'kp3d_fxdJointLen.pickle' if fixed else 'kp3d.pickle'
+    if os.path.exists(os.path.join(result_dir, out_name)) and not redo:
+        print(f'Skip as exist:{data_name:s}/{out_name}')
+        return
+
+    # ---- configuration + calibration (step4:101-138)
+    config = mqio.load_toml(CONFIG_TMPL)
+    config['model_folder'] = os.path.abspath(os.path.dirname(result_dir))
+    mqio.dump_toml(config, result_dir + '/config.toml')
+    with open(config_path, 'r') as f:
+        cam_ids = [str(i) for i in yaml.safe_load(f)['camera_id']]
+    h5_in = os.path.dirname(config_path) + '/cam_intrinsic.h5'
+    if os.path.exists(h5_in):
+        write_calibration(config_path, result_dir, cam_ids)
+    elif not os.path.exists(result_dir + '/calibration.toml'):
+        raise FileNotFoundError(f'need {h5_in} (+ h5py) or {result_dir}/calibration.toml')
+
+    # ---- 2D filtering (step4:140-170)
+    print('##### 2D filtering....', flush=True)
+    kp2d = np.asarray(mqio.load_array_pickle(result_dir + '/kp2d.pickle'), dtype=np.float64)
+    kp2d_f = filter_2d(kp2d, device=device)
+    mqio.dump_pickle(kp2d_f, result_dir + '/kp2d_f.pickle')
+
+    # ---- 3D reconstruction (step4:172-339)
+    print('##### 3D reconstruction....', flush=True)
+    joint_len_median = None
+    if fixed:
+        joint_len_median = np.median(np.load(os.path.dirname(config_path) + '/joint_len.npy'), axis=0)
+    config = mqio.load_toml(result_dir + '/config.toml')
+    cgroup = CameraGroup.load(result_dir + '/calibration.toml', device=device).subset_cameras_names(cam_ids)
+    kp3d, S, E, joint_len = reconstruct_3d(kp2d_f, cgroup, config, joint_len_median=joint_len_median,
+                                           verbose=verbose)
+    if config['triangulation']['optim']:
+        np.save(result_dir + '/joint_len.npy', np.array(joint_len))
+    data = {'kp3d': kp3d, 'kp3d_score': S, 'kp3d_err': E, 'joint_len': joint_len}
+    mqio.dump_pickle(data, os.path.join(result_dir, out_name))
+    return data

@@ -1,0 +1,117 @@
+"""GPU optim_points (mq_optim_points) vs the scipy-TRF oracle (row a16).
+
+Tolerance: the GPU solution must lie within
+max(|scipy(ftol=1e-3) - scipy(ftol=1e-10)| band, 1 mm median / 5 mm p99) of the
+scipy result run with the reference's own arguments (cameras.py:1166-1180,
+step4:248-258 / config_tmpl.toml:89-97).  The objective is also checked
+directly: evaluated by the oracle's residual function, the GPU optimum may not
+be worse than scipy's by more than 0.1 %.  Parity is pinned to the oracle only
+(scipy least_squares is unpinned by the reference).
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+ARGS = dict(scale_smooth=3, scale_length=5, scale_length_weak=2, n_deriv_smooth=2, reproj_error_threshold=3)
+
+
+def _problem(F, drop=0.1, gap=False, seed=3):
+    from mqhip import synth
+    from oracle.geometry import CameraGroupOracle
+    cams = synth.make_cameras(8)
+    skel = synth.make_skeletons(1, F)
+    kp2d = synth.make_kp2d(cams, skel, noise_px=2.0, drop=drop, seed=seed)
+    o = CameraGroupOracle(cams)
+    pts = kp2d[0].transpose(1, 0, 2, 3)
+    p2 = pts[..., :2].copy()
+    p2[pts[..., 2] < 0.5] = np.nan
+    if gap:
+        p2[:, F // 3:F // 3 + 8, 9] = np.nan      # left wrist unseen for 8 frames
+        p2[:6, :, 15] = np.nan                    # left ankle seen by 2 cameras only
+    init = o.triangulate(p2.reshape(8, -1, 2)).reshape(F, 17, 3)
+    cons = synth.constraint_indices(synth.CONSTRAINTS)
+    weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
+    return cams, o, p2, init, cons, weak, skel[0]
+
+
+def _oracle_cost(o, x, p2, cons, weak, ssf, args, loss="soft_l1"):
+    r = o._error_fun_triangulation(x, p2, np.array(cons), np.array(weak), ssf, args["scale_length"],
+                                   args["scale_length_weak"], args["reproj_error_threshold"], loss,
+                                   args["n_deriv_smooth"])
+    return 0.5 * np.sum(r ** 2)
+
+
+def _check_against_scipy(F, drop=0.1, gap=False, args=ARGS, loss="soft_l1"):
+    from mqhip.geometry import CameraGroup
+    from oracle.geometry import optim_points
+    cams, o, p2, init, cons, weak, truth = _problem(F, drop, gap)
+    sa = optim_points(o, p2, init, cons, weak, reproj_loss=loss, ftol=1e-3, return_result=True, **args)
+    sb = optim_points(o, p2, init, cons, weak, reproj_loss=loss, ftol=1e-10, return_result=True, **args)
+    g = CameraGroup.from_dicts(cams)
+    p3g, jlg = g.optim_points(p2, init, constraints=cons, constraints_weak=weak, reproj_loss=loss, **args)
+    p3a, p3b = sa[0], sb[0]
+    band = np.linalg.norm(p3a - p3b, axis=-1)
+    dev = np.linalg.norm(p3g - p3a, axis=-1)
+    assert np.median(dev) <= max(np.median(band), 1.0), (np.median(dev), np.median(band))
+    assert np.percentile(dev, 99) <= max(np.percentile(band, 99), 5.0), (np.percentile(dev, 99),
+                                                                          np.percentile(band, 99))
+    ssf = sa[3]
+    xg = np.hstack([p3g.ravel(), jlg])
+    cg = _oracle_cost(o, xg, p2, cons, weak, ssf, args, loss)
+    assert cg <= sa[2].cost * (1 + 1e-3), (cg, sa[2].cost, sb[2].cost)
+    np.testing.assert_allclose(jlg, sa[1], rtol=0.02, atol=1.0)
+    return p3g, jlg
+
+
+def test_optim_points_matches_scipy():
+    _check_against_scipy(40)
+
+
+def test_optim_points_with_gaps_and_sparse_views():
+    _check_against_scipy(36, drop=0.3, gap=True)
+
+
+@pytest.mark.parametrize("loss,n", [("huber", 2), ("linear", 1)])
+def test_optim_points_loss_and_order_variants(loss, n):
+    args = dict(ARGS, n_deriv_smooth=n)
+    _check_against_scipy(24, args=args, loss=loss)
+
+
+def test_optim_batch_equals_single_and_is_deterministic():
+    from mqhip.geometry import CameraGroup
+    from mqhip.optim import optim_points_batch
+    probs = [_problem(20, seed=s) for s in (3, 4, 5)]
+    cams = probs[0][0]
+    g = CameraGroup.from_dicts(cams)
+    P2 = np.stack([p[2] for p in probs])
+    I3 = np.stack([p[3] for p in probs])
+    cons, weak = probs[0][4], probs[0][5]
+    a, la = optim_points_batch(g, P2, I3, cons, weak, **ARGS)
+    b, lb = optim_points_batch(g, P2, I3, cons, weak, **ARGS)
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(la, lb)
+    for i in range(3):
+        s, ls = optim_points_batch(g, P2[i:i + 1], I3[i:i + 1], cons, weak, **ARGS)
+        np.testing.assert_array_equal(s[0], a[i])
+        np.testing.assert_array_equal(ls[0], la[i])
+
+
+def test_optim_points_jointlenfix_keeps_lengths_and_lowers_cost():
+    from mqhip.geometry import CameraGroup
+    from mqhip.optim import optim_points_batch, prepare
+    cams, o, p2, init, cons, weak, truth = _problem(30)
+    g = CameraGroup.from_dicts(cams)
+    jl_fixed = np.linspace(60, 300, len(cons) + len(weak))
+    p3, jl = g.optim_points_jointlenfix(p2, init, jl_fixed, constraints=cons, constraints_weak=weak, **ARGS)
+    np.testing.assert_array_equal(jl, jl_fixed)
+    x0, ssf = prepare(init, cons, weak, ARGS["scale_smooth"])
+    x0[-len(jl_fixed):] = jl_fixed
+    c0 = _oracle_cost(o, x0, p2, cons, weak, ssf, ARGS)
+    c1 = _oracle_cost(o, np.hstack([p3.ravel(), jl_fixed]), p2, cons, weak, ssf, ARGS)
+    assert c1 < 0.5 * c0
+    _, _, stats, _ = optim_points_batch(g, p2[None], init[None], cons, weak, joint_len=jl_fixed, max_iter=15,
+                                        return_stats=True, **ARGS)
+    assert stats[0, 2] <= 15
