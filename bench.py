@@ -111,6 +111,7 @@ def main():
     from mqhip import _lib, synth
     from mqhip.geometry import CameraGroup
     from mqhip.pose import VitPoseHip
+    from mqhip.shard import gather_keypoints
     from mqhip.weights import CONFIGS, make_random_weights
 
     cfg = CONFIGS[args.model]
@@ -185,8 +186,9 @@ def main():
     for i in range(args.steps):
         step(args.warmup + i, log_slot=i)
     if world > 1:
-        gathered = torch.empty((world,) + tuple(kp_log.shape), device=dev, dtype=kp_log.dtype)
-        dist.all_gather_into_tensor(gathered, kp_log)
+        # the one exchange step: every rank's per-view 2D keypoints, in frame order (mqhip.shard)
+        per_frame = kp_log.view(args.steps, FPS, N_VIEWS, N_ANIMALS, cfg.n_joints, 3).flatten(0, 1)
+        gathered = gather_keypoints(per_frame, world * args.steps * FPS, world)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

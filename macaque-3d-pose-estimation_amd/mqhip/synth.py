@@ -294,3 +294,16 @@ def make_frames(n_views: int, kp2d_frame=None, seed: int = 4, height: int = IMG_
                     patch = frames[v, y0 - 6:y0 + 7, x0 - 6:x0 + 7]
                     patch[disk] = col
     return frames
+
+
+def write_calibration_toml(cams, path):
+    """calibration.toml in the layout step4 writes (step4:101-138) for synthetic cameras."""
+    from .io import dump_toml
+    calib = {}
+    for i, c in enumerate(cams):
+        calib[f"cam_{i}"] = {
+            "name": str(c["name"]), "size": list(c["size"]), "matrix": np.asarray(c["matrix"]).tolist(),
+            "distortions": np.ravel(c["distortions"]).tolist(), "rotation": np.ravel(c["rvec"]).tolist(),
+            "translation": np.ravel(c["tvec"]).tolist(), "fisheye": False, "omnidir": True,
+            "xi": np.ravel(c["xi"]).tolist(), "K": np.asarray(c["K"]).tolist(), "D": np.ravel(c["D"]).tolist()}
+    dump_toml(calib, path)

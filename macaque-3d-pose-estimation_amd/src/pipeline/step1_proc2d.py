@@ -1,0 +1,189 @@
+"""Step 1 -- the pose slice of ``src/pipeline/step1_proc2d.py`` on MI355X.
+
+Kept from the reference (same constants, same row format, same files):
+  * box filtering and dynamic-margin expansion with aspect fix (step1:255-292),
+  * top-down ViTPose-H with heatmap flip test (step1:100-101, :294-298) --
+    through ``mqhip.apis`` (crop -> 32-layer ViT -> UDP/DARK decode in libmq_hip),
+  * keypoint threshold (KP_THR) and the recursive per-track EMA (step1:300-343),
+  * ``alldata.json`` rows ``[tid, x1, y1, x2, y2, [[x, y, s] x 17], id, id_score]``
+    and ``frame_num.npy`` (step1:345-395).
+
+MI355X-first: ``process_frame_multiview`` sends every box of every view of a
+frame through ONE batched launch sequence instead of one ``inference_topdown``
+per camera.
+
+Out of scope: the Swin Mask R-CNN detector, BoT-SORT tracker and
+ResNet ID classifier, and imgstore video decoding.  Their outputs enter here as
+arguments: per-frame tracker rows ``(N, >=5)`` [x1, y1, x2, y2, track_id, ...]
+and, optionally, ID predictions; without ID predictions every box gets
+``assigned_id = -1`` (the reference's "not confident" value).
+"""
+from __future__ import annotations
+
+import json
+import os
+from collections import deque
+from pathlib import Path
+
+import numpy as np
+
+from mqhip.apis import inference_topdown, inference_topdown_batch, init_model
+
+POSE_CONFIG = "./model/pose/ViTPose_huge_macaque_256x192.py"
+POSE_CHECKPOINT = "./model/pose/pose.pth"
+
+SCORE_THR = 0.85
+KP_THR = 0.30
+EMA_ALPHA = 0.50
+DISP_THR = 20.0
+MIN_MARGIN = 0.20
+MAX_MARGIN = 0.50
+DESIRED_AR = 192.0 / 256.0
+ID_CONF_THR = 0.80
+
+KP_PARAMS = {"score_thr": SCORE_THR, "kp_thr": KP_THR, "ema_alpha": EMA_ALPHA, "disp_thr": DISP_THR,
+             "min_margin": MIN_MARGIN, "max_margin": MAX_MARGIN, "desired_ar": DESIRED_AR,
+             "id_conf_thr": ID_CONF_THR}
+
+
+def init_pose_model(config=POSE_CONFIG, checkpoint=POSE_CHECKPOINT, device="cuda:0"):
+    """step1:100-101: the pose model with the reference's test_cfg."""
+    model = init_model(config, checkpoint, device=device)
+    model.test_cfg = dict(flip_test=True, flip_mode="heatmap", shift_heatmap=False)
+    return model
+
+
+def filter_tracks(tracks):
+    """step1:255-268: tracker rows -> int32 boxes with positive extent + their track ids."""
+    t = np.asarray(tracks, dtype=np.float64)
+    if t.size == 0:
+        return np.zeros((0, 4), np.int32), np.zeros((0,), np.int32)
+    t = t.reshape(len(t), -1)
+    b = t[:, :4].astype(np.int64)                     # int() truncation toward zero
+    ok = (b[:, 2] > b[:, 0]) & (b[:, 3] > b[:, 1])
+    return b[ok].astype(np.int32), t[ok, 4].astype(int).astype(np.int32)
+
+
+def expand_boxes(boxes, kp_params=KP_PARAMS):
+    """step1:270-292: margin 0.5 -> 0.2 as the box height grows 50 -> 200 px, aspect fixed to
+    0.75 when off by > 0.2, centre kept.  int32 (N,4) xyxy -> float32 (N,4) xyxy."""
+    b = np.asarray(boxes, dtype=np.float64).reshape(-1, 4)
+    w, h = b[:, 2] - b[:, 0], b[:, 3] - b[:, 1]
+    cx, cy = b[:, 0] + 0.5 * w, b[:, 1] + 0.5 * h
+    frac = np.clip((h - 50.0) / (200.0 - 50.0), 0.0, 1.0)
+    mx, mn, ar_t = kp_params["max_margin"], kp_params["min_margin"], kp_params["desired_ar"]
+    m = mx - (mx - mn) * frac
+    wn, hn = w * (1 + m), h * (1 + m)
+    ar = wn / hn
+    fix = np.abs(ar - ar_t) > 0.20
+    wide = ar >= ar_t
+    wn = np.where(fix & ~wide, hn * ar_t, wn)
+    hn = np.where(fix & wide, wn / ar_t, hn)
+    xywh = np.stack([cx, cy, wn, hn], axis=1).astype(np.float32).astype(np.float64)
+    half = 0.5 * xywh[:, 2:]
+    return np.concatenate([xywh[:, :2] - half, xywh[:, :2] + half], axis=1).astype(np.float32)
+
+
+class KeypointSmoother:
+    """step1:300-343: KP_THR masking, then the recursive EMA over a per-track deque(5)."""
+
+    def __init__(self, kp_params=KP_PARAMS):
+        self.p = kp_params
+        self.buffers: dict[int, deque] = {}
+
+    def clear(self):
+        self.buffers.clear()
+
+    def update(self, tid, frame_number, kpt_xy, kpt_score):
+        xy = np.array(kpt_xy, dtype=np.float64, copy=True)
+        sc = np.array(kpt_score, dtype=np.float32, copy=True)
+        low = sc < self.p["kp_thr"]
+        xy[low, :2] = np.nan
+        sc[low] = 0.0
+        kp = np.concatenate([xy, sc.reshape(-1, 1)], axis=1)
+        buf = self.buffers.setdefault(int(tid), deque(maxlen=5))
+        buf.append((frame_number, kp.copy()))
+        if len(buf) >= 2:
+            (_, prev), (fc, cur) = buf[-2], buf[-1]
+            both = ~np.isnan(prev[:, 0]) & ~np.isnan(cur[:, 0])
+            disp = np.zeros(prev.shape[0], dtype=np.float32)
+            if both.any():
+                disp[both] = np.linalg.norm(cur[both, :2] - prev[both, :2], axis=1)
+            sm = (disp < self.p["disp_thr"]) & both
+            a = self.p["ema_alpha"]
+            cur[sm, :2] = a * prev[sm, :2] + (1 - a) * cur[sm, :2]
+            buf[-1] = (fc, cur)
+        return buf[-1][1]
+
+
+def _rows(pose_results, boxes, tids, smoother, frame_number, id_preds, kp_params):
+    rows = []
+    for i, pr in enumerate(pose_results):
+        kp = pr.pred_instances.keypoints[0]
+        try:
+            sc = pr.pred_instances.keypoint_scores[0]
+        except AttributeError:
+            sc = np.ones(kp.shape[0], dtype=np.float32)
+        sm = smoother.update(int(tids[i]), frame_number, kp, sc)
+        if id_preds is None:
+            label, score = -1, 0.0
+        else:
+            label, score = int(id_preds[i]["pred_label"]), float(id_preds[i]["pred_score"])
+        assigned = label if score >= kp_params["id_conf_thr"] else -1
+        x1, y1, x2, y2 = boxes[i]
+        rows.append([int(tids[i]), float(x1), float(y1), float(x2), float(y2),
+                     [[float(x), float(y), float(s)] for (x, y, s) in sm], assigned, score])
+    return rows
+
+
+def process_frame(pose_model, img, tracks, smoother, frame_number, id_preds=None, kp_params=KP_PARAMS):
+    """One camera frame: tracker rows -> alldata.json rows (step1:255-364)."""
+    boxes, tids = filter_tracks(tracks)
+    if len(boxes) == 0:
+        return []
+    bb = expand_boxes(boxes, kp_params)
+    res = inference_topdown(pose_model, img, bboxes=bb, bbox_format="xyxy")
+    return _rows(res, boxes, tids, smoother, frame_number, id_preds, kp_params)
+
+
+def process_frame_multiview(pose_model, imgs, tracks_per_view, smoothers, frame_number, id_preds_per_view=None,
+                            kp_params=KP_PARAMS):
+    """All views of one frame in one batched crop -> ViT -> decode pass.  imgs: list of HxWx3
+    uint8 or a (V,H,W,3) uint8 GPU tensor; smoothers: one KeypointSmoother per view."""
+    per_view = [filter_tracks(t) for t in tracks_per_view]
+    bbs = [expand_boxes(b, kp_params) if len(b) else np.zeros((0, 4), np.float32) for b, _ in per_view]
+    results = inference_topdown_batch(pose_model, imgs, bbs)
+    out = []
+    for v, ((boxes, tids), res) in enumerate(zip(per_view, results)):
+        ids = None if id_preds_per_view is None else id_preds_per_view[v]
+        out.append(_rows(res, boxes, tids, smoothers[v], frame_number, ids, kp_params) if len(boxes) else [])
+    return out
+
+
+def process_single_cam(frames, tracks, out_dir, pose_model, frame_numbers=None, id_preds=None,
+                       kp_params=KP_PARAMS):
+    """Pose half of step1:166-410 for one camera.  frames: iterable of BGR uint8 images;
+    tracks: per-frame tracker rows; writes alldata.json + frame_num.npy to out_dir."""
+    os.makedirs(out_dir, exist_ok=True)
+    smoother = KeypointSmoother(kp_params)
+    results, fnums = [], []
+    for k, (img, trk) in enumerate(zip(frames, tracks)):
+        fn = k if frame_numbers is None else int(frame_numbers[k])
+        ids = None if id_preds is None else id_preds[k]
+        results.append(process_frame(pose_model, img, trk, smoother, fn, ids, kp_params))
+        fnums.append(fn)
+    np.save(Path(out_dir) / "frame_num.npy", np.array(fnums, dtype=np.int32))
+    with open(Path(out_dir) / "alldata.json", "w") as fp:
+        json.dump(results, fp)
+    return results
+
+
+def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0):
+    """step1.proc (step1:450): needs the detector, tracker and imgstore reader, which are outside
+    this build's scope.  Use process_single_cam / process_frame_multiview
+    with externally produced tracks."""
+    import glob
+    if not glob.glob(os.path.join(raw_root, f"{data_name}.*", "metadata.yaml")):
+        raise FileNotFoundError(f'No imgstore metadata for "{data_name}" in {raw_root}')
+    raise NotImplementedError("detection/tracking/ID (Swin Mask R-CNN, BoT-SORT, ResNet-152) are not part of "
+                              "this build; feed tracker rows to process_single_cam")

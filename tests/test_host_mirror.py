@@ -21,3 +21,50 @@ def test_optim_prepare_matches_oracle_init():
     ref_x0[~np.isfinite(ref_x0)] = 0
     np.testing.assert_array_equal(x0, ref_x0)
     assert ssf == ref_ssf
+
+
+def _rng_boxes(rng, n):
+    x1 = rng.integers(0, 1800, n)
+    y1 = rng.integers(0, 1300, n)
+    w = rng.integers(-3, 400, n)
+    h = rng.integers(-3, 400, n)
+    tr = np.stack([x1 + rng.random(n), y1 + rng.random(n), x1 + w + rng.random(n), y1 + h + rng.random(n),
+                   rng.integers(1, 9, n), rng.random(n)], axis=1)
+    return tr
+
+
+def test_step1_box_filter_and_expansion_match_oracle():
+    """Rows a1 + the degenerate-box filter (step1:255-292), bit-exact vs the per-box oracle."""
+    from oracle import postprocess as op
+    from src.pipeline import step1_proc2d as s1
+    rng = np.random.default_rng(1)
+    tr = _rng_boxes(rng, 400)
+    b, t = s1.filter_tracks(tr)
+    ob, ot = op.filter_tracks(tr)
+    np.testing.assert_array_equal(b, ob)
+    np.testing.assert_array_equal(t, ot)
+    np.testing.assert_array_equal(s1.expand_boxes(b), op.expand_boxes(ob))
+    assert s1.filter_tracks(np.zeros((0, 7)))[0].shape == (0, 4)
+
+
+def test_step1_keypoint_threshold_and_ema_match_oracle():
+    """Row a10: KP_THR masking + recursive EMA over per-track deques, bit-exact vs the oracle."""
+    from types import SimpleNamespace
+    from oracle import postprocess as op
+    from src.pipeline import step1_proc2d as s1
+    rng = np.random.default_rng(2)
+    sm, osm = s1.KeypointSmoother(), op.Smoother()
+    base = rng.uniform(100, 1500, (3, 17, 2))
+    for fn in range(40):
+        tids = rng.permutation([3, 5, 9])[:rng.integers(1, 4)]
+        kps = np.stack([base[[3, 5, 9].index(t)] + rng.normal(0, 12, (17, 2)) for t in tids])
+        sc = rng.uniform(0, 1, (len(tids), 17)).astype(np.float32)
+        boxes = np.tile(np.array([[10, 20, 200, 300]], np.int32), (len(tids), 1))
+        res = [SimpleNamespace(pred_instances=SimpleNamespace(keypoints=kps[i][None], keypoint_scores=sc[i][None]))
+               for i in range(len(tids))]
+        rows = s1._rows(res, boxes, tids, sm, fn, None, s1.KP_PARAMS)
+        orows = op.frame_rows(kps, sc, boxes, tids, osm, fn)
+        assert len(rows) == len(orows)
+        for r, o in zip(rows, orows):
+            assert r[:5] == o[:5] and r[6:] == o[6:]
+            np.testing.assert_array_equal(np.array(r[5]), np.array(o[5]))
