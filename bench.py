@@ -217,7 +217,9 @@ def main():
                 traffic = None
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                "kernel": "gemm_bf16_kernel<EPI_GELU_BF16> (FFN fc1, M=%d N=%d K=%d)" % (
+                "traffic_source": "profiles/pmc_fc1_gemm.json: rocprofv3 --pmc 2*FETCH_SIZE + WRITE_SIZE per launch "
+                                  "(gfx950 corrections; Infinity-Cache hits included); algorithmic 170,414,080 B",
+                "kernel": "gemm256_kernel<EPI_GELU_BF16> (FFN fc1, M=%d N=%d K=%d)" % (
                     2 * n * cfg.tokens, cfg.ffn, cfg.embed_dims),
                 "flops_per_launch": fl.value, "avg_launch_ms": round(avg_ms.value, 5), "launches": cnt.value}
 

@@ -37,7 +37,9 @@ const char* mq_last_error(void);
 #define MQ_TUNE_GEMM_STAGES 1       /* LDS ring depth of the 256x256 GEMM: 4 (128 KiB) or 5 (160 KiB) */
 #define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 kernel */
 #define MQ_TUNE_GEMM_ABLATE 3       /* timing ablations of the f32-epilogue 256 GEMM (WRONG results):
-                                       1 no steady-state DMA, 2 no barrier, 3 both, 7 + no LDS reads */
+                                       1 no steady-state DMA, 2 no barrier, 3 both, 7 + no LDS reads,
+                                       8 DMA issued but never waited for, 9 = 8 with buffer_load staging */
+#define MQ_TUNE_GEMM_BUFLOAD 5      /* 1: stage GEMM tiles with buffer_load_dwordx4 ... lds */
 #define MQ_TUNE_OPTIM_PCG_ITERS 4   /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
 int mq_set_tuning(int key, int value);
 

@@ -133,12 +133,15 @@ int mq_set_tuning(int key, int value) {
       mq::g_gemm_stages = value;
       return 0;
     case MQ_TUNE_GEMM_ABLATE:
-      if (value != 0 && value != 1 && value != 2 && value != 3 && value != 7)
-        return fail("mq_set_tuning: ablation must be 0, 1, 2, 3 or 7", -2);
+      if (value != 0 && value != 1 && value != 2 && value != 3 && value != 7 && value != 8 && value != 9)
+        return fail("mq_set_tuning: ablation must be 0, 1, 2, 3, 7, 8 or 9", -2);
       mq::g_gemm_ablate = value;
       return 0;
     case MQ_TUNE_GEMM_FORCE_SMALL:
       mq::g_gemm_force_small = value != 0;
+      return 0;
+    case MQ_TUNE_GEMM_BUFLOAD:
+      mq::g_gemm_bufload = value != 0;
       return 0;
     case MQ_TUNE_OPTIM_PCG_ITERS:
       if (value < 1 || value > 128) return fail("mq_set_tuning: PCG iterations must be in [1, 128]", -2);

@@ -228,11 +228,13 @@ __device__ __forceinline__ void tile_coords(int wid, int tiles_m, int tiles_n, i
 // next tile are in flight while the current tile's epilogue stores drain).
 // ABL (timing ablations only, outputs are wrong when non-zero): bit0 no steady-state
 // DMA, bit1 no per-step barrier, bit2 no fragment re-reads.
-template <int EPI, int NS, int ABL = 0>
+// BUF: stage with buffer_load_dwordx4 ... lds (32-bit per-lane offset fixed per tile, K advance in
+// soffset) instead of global_load_lds_dwordx4 (64-bit per-lane address rebuilt every stage).
+template <int EPI, int NS, int ABL = 0, bool BUF = false>
 __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
   const int wm = wave >> 2, wn = wave & 3;
   const int frow = lane & 15;
   const int fk = lane >> 4;
@@ -259,6 +261,11 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
   int iss_t = 0, iss_k = 0, iss_slot = 0;
   const bf16_t* pa[2];
   const bf16_t* pw[2];
+  unsigned va[2], vw[2];
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)((size_t)p.M * p.lda * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
   auto set_tile_ptrs = [&](int ti) {
     int m0, n0;
     tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
@@ -267,24 +274,39 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       const int row = (wave * 2 + i) * 16 + (lane >> 2);
       const int chunk = (lane & 3) ^ swz2(row);
       const int ga = min(m0 + row, p.M - 1), gw = min(n0 + row, p.N - 1);
-      pa[i] = p.A + (size_t)ga * p.lda + chunk * 8;
-      pw[i] = p.W + (size_t)gw * p.ldw + chunk * 8;
+      if constexpr (BUF) {
+        va[i] = (unsigned)(((size_t)ga * p.lda + chunk * 8) * 2);
+        vw[i] = (unsigned)(((size_t)gw * p.ldw + chunk * 8) * 2);
+      } else {
+        pa[i] = p.A + (size_t)ga * p.lda + chunk * 8;
+        pw[i] = p.W + (size_t)gw * p.ldw + chunk * 8;
+      }
     }
   };
   set_tile_ptrs(0);
   auto issue_a = [&]() {
     char* sb = smem + iss_slot * B2_STAGE_BYTES;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pa[i] + iss_k * B2K),
-                                       MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (BUF)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, va[i],
+                                                 iss_k * B2K * 2, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pa[i] + iss_k * B2K),
+                                         MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+    }
   };
   auto issue_w_and_advance = [&]() {
     char* sb = smem + iss_slot * B2_STAGE_BYTES + B2_OP_BYTES;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pw[i] + iss_k * B2K),
-                                       MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (BUF)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, vw[i],
+                                                 iss_k * B2K * 2, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pw[i] + iss_k * B2K),
+                                         MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+    }
     iss_slot = iss_slot + 1 == NS ? 0 : iss_slot + 1;
     if (iss_k + 1 < nk) {
       ++iss_k;
@@ -442,7 +464,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     // stage g+2 landed; g+3 .. g+NS-1 in flight.  Right after a full tile's epilogue its
     // 32 stores per wave sit between those DMAs in the in-order vmcnt queue: let them
     // drain behind this step instead of stalling the MFMAs on them.
-    if constexpr (!(ABL & 1)) {
+    if constexpr (!(ABL & 1) && !(ABL & 8)) {
       // >= this many VMEM ops of a full tile's epilogue are younger than stage g+2's DMA
       constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
       if (stores_pending)
@@ -473,17 +495,18 @@ static int g_num_cus = 0;
 
 int g_gemm_stages = 4;  // tuning knob (mq_set_tuning(MQ_TUNE_GEMM_STAGES, 4|5))
 int g_gemm_ablate = 0;  // timing ablation knob (MQ_TUNE_GEMM_ABLATE)
+int g_gemm_bufload = 0; // MQ_TUNE_GEMM_BUFLOAD: stage with buffer_load ... lds
 
-template <int EPI, int NS, int ABL>
+template <int EPI, int NS, int ABL, bool BUF = false>
 static void launch256(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   const int lds = NS * B2_STAGE_BYTES;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS, ABL, BUF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<EPI, NS, ABL>), grid, dim3(B2T), lds, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm256_kernel<EPI, NS, ABL, BUF>), grid, dim3(B2T), lds, stream, p, tiles_m, tiles_n);
 }
 
 template <int EPI>
@@ -494,8 +517,17 @@ static void launch256s(dim3 grid, hipStream_t stream, const GemmArgs& p, int til
       case 2: launch256<EPI, 4, 2>(grid, stream, p, tiles_m, tiles_n); return;
       case 3: launch256<EPI, 4, 3>(grid, stream, p, tiles_m, tiles_n); return;
       case 7: launch256<EPI, 4, 7>(grid, stream, p, tiles_m, tiles_n); return;
+      case 8: launch256<EPI, 4, 8>(grid, stream, p, tiles_m, tiles_n); return;
+      case 9: launch256<EPI, 4, 8, true>(grid, stream, p, tiles_m, tiles_n); return;
       default: break;
     }
+  }
+  if (g_gemm_bufload) {
+    if (g_gemm_stages == 5)
+      launch256<EPI, 5, 0, true>(grid, stream, p, tiles_m, tiles_n);
+    else
+      launch256<EPI, 4, 0, true>(grid, stream, p, tiles_m, tiles_n);
+    return;
   }
   if (g_gemm_stages == 5)
     launch256<EPI, 5, 0>(grid, stream, p, tiles_m, tiles_n);

@@ -28,6 +28,7 @@ struct GemmArgs {
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 extern int g_gemm_stages;
 extern int g_gemm_ablate;
+extern int g_gemm_bufload;
 extern bool g_gemm_force_small;
 
 // ViT ops (vit_ops.hip)

@@ -50,15 +50,25 @@ def _run(M, N, K, epi, aux_rows=0, seed=0):
     return err, scale
 
 
+@pytest.fixture(params=[0, 1], ids=["glds", "bufload"])
+def staging(request):
+    """Both LDS-DMA staging forms of the 256x256 kernel (MQ_TUNE_GEMM_BUFLOAD)."""
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    assert ctx.lib.mq_set_tuning(5, request.param) == 0
+    yield request.param
+    ctx.lib.mq_set_tuning(5, 0)
+
+
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
-def test_gemm_256_path_all_epilogues(epi):
+def test_gemm_256_path_all_epilogues(epi, staging):
     err, scale = _run(700, 512, 320, epi, aux_rows=192)
     tol = 2e-3 * scale + (0.01 * scale if epi in (0, 1) else 0.0)
     assert err <= tol, (err, tol)
 
 
 @pytest.mark.parametrize("M,N,K", [(12288, 1280, 1280), (1024, 3840, 1280), (512, 5120, 256)])
-def test_gemm_vit_shapes(M, N, K):
+def test_gemm_vit_shapes(M, N, K, staging):
     err, scale = _run(M, N, K, 4)
     assert err <= 2e-3 * scale
 

@@ -40,6 +40,17 @@ def main():
     for rnd in range(2):
       for var in variants:
         ctx.lib.mq_set_tuning(3, 0)
+        ctx.lib.mq_set_tuning(5, 0)
+        if var.startswith("buf"):
+            ctx.lib.mq_set_tuning(5, 1)
+            var_st = var[3:]
+        else:
+            var_st = var
+        if var == "torch":
+            for name in names:
+                res[f"{name}/{var}/r{rnd}"] = bench_torch(torch, name, args.iters)
+                print(f"{name} v={var} r={rnd}", res[f"{name}/{var}/r{rnd}"], flush=True)
+            continue
         if var == "small":
             ctx.lib.mq_set_tuning(2, 1)
         elif var.startswith("abl"):
@@ -48,11 +59,30 @@ def main():
             ctx.lib.mq_set_tuning(3, int(var[3:]))
         else:
             ctx.lib.mq_set_tuning(2, 0)
-            ctx.lib.mq_set_tuning(1, int(var))
+            ctx.lib.mq_set_tuning(1, int(var_st))
         for name in names:
             res[f"{name}/{var}/r{rnd}"] = bench_one(ctx, _lib, torch, name, args.iters)
             print(f"{name} v={var} r={rnd}", res[f"{name}/{var}/r{rnd}"], flush=True)
     print(json.dumps(res))
+
+
+def bench_torch(torch, name, iters):
+    """torch.matmul (hipBLASLt) on the same shape, bf16 out, no fused epilogue -- a reference point."""
+    M, N, K, epi = SHAPES[name]
+    A = (torch.rand((M, K), device="cuda") * 2 - 1).to(torch.bfloat16)
+    W = ((torch.rand((N, K), device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+    out = torch.empty((M, N), device="cuda", dtype=torch.bfloat16)
+    for _ in range(3):
+        torch.matmul(A, W.t(), out=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        torch.matmul(A, W.t(), out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    return {"M": M, "N": N, "K": K, "ms": round(ms, 4), "tflops": round(2 * M * N * K / (ms * 1e-3) / 1e12, 1)}
 
 
 def bench_one(ctx, _lib, torch, name, iters):

@@ -1,0 +1,48 @@
+"""Summarise rocprofv3 --pmc passes (gpurun_out/pmc/p*/run_counter_collection.csv) for one kernel.
+
+HBM traffic per launch follows /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
+FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide
+coalesced streaming reads (16 B/lane, incl. global_load_lds) -> x2; WRITE_SIZE is exact for
+16 B/lane stores.  hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
+
+python tools/pmc_summary.py <pmc_dir> <kernel-substring> <algorithmic_bytes> <flops> > out.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main():
+    d, key, alg_bytes, flops = sys.argv[1], sys.argv[2], float(sys.argv[3]), float(sys.argv[4])
+    csv.field_size_limit(1 << 30)
+    vals = defaultdict(list)
+    dur = []
+    for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if key not in row["Kernel_Name"]:
+                    continue
+                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                dur.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    out = {"kernel": key, "samples": {k: len(v) for k, v in vals.items()}, "counters_avg_per_launch": avg,
+           "algorithmic_bytes_per_launch": alg_bytes, "flops_per_launch": flops,
+           "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section gfx950 corrections)"}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        rd, wr = 2 * avg["FETCH_SIZE"] * 1024, avg["WRITE_SIZE"] * 1024
+        out.update(hbm_read_bytes_per_launch=rd, hbm_write_bytes_per_launch=wr, hbm_bytes_per_launch=rd + wr,
+                   traffic_over_algorithmic=(rd + wr) / alg_bytes)
+    if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
+        out["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
+        out["mfma_busy_per_gui_cycle"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, avg["GRBM_GUI_ACTIVE"])
+    if dur:
+        out["avg_duration_ns_under_pmc"] = sum(dur) / len(dur)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
