@@ -39,9 +39,15 @@ const char* mq_last_error(void);
 #define MQ_TUNE_GEMM_ABLATE 3       /* timing ablations of the f32-epilogue 256 GEMM (WRONG results):
                                        1 no steady-state DMA, 2 no barrier, 3 both, 7 + no LDS reads,
                                        8 DMA issued but never waited for, 9 = 8 with buffer_load staging */
-#define MQ_TUNE_GEMM_BUFLOAD 5      /* 1: stage GEMM tiles with buffer_load_dwordx4 ... lds */
+#define MQ_TUNE_GEMM_BUFLOAD 5      /* 1 (default): stage GEMM tiles with buffer_load_dwordx4 ... lds; 0: global_load_lds */
+#define MQ_TUNE_GEMM_MFMA32 6       /* 1: 256x256 GEMM on v_mfma_f32_32x32x16_bf16 (else 16x16x32) */
+#define MQ_TUNE_ATTENTION_ABLATE 8  /* attention timing ablations (WRONG results): 1 staging only, 2 no K/V loads,
+                                       3 no output stores */
+#define MQ_TUNE_GEMM_SCHED 7        /* 1 (default): K-step with DMA issue / fragment reads interleaved between MFMAs */
 #define MQ_TUNE_OPTIM_PCG_ITERS 4   /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
 int mq_set_tuning(int key, int value);
+/* Current value of a tuning knob (negative on an unknown key). */
+int mq_get_tuning(int key);
 
 /* Bind a context to HIP device `device`. */
 int mq_create(int device, mq_ctx** out);
@@ -144,6 +150,13 @@ int mq_triangulate_pinv(mq_ctx* ctx, const double* cams, int n_cams, const doubl
  * owned by the context.  score_threshold 0.3, n_back 3, offset_threshold 25 in step 4. */
 int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int n_animals, int n_frames, int n_cams, int n_joints,
                       double score_threshold, int n_back, double offset_threshold, double* out, void* stream);
+
+/* Global multi-head self-attention of the ViT encoder (mmpretrain MultiheadAttention, qkv_bias,
+ * scale 1/sqrt(head_dim)) -- the building block inside mq_vitpose_forward.
+ *   qkv  bf16 (n_img * tokens, 3 * dim) = [q | k | v] per token row; out bf16 (n_img * tokens, dim).
+ *   tokens % 32 == 0 and <= 192; head_dim = dim / heads in {64, 80}. */
+int mq_attention_bf16(mq_ctx* ctx, const uint16_t* qkv, uint16_t* out, int n_img, int tokens, int dim, int heads,
+                      void* stream);
 
 /* CameraGroup.optim_points (cameras.py:1116-1190) and optim_points_jointlenfix (:1192-1415) for
  * B animals at once.  Replaces scipy least_squares(trf, 2-point sparse Jacobian) with

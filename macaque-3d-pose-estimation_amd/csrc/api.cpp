@@ -143,12 +143,36 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_GEMM_BUFLOAD:
       mq::g_gemm_bufload = value != 0;
       return 0;
+    case MQ_TUNE_GEMM_MFMA32:
+      mq::g_gemm_mfma32 = value != 0;
+      return 0;
+    case MQ_TUNE_GEMM_SCHED:
+      mq::g_gemm_sched = value != 0;
+      return 0;
+    case MQ_TUNE_ATTENTION_ABLATE:
+      if (value < 0 || value > 3) return fail("mq_set_tuning: attention ablation must be 0..3", -2);
+      mq::g_attention_ablate = value;
+      return 0;
     case MQ_TUNE_OPTIM_PCG_ITERS:
       if (value < 1 || value > 128) return fail("mq_set_tuning: PCG iterations must be in [1, 128]", -2);
       mq::g_optim_pcg_iters = value;
       return 0;
     default:
       return fail("mq_set_tuning: unknown key", -2);
+  }
+}
+
+int mq_get_tuning(int key) {
+  switch (key) {
+    case MQ_TUNE_GEMM_STAGES: return mq::g_gemm_stages;
+    case MQ_TUNE_GEMM_FORCE_SMALL: return mq::g_gemm_force_small ? 1 : 0;
+    case MQ_TUNE_GEMM_ABLATE: return mq::g_gemm_ablate;
+    case MQ_TUNE_OPTIM_PCG_ITERS: return mq::g_optim_pcg_iters;
+    case MQ_TUNE_GEMM_BUFLOAD: return mq::g_gemm_bufload;
+    case MQ_TUNE_GEMM_MFMA32: return mq::g_gemm_mfma32;
+    case MQ_TUNE_GEMM_SCHED: return mq::g_gemm_sched;
+    case MQ_TUNE_ATTENTION_ABLATE: return mq::g_attention_ablate;
+    default: return fail("mq_get_tuning: unknown key", -2);
   }
 }
 
@@ -731,6 +755,16 @@ int mq_optim_points(mq_ctx* ctx, const double* cams, int C, const double* p2d, d
                                   n_deriv_smooth, fix_lengths, max_iter, ftol, ctx->optim_ws.p, stats,
                                   (hipStream_t)stream);
   if (rc != 0) return fail("mq_optim_points: solver failed (" + std::to_string(rc) + ")", -6);
+  return 0;
+}
+
+int mq_attention_bf16(mq_ctx* ctx, const uint16_t* qkv, uint16_t* out, int n_img, int tokens, int dim, int heads,
+                      void* stream) {
+  if (!ctx || !qkv || !out) return fail("mq_attention_bf16: null argument");
+  if (n_img <= 0) return 0;
+  HIP_TRY(hipSetDevice(ctx->device));
+  const int rc = mq::attention_bf16(qkv, out, n_img, tokens, dim, heads, (hipStream_t)stream);
+  if (rc != 0) return fail("mq_attention_bf16: unsupported shape (tokens % 32 == 0, <= 192; head dim 64 or 80)", -2);
   return 0;
 }
 

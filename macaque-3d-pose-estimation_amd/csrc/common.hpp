@@ -6,6 +6,7 @@
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) short short4v;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef unsigned short bf16_t;  // raw bf16 storage
 
 #define MQ_LDS_GLOBAL(p) ((const void __attribute__((address_space(1)))*)(p))

@@ -230,7 +230,7 @@ __device__ __forceinline__ void tile_coords(int wid, int tiles_m, int tiles_n, i
 // DMA, bit1 no per-step barrier, bit2 no fragment re-reads.
 // BUF: stage with buffer_load_dwordx4 ... lds (32-bit per-lane offset fixed per tile, K advance in
 // soffset) instead of global_load_lds_dwordx4 (64-bit per-lane address rebuilt every stage).
-template <int EPI, int NS, int ABL = 0, bool BUF = false>
+template <int EPI, int NS, int ABL = 0, bool BUF = false, bool SCHED = false>
 __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
                                          MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
     }
   };
-  auto issue_w_and_advance = [&]() {
+  auto issue_w = [&]() {
     char* sb = smem + iss_slot * B2_STAGE_BYTES + B2_OP_BYTES;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -307,6 +307,8 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
         __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pw[i] + iss_k * B2K),
                                          MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
     }
+  };
+  auto advance = [&]() {
     iss_slot = iss_slot + 1 == NS ? 0 : iss_slot + 1;
     if (iss_k + 1 < nk) {
       ++iss_k;
@@ -315,6 +317,10 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       iss_k = 0;
       set_tile_ptrs(iss_t);
     }
+  };
+  auto issue_w_and_advance = [&]() {
+    issue_w();
+    advance();
   };
   auto stage_ptr = [&](int g) { return smem + (g % NS) * B2_STAGE_BYTES; };
 
@@ -430,7 +436,71 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
   };
 
   bool stores_pending = false;
+  // SCHED: one basic block per K-step body with the DMAs and fragment reads spread between the
+  // MFMAs (sched_group_barrier), instead of DMA issue right after the barrier.
+  auto kstep_sched = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
+    const char* An = stage_ptr(g + 1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
+    issue_a();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bn[j] = frag256(An + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+    __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+#pragma unroll
+    for (int i = 4; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
+    issue_w();
+#pragma unroll
+    for (int i = 4; i < 8; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+    __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+    __builtin_amdgcn_s_setprio(0);
+    advance();
+    constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
+    if (stores_pending)
+      wait_vm<4 * (NS - 3) + EPI_OPS>();
+    else
+      wait_vm<4 * (NS - 3)>();
+    stores_pending = false;
+    __builtin_amdgcn_s_barrier();
+    const int ti = g / nk;
+    if (g - ti * nk == nk - 1) {
+      epilogue(ti);
+      int m0, n0;
+      tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+      stores_pending = (m0 + B2M <= p.M) && (n0 + B2N <= p.N);
+    }
+  };
   auto kstep = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
+    if constexpr (SCHED) {
+      kstep_sched(g, bc, bn);
+      return;
+    }
     const char* An = stage_ptr(g + 1);  // past the end: harmless reads of a dead buffer
     if constexpr (!(ABL & 1)) issue_a();
     __builtin_amdgcn_s_setprio(1);
@@ -491,26 +561,323 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the block
 }
 
+// ============================================================================
+// Same persistent 256x256 tile and DMA pipeline, on v_mfma_f32_32x32x16_bf16.  A 32x32x16
+// MFMA holds the SIMD's vector issue for 8 of its 32 cycles (16x16x32: 8 of 16), so the
+// fragment reads, LDS-DMA issues and waits of a K-step fit in the MFMA shadow.
+// Each wave: 128 x 64 = 4 (M) x 2 (N) blocks of 32x32, acc = 8 x f32x16.
+// Operand fragment (both operands): lane l holds row (l & 31), k = 8 * (l >> 5) .. +7 of a
+// 16-deep K slice; a BK = 32 stage has two slices (kk), i.e. 16-B chunk c = 2 kk + (l >> 5).
+// Swapped product D = W * A^T: lane l, register r holds C[m = l & 31][n = 8 (r >> 2) + 4 (l >> 5) + (r & 3)].
+// LDS image: 64-B rows, chunk c of row r at slot c ^ ((r >> 2) & 3) -- conflict-free for the
+// ds_read_b128 lane groups of this pattern (rows {0-3,12-15,20-27}, {4-11,16-19,28-31}).
+__device__ __forceinline__ int swz32(int row) { return (row >> 2) & 3; }
+
+__device__ __forceinline__ bf16x8 frag32(const char* lds_op, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(lds_op + row * 64 + ((chunk ^ swz32(row)) << 4));
+}
+
+template <int EPI, int NS, bool BUF>
+__global__ __launch_bounds__(B2T, 2) void gemm256m32_kernel(GemmArgs p, int tiles_m, int tiles_n) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int frow = lane & 31;
+  const int fh = lane >> 5;
+
+  const int nt = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int nbx = (G - xcd + 7) >> 3;
+  const int xb = bid >> 3;
+  const int q = nt >> 3, r = nt & 7;
+  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int len = q + (xcd < r ? 1 : 0);
+  const int my_tiles = xb < len ? (len - xb + nbx - 1) / nbx : 0;
+  const int nk = p.K / B2K;
+  const int total = my_tiles * nk;
+  if (total == 0) return;
+
+  int iss_t = 0, iss_k = 0, iss_slot = 0;
+  const bf16_t* pa[2];
+  const bf16_t* pw[2];
+  unsigned va[2], vw[2];
+  const __amdgpu_buffer_rsrc_t rsA =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)((size_t)p.M * p.lda * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
+  auto set_tile_ptrs = [&](int ti) {
+    int m0, n0;
+    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wave * 2 + i) * 16 + (lane >> 2);
+      const int chunk = (lane & 3) ^ swz32(row);
+      const int ga = min(m0 + row, p.M - 1), gw = min(n0 + row, p.N - 1);
+      if constexpr (BUF) {
+        va[i] = (unsigned)(((size_t)ga * p.lda + chunk * 8) * 2);
+        vw[i] = (unsigned)(((size_t)gw * p.ldw + chunk * 8) * 2);
+      } else {
+        pa[i] = p.A + (size_t)ga * p.lda + chunk * 8;
+        pw[i] = p.W + (size_t)gw * p.ldw + chunk * 8;
+      }
+    }
+  };
+  set_tile_ptrs(0);
+  auto issue_a = [&]() {
+    char* sb = smem + iss_slot * B2_STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (BUF)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, va[i],
+                                                 iss_k * B2K * 2, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pa[i] + iss_k * B2K),
+                                         MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+    }
+  };
+  auto issue_w_and_advance = [&]() {
+    char* sb = smem + iss_slot * B2_STAGE_BYTES + B2_OP_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (BUF)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, vw[i],
+                                                 iss_k * B2K * 2, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pw[i] + iss_k * B2K),
+                                         MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+    }
+    iss_slot = iss_slot + 1 == NS ? 0 : iss_slot + 1;
+    if (iss_k + 1 < nk) {
+      ++iss_k;
+    } else if (iss_t + 1 < my_tiles) {
+      ++iss_t;
+      iss_k = 0;
+      set_tile_ptrs(iss_t);
+    }
+  };
+  auto stage_ptr = [&](int g) { return smem + (g % NS) * B2_STAGE_BYTES; };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st) {
+    issue_a();
+    issue_w_and_advance();
+  }
+  wait_vm<4 * (NS - 3)>();
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+  {
+    const char* S = stage_ptr(0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) b0[j][kk] = frag32(S + B2_OP_BYTES, wn * 64 + j * 32 + frow, 2 * kk + fh);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = frag32(S, wm * 128 + i * 32 + frow, 2 * kk + fh);
+  }
+
+  auto epilogue = [&](int ti) {
+    int m0, n0;
+    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+      // lanes l and l+32 hold columns 8g+0..3 and 8g+4..7 of row l & 31; pairing groups
+      // (g, g+1) with v_permlane32_swap gives each lane 8 consecutive columns -> 16-B stores.
+      float4 bias[2][4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int n = n0 + wn * 64 + j * 32 + g4 * 8 + fh * 4;
+          bias[j][g4] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 128 + i * 32 + frow;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+#pragma unroll
+          for (int gp = 0; gp < 4; gp += 2) {
+            unsigned pk[2][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int g4 = gp + h;
+              const float4 bb = bias[j][g4];
+              float v[4] = {acc[i][j][4 * g4 + 0] + bb.x, acc[i][j][4 * g4 + 1] + bb.y,
+                            acc[i][j][4 * g4 + 2] + bb.z, acc[i][j][4 * g4 + 3] + bb.w};
+              if constexpr (EPI == EPI_GELU_BF16) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+              }
+              pk[h][0] = pack_bf16x2(v[0], v[1]);
+              pk[h][1] = pack_bf16x2(v[2], v[3]);
+            }
+            const auto s0 = __builtin_amdgcn_permlane32_swap(pk[0][0], pk[1][0], false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(pk[0][1], pk[1][1], false, false);
+            // lanes < 32: group gp of row m; lanes >= 32: group gp+1 of row m
+            const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            const int n = n0 + wn * 64 + j * 32 + (gp + fh) * 8;
+            if (m < p.M && n < p.N) *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 128 + i * 32 + frow;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int n = n0 + wn * 64 + j * 32 + g4 * 8 + fh * 4;
+          float v[4] = {acc[i][j][4 * g4 + 0], acc[i][j][4 * g4 + 1], acc[i][j][4 * g4 + 2], acc[i][j][4 * g4 + 3]};
+          if (m >= p.M || n >= p.N) continue;
+          if (p.bias) {
+            const float4 bias = *reinterpret_cast<const float4*>(p.bias + n);
+            v[0] += bias.x;
+            v[1] += bias.y;
+            v[2] += bias.z;
+            v[3] += bias.w;
+          }
+          if constexpr (EPI == EPI_RESID_F32) {
+            float4* c = reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n);
+            float4 x = *c;
+            x.x += v[0];
+            x.y += v[1];
+            x.z += v[2];
+            x.w += v[3];
+            *c = x;
+          } else if constexpr (EPI == EPI_POS_F32) {
+            const float4 ps = *reinterpret_cast<const float4*>(p.aux + (size_t)(m % p.aux_rows) * p.N + n);
+            *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) =
+                make_float4(v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w);
+          } else if constexpr (EPI == EPI_F32) {
+            *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      }
+    }
+  };
+
+  bool stores_pending = false;
+  auto kstep = [&](int g, bf16x8 (&bc)[2][2], bf16x8 (&bn)[2][2]) {
+    const char* Sn = stage_ptr(g + 1);  // past the end: harmless reads of a dead buffer
+    issue_a();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[j][kk], a[i][kk], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = frag32(Sn, wm * 128 + i * 32 + frow, 2 * kk + fh);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bn[j][kk] = frag32(Sn + B2_OP_BYTES, wn * 64 + j * 32 + frow, 2 * kk + fh);
+    issue_w_and_advance();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 2; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[j][kk], a[i][kk], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int i = 2; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) a[i][kk] = frag32(Sn, wm * 128 + i * 32 + frow, 2 * kk + fh);
+    constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
+    if (stores_pending)
+      wait_vm<4 * (NS - 3) + EPI_OPS>();
+    else
+      wait_vm<4 * (NS - 3)>();
+    stores_pending = false;
+    __builtin_amdgcn_s_barrier();
+    const int ti = g / nk;
+    if (g - ti * nk == nk - 1) {
+      epilogue(ti);
+      int m0, n0;
+      tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+      stores_pending = (m0 + B2M <= p.M) && (n0 + B2N <= p.N);
+    }
+  };
+  int g = 0;
+  for (; g + 1 < total; g += 2) {
+    kstep(g, b0, b1);
+    kstep(g + 1, b1, b0);
+  }
+  if (g < total) kstep(g, b0, b1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 static int g_num_cus = 0;
 
 int g_gemm_stages = 4;  // tuning knob (mq_set_tuning(MQ_TUNE_GEMM_STAGES, 4|5))
 int g_gemm_ablate = 0;  // timing ablation knob (MQ_TUNE_GEMM_ABLATE)
-int g_gemm_bufload = 0; // MQ_TUNE_GEMM_BUFLOAD: stage with buffer_load ... lds
+int g_gemm_bufload = 1; // MQ_TUNE_GEMM_BUFLOAD: stage with buffer_load ... lds (default: +3-11 % over glds)
+int g_gemm_sched = 1;   // MQ_TUNE_GEMM_SCHED: K-step with DMAs/reads interleaved between MFMAs (default: +1-3 %)
+int g_gemm_mfma32 = 0;  // MQ_TUNE_GEMM_MFMA32: 32x32x16 MFMA variant of the 256x256 kernel
 
-template <int EPI, int NS, int ABL, bool BUF = false>
+template <int EPI, int NS, int ABL, bool BUF = false, bool SCHED = false>
 static void launch256(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   const int lds = NS * B2_STAGE_BYTES;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS, ABL, BUF>,
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS, ABL, BUF, SCHED>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<EPI, NS, ABL, BUF>), grid, dim3(B2T), lds, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm256_kernel<EPI, NS, ABL, BUF, SCHED>), grid, dim3(B2T), lds, stream, p, tiles_m,
+                     tiles_n);
+}
+
+template <int EPI, int NS, bool BUF>
+static void launch256m32(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
+  static bool attr = false;
+  const int lds = NS * B2_STAGE_BYTES;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm256m32_kernel<EPI, NS, BUF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm256m32_kernel<EPI, NS, BUF>), grid, dim3(B2T), lds, stream, p, tiles_m, tiles_n);
 }
 
 template <int EPI>
 static void launch256s(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
+  if (g_gemm_mfma32) {
+    if (g_gemm_bufload)
+      launch256m32<EPI, 4, true>(grid, stream, p, tiles_m, tiles_n);
+    else
+      launch256m32<EPI, 4, false>(grid, stream, p, tiles_m, tiles_n);
+    return;
+  }
   if constexpr (EPI == EPI_F32) {  // ablations are compiled for the plain-f32 epilogue only
     switch (g_gemm_ablate) {
       case 1: launch256<EPI, 4, 1>(grid, stream, p, tiles_m, tiles_n); return;
@@ -521,6 +888,10 @@ static void launch256s(dim3 grid, hipStream_t stream, const GemmArgs& p, int til
       case 9: launch256<EPI, 4, 8, true>(grid, stream, p, tiles_m, tiles_n); return;
       default: break;
     }
+  }
+  if (g_gemm_sched) {
+    launch256<EPI, 4, 0, true, true>(grid, stream, p, tiles_m, tiles_n);
+    return;
   }
   if (g_gemm_bufload) {
     if (g_gemm_stages == 5)

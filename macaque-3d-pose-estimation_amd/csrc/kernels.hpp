@@ -29,11 +29,14 @@ int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 extern int g_gemm_stages;
 extern int g_gemm_ablate;
 extern int g_gemm_bufload;
+extern int g_gemm_mfma32;
+extern int g_gemm_sched;
 extern bool g_gemm_force_small;
 
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
                        float eps, hipStream_t s);
+extern int g_attention_ablate;
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s);
 int patch_im2col(const float* crops, unsigned short* A, int n_crops, int flip_copies, int img_h, int img_w,

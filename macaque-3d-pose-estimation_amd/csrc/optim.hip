@@ -269,10 +269,136 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_reduce_kernel(OptDims D, Op
 __device__ __forceinline__ double damp_of(double dg) { return fmax(dg, 1e-12); }
 
 // Block-banded Cholesky of the per-joint preconditioner (thread per (animal, joint)).
-// fac[((b*J + j)*F + f)*36]: [0..8] inverse of L_ff, [9d .. 9d+8] L_{f,f-d} (d = 1..n).
-__global__ void optim_factor_kernel(OptDims D, OptBufs Bf) {
+// fac[((b*J + j)*F + f)*36]: [0..8] inverse of L_ff (lower), [9d .. 9d+8] L_{f,f-d} (d = 1..n).
+// The recurrence is latency-bound: the last NN frames' blocks stay in registers and frame
+// f+1's inputs are loaded while frame f is factored.
+struct FacRec {
+  double inv[9];
+  double L[OPT_MAXN][9];  // L[d-1] = L_{f,f-d}
+};
+
+template <int NN>
+__device__ void factor_series(const OptDims& D, const OptBufs& Bf, int b, int j, double lam) {
+  const int F = D.F, J = D.J;
+  const double ssf = Bf.ssf[b];
+  const double s2 = F > NN ? ssf * ssf : 0.0;
+  double* fb = Bf.fac + ((size_t)b * J + j) * F * 36;
+  int ck[16], nck = 0;
+  bool many = false;
+  for (int k = 0; k < D.NL; ++k)
+    if (Bf.cons[2 * k] == j || Bf.cons[2 * k + 1] == j) {
+      if (nck < 16) ck[nck++] = k;
+      else many = true;
+    }
+  auto load_A = [&](int f, double (&A)[3][3]) {
+    const double* Rm = Bf.R + (((size_t)b * F + f) * J + j) * 6;
+    A[0][0] = Rm[0]; A[0][1] = Rm[1]; A[0][2] = Rm[2];
+    A[1][0] = Rm[1]; A[1][1] = Rm[3]; A[1][2] = Rm[4];
+    A[2][0] = Rm[2]; A[2][1] = Rm[4]; A[2][2] = Rm[5];
+    const double* lb = Bf.lenJ + ((size_t)b * F + f) * D.NL * 5;
+    if (!many) {
+      for (int t = 0; t < nck; ++t) {
+        const double* l = lb + ck[t] * 5;
+        const double l0 = l[0], l1 = l[1], l2 = l[2];
+        A[0][0] += l0 * l0; A[0][1] += l0 * l1; A[0][2] += l0 * l2;
+        A[1][0] += l1 * l0; A[1][1] += l1 * l1; A[1][2] += l1 * l2;
+        A[2][0] += l2 * l0; A[2][1] += l2 * l1; A[2][2] += l2 * l2;
+      }
+    } else {
+      for (int k = 0; k < D.NL; ++k) {
+        if (Bf.cons[2 * k] != j && Bf.cons[2 * k + 1] != j) continue;
+        const double* l = lb + k * 5;
+        for (int r = 0; r < 3; ++r)
+          for (int c = 0; c < 3; ++c) A[r][c] += l[r] * l[c];
+      }
+    }
+    const double* dg = Bf.diag + (size_t)b * D.NV + (size_t)f * J * 3 + 3 * j;
+    const double sd = s2 * dtd(f, f, F, NN, D.c);
+    A[0][0] += sd + lam * damp_of(dg[0]);
+    A[1][1] += sd + lam * damp_of(dg[1]);
+    A[2][2] += sd + lam * damp_of(dg[2]);
+  };
+  FacRec W[NN];  // W[k-1] = frame f-k
+  double An[3][3];
+  load_A(0, An);
+  for (int f = 0; f < F; ++f) {
+    double A[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) A[r][c] = An[r][c];
+    if (f + 1 < F) load_A(f + 1, An);
+    FacRec cur;
+#pragma unroll
+    for (int d = NN; d >= 1; --d) {
+      const int i = f - d;
+      if (i < 0) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) cur.L[d - 1][e] = 0.0;
+        continue;
+      }
+      double M[3][3];
+      const double off = s2 * dtd(f, i, F, NN, D.c);
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) M[r][c] = (r == c) ? off : 0.0;
+#pragma unroll
+      for (int e = d + 1; e <= NN; ++e) {
+        if (f - e < 0) continue;
+        const double* Lf = cur.L[e - 1];          // L_{f, f-e}
+        const double* Li = W[d - 1].L[e - d - 1];  // L_{i, f-e}
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            M[r][c] -= Lf[3 * r] * Li[3 * c] + Lf[3 * r + 1] * Li[3 * c + 1] + Lf[3 * r + 2] * Li[3 * c + 2];
+      }
+      const double* Ii = W[d - 1].inv;  // inv(L_ii) (lower)
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          cur.L[d - 1][3 * r + c] = M[r][0] * Ii[3 * c] + M[r][1] * Ii[3 * c + 1] + M[r][2] * Ii[3 * c + 2];
+    }
+#pragma unroll
+    for (int d = 1; d <= NN; ++d) {
+      if (f - d < 0) continue;
+      const double* Lf = cur.L[d - 1];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          A[r][c] -= Lf[3 * r] * Lf[3 * c] + Lf[3 * r + 1] * Lf[3 * c + 1] + Lf[3 * r + 2] * Lf[3 * c + 2];
+    }
+    const double l00 = sqrt(fmax(A[0][0], 1e-300));
+    const double l10 = A[1][0] / l00, l20 = A[2][0] / l00;
+    const double l11 = sqrt(fmax(A[1][1] - l10 * l10, 1e-300));
+    const double l21 = (A[2][1] - l20 * l10) / l11;
+    const double l22 = sqrt(fmax(A[2][2] - l20 * l20 - l21 * l21, 1e-300));
+    const double i00 = 1 / l00, i11 = 1 / l11, i22 = 1 / l22;
+    const double i10 = -l10 * i00 * i11;
+    const double i21 = -l21 * i11 * i22;
+    const double i20 = -(l20 * i00 + l21 * i10) * i22;
+    cur.inv[0] = i00; cur.inv[1] = 0; cur.inv[2] = 0;
+    cur.inv[3] = i10; cur.inv[4] = i11; cur.inv[5] = 0;
+    cur.inv[6] = i20; cur.inv[7] = i21; cur.inv[8] = i22;
+    double* o = fb + (size_t)f * 36;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) o[e] = cur.inv[e];
+#pragma unroll
+    for (int d = 1; d <= NN; ++d)
+#pragma unroll
+      for (int e = 0; e < 9; ++e) o[9 * d + e] = cur.L[d - 1][e];
+#pragma unroll
+    for (int k = NN - 1; k >= 1; --k) W[k] = W[k - 1];
+    W[0] = cur;
+  }
+}
+
+__global__ void __launch_bounds__(64) optim_factor_kernel(OptDims D, OptBufs Bf) {
   const int b = blockIdx.x, j = threadIdx.x;
-  const int F = D.F, J = D.J, n = D.n;
+  const int J = D.J;
   const double lam = Bf.ctl[2 * b];
   if (j == J) {
     if (!D.fix)
@@ -283,69 +409,9 @@ __global__ void optim_factor_kernel(OptDims D, OptBufs Bf) {
     return;
   }
   if (j > J) return;
-  const double ssf = Bf.ssf[b];
-  const double s2 = F > n ? ssf * ssf : 0.0;
-  double* fb = Bf.fac + ((size_t)b * J + j) * F * 36;
-  for (int f = 0; f < F; ++f) {
-    const double* Rm = Bf.R + (((size_t)b * F + f) * J + j) * 6;
-    double A[3][3] = {{Rm[0], Rm[1], Rm[2]}, {Rm[1], Rm[3], Rm[4]}, {Rm[2], Rm[4], Rm[5]}};
-    for (int k = 0; k < D.NL; ++k) {
-      const int a = Bf.cons[2 * k], c2 = Bf.cons[2 * k + 1];
-      if (a != j && c2 != j) continue;
-      const double* l = Bf.lenJ + (((size_t)b * F + f) * D.NL + k) * 5;
-      for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) A[r][c] += l[r] * l[c];
-    }
-    const double sd = s2 * dtd(f, f, F, n, D.c);
-    for (int i = 0; i < 3; ++i) {
-      const double dg = Bf.diag[(size_t)b * D.NV + (size_t)f * J * 3 + 3 * j + i];
-      A[i][i] += sd + lam * damp_of(dg);
-    }
-    double* cur = fb + (size_t)f * 36;
-    for (int d = n; d >= 1; --d) {
-      const int i = f - d;
-      if (i < 0) {
-        for (int e = 0; e < 9; ++e) cur[9 * d + e] = 0;
-        continue;
-      }
-      double M[3][3];
-      const double off = s2 * dtd(f, i, F, n, D.c);
-      for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) M[r][c] = (r == c) ? off : 0.0;
-      for (int e = d + 1; e <= n; ++e) {
-        if (f - e < 0) break;
-        const double* Lf = cur + 9 * e;                                 // L_{f, f-e}
-        const double* Li = fb + (size_t)i * 36 + 9 * (e - d);          // L_{i, f-e}
-        for (int r = 0; r < 3; ++r)
-          for (int c = 0; c < 3; ++c)
-            M[r][c] -= Lf[3 * r] * Li[3 * c] + Lf[3 * r + 1] * Li[3 * c + 1] + Lf[3 * r + 2] * Li[3 * c + 2];
-      }
-      const double* Ii = fb + (size_t)i * 36;  // inv(L_ii) (lower)
-      // L_{f,i} = M L_ii^{-T}:  (M Ii^T)[r][c] = sum_k M[r][k] Ii[c][k]
-      for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c)
-          cur[9 * d + 3 * r + c] = M[r][0] * Ii[3 * c] + M[r][1] * Ii[3 * c + 1] + M[r][2] * Ii[3 * c + 2];
-    }
-    for (int d = 1; d <= n; ++d) {
-      if (f - d < 0) break;
-      const double* Lf = cur + 9 * d;
-      for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c)
-          A[r][c] -= Lf[3 * r] * Lf[3 * c] + Lf[3 * r + 1] * Lf[3 * c + 1] + Lf[3 * r + 2] * Lf[3 * c + 2];
-    }
-    // 3x3 Cholesky and its inverse
-    const double l00 = sqrt(fmax(A[0][0], 1e-300));
-    const double l10 = A[1][0] / l00, l20 = A[2][0] / l00;
-    const double l11 = sqrt(fmax(A[1][1] - l10 * l10, 1e-300));
-    const double l21 = (A[2][1] - l20 * l10) / l11;
-    const double l22 = sqrt(fmax(A[2][2] - l20 * l20 - l21 * l21, 1e-300));
-    const double i00 = 1 / l00, i11 = 1 / l11, i22 = 1 / l22;
-    const double i10 = -l10 * i00 * i11;
-    const double i21 = -l21 * i11 * i22;
-    const double i20 = -(l20 * i00 + l21 * i10) * i22;
-    const double inv[9] = {i00, 0, 0, i10, i11, 0, i20, i21, i22};
-    for (int e = 0; e < 9; ++e) cur[e] = inv[e];
-  }
+  if (D.n == 1) factor_series<1>(D, Bf, b, j, lam);
+  else if (D.n == 2) factor_series<2>(D, Bf, b, j, lam);
+  else factor_series<3>(D, Bf, b, j, lam);
 }
 
 __device__ __forceinline__ double rz_at(const OptDims& D, const OptBufs& Bf, int b, int it) {
@@ -365,9 +431,155 @@ __device__ __forceinline__ bool pcg_done(const OptDims& D, const OptBufs& Bf, in
 
 // z = M^-1 r for one joint series (and the length diagonal for j == J); it < 0: init (d = 0, r = -g),
 // else first d += alpha p_it, r -= alpha q_it.  Writes the series' r.z partial to rzJ[it + 1].
-__global__ void optim_precond_kernel(OptDims D, OptBufs Bf, int it) {
+// Both substitutions keep the last NN solution vectors in registers and load frame f+-1's
+// inputs while frame f is solved (the recurrence is latency-bound, one thread per series).
+template <int NN>
+__device__ double solve_series(const OptDims& D, const OptBufs& Bf, int b, int j, int it, double alpha,
+                               const double* __restrict__ P) {
+  const int F = D.F, J = D.J, J3 = 3 * J;
+  const size_t base = (size_t)b * D.NV + 3 * j;
+  const double* __restrict__ fb = Bf.fac + ((size_t)b * J + j) * F * 36;
+  double* __restrict__ z = Bf.z;
+  double* __restrict__ r = Bf.r;
+  double* __restrict__ dd = Bf.d;
+  const double* __restrict__ g = Bf.g;
+  const double* __restrict__ q = Bf.q;
+  struct In {
+    double rec[9 + 9 * NN];
+    double r[3], d[3], p[3], q[3];
+  };
+  auto load_in = [&](int f, In& x) {
+    const double* rc = fb + (size_t)f * 36;
+#pragma unroll
+    for (int e = 0; e < 9 + 9 * NN; ++e) x.rec[e] = rc[e];
+    const size_t o = base + (size_t)f * J3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (it < 0) {
+        x.r[i] = -g[o + i];
+      } else {
+        x.r[i] = r[o + i];
+        x.d[i] = dd[o + i];
+        x.p[i] = P[o + i];
+        x.q[i] = q[o + i];
+      }
+    }
+  };
+  double Y[NN][3];
+#pragma unroll
+  for (int k = 0; k < NN; ++k) Y[k][0] = Y[k][1] = Y[k][2] = 0.0;
+  In nx;
+  load_in(0, nx);
+  for (int f = 0; f < F; ++f) {  // forward: L y = r
+    const In cu = nx;
+    if (f + 1 < F) load_in(f + 1, nx);
+    const size_t o = base + (size_t)f * J3;
+    double rr[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (it < 0) {
+        dd[o + i] = 0.0;
+        rr[i] = cu.r[i];
+      } else {
+        dd[o + i] = cu.d[i] + alpha * cu.p[i];
+        rr[i] = cu.r[i] - alpha * cu.q[i];
+      }
+      r[o + i] = rr[i];
+    }
+    double w[3] = {rr[0], rr[1], rr[2]};
+#pragma unroll
+    for (int d = 1; d <= NN; ++d) {
+      const double* Lf = cu.rec + 9 * d;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        w[i] -= Lf[3 * i] * Y[d - 1][0] + Lf[3 * i + 1] * Y[d - 1][1] + Lf[3 * i + 2] * Y[d - 1][2];
+    }
+    const double* I = cu.rec;
+    const double y0 = I[0] * w[0];
+    const double y1 = I[3] * w[0] + I[4] * w[1];
+    const double y2 = I[6] * w[0] + I[7] * w[1] + I[8] * w[2];
+    z[o] = y0;
+    z[o + 1] = y1;
+    z[o + 2] = y2;
+#pragma unroll
+    for (int k = NN - 1; k >= 1; --k) {
+      Y[k][0] = Y[k - 1][0];
+      Y[k][1] = Y[k - 1][1];
+      Y[k][2] = Y[k - 1][2];
+    }
+    Y[0][0] = y0;
+    Y[0][1] = y1;
+    Y[0][2] = y2;
+  }
+  // backward: L^T z = y.  Frame f needs inv(L_ff), L_{f+d,f} (block d of frame f+d), y_f, r_f.
+  struct Bk {
+    double inv[9];
+    double Ld[NN][9];
+    double y[3], r[3];
+  };
+  auto load_bk = [&](int f, Bk& x) {
+    const double* rc = fb + (size_t)f * 36;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) x.inv[e] = rc[e];
+#pragma unroll
+    for (int d = 1; d <= NN; ++d) {
+      if (f + d < F) {
+        const double* rd = fb + (size_t)(f + d) * 36 + 9 * d;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) x.Ld[d - 1][e] = rd[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) x.Ld[d - 1][e] = 0.0;
+      }
+    }
+    const size_t o = base + (size_t)f * J3;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      x.y[i] = z[o + i];
+      x.r[i] = r[o + i];
+    }
+  };
+  double Z[NN][3];
+#pragma unroll
+  for (int k = 0; k < NN; ++k) Z[k][0] = Z[k][1] = Z[k][2] = 0.0;
+  double rz = 0;
+  Bk bn;
+  load_bk(F - 1, bn);
+  for (int f = F - 1; f >= 0; --f) {
+    const Bk bc = bn;
+    if (f > 0) load_bk(f - 1, bn);
+    double w[3] = {bc.y[0], bc.y[1], bc.y[2]};
+#pragma unroll
+    for (int d = 1; d <= NN; ++d) {
+      const double* Ld = bc.Ld[d - 1];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) w[i] -= Ld[i] * Z[d - 1][0] + Ld[3 + i] * Z[d - 1][1] + Ld[6 + i] * Z[d - 1][2];
+    }
+    const double* I = bc.inv;
+    const double z0 = I[0] * w[0] + I[3] * w[1] + I[6] * w[2];
+    const double z1 = I[4] * w[1] + I[7] * w[2];
+    const double z2 = I[8] * w[2];
+    const size_t o = base + (size_t)f * J3;
+    z[o] = z0;
+    z[o + 1] = z1;
+    z[o + 2] = z2;
+    rz += bc.r[0] * z0 + bc.r[1] * z1 + bc.r[2] * z2;
+#pragma unroll
+    for (int k = NN - 1; k >= 1; --k) {
+      Z[k][0] = Z[k - 1][0];
+      Z[k][1] = Z[k - 1][1];
+      Z[k][2] = Z[k - 1][2];
+    }
+    Z[0][0] = z0;
+    Z[0][1] = z1;
+    Z[0][2] = z2;
+  }
+  return rz;
+}
+
+__global__ void __launch_bounds__(64) optim_precond_kernel(OptDims D, OptBufs Bf, int it) {
   const int b = blockIdx.x, j = threadIdx.x;
-  const int F = D.F, J = D.J, n = D.n, J3 = 3 * J;
+  const int J = D.J;
   if (j > J) return;
   double alpha = 0;
   const double* P = (it & 1) ? Bf.P1 : Bf.P0;
@@ -396,50 +608,12 @@ __global__ void optim_precond_kernel(OptDims D, OptBufs Bf, int it) {
         Bf.z[o] = z;
         rz += r * z;
       }
+  } else if (D.n == 1) {
+    rz = solve_series<1>(D, Bf, b, j, it, alpha, P);
+  } else if (D.n == 2) {
+    rz = solve_series<2>(D, Bf, b, j, it, alpha, P);
   } else {
-    const double* fb = Bf.fac + ((size_t)b * J + j) * F * 36;
-    for (int f = 0; f < F; ++f) {  // forward: L y = r
-      const size_t o = base + (size_t)f * J3 + 3 * j;
-      double r[3];
-      for (int i = 0; i < 3; ++i) {
-        if (it < 0) {
-          Bf.d[o + i] = 0;
-          r[i] = -Bf.g[o + i];
-        } else {
-          Bf.d[o + i] += alpha * P[o + i];
-          r[i] = Bf.r[o + i] - alpha * Bf.q[o + i];
-        }
-        Bf.r[o + i] = r[i];
-      }
-      double w[3] = {r[0], r[1], r[2]};
-      const double* cur = fb + (size_t)f * 36;
-      for (int d = 1; d <= n && f - d >= 0; ++d) {
-        const double* y = Bf.z + base + (size_t)(f - d) * J3 + 3 * j;
-        const double* Lf = cur + 9 * d;
-        for (int i = 0; i < 3; ++i) w[i] -= Lf[3 * i] * y[0] + Lf[3 * i + 1] * y[1] + Lf[3 * i + 2] * y[2];
-      }
-      double* y = Bf.z + o;
-      y[0] = cur[0] * w[0];
-      y[1] = cur[3] * w[0] + cur[4] * w[1];
-      y[2] = cur[6] * w[0] + cur[7] * w[1] + cur[8] * w[2];
-    }
-    for (int f = F - 1; f >= 0; --f) {  // backward: L^T z = y
-      const size_t o = base + (size_t)f * J3 + 3 * j;
-      double w[3] = {Bf.z[o], Bf.z[o + 1], Bf.z[o + 2]};
-      for (int d = 1; d <= n && f + d < F; ++d) {
-        const double* zz = Bf.z + base + (size_t)(f + d) * J3 + 3 * j;
-        const double* Ld = fb + (size_t)(f + d) * 36 + 9 * d;  // L_{f+d, f}
-        for (int i = 0; i < 3; ++i) w[i] -= Ld[i] * zz[0] + Ld[3 + i] * zz[1] + Ld[6 + i] * zz[2];
-      }
-      const double* I = fb + (size_t)f * 36;  // z = I^T w
-      const double z0 = I[0] * w[0] + I[3] * w[1] + I[6] * w[2];
-      const double z1 = I[4] * w[1] + I[7] * w[2];
-      const double z2 = I[8] * w[2];
-      Bf.z[o] = z0;
-      Bf.z[o + 1] = z1;
-      Bf.z[o + 2] = z2;
-      rz += Bf.r[o] * z0 + Bf.r[o + 1] * z1 + Bf.r[o + 2] * z2;
-    }
+    rz = solve_series<3>(D, Bf, b, j, it, alpha, P);
   }
   Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
 }

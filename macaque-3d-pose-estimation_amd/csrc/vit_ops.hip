@@ -72,10 +72,16 @@ int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, un
 //   softmax over the 192 tokens = in-register reduction + 2 cross-lane steps,
 //   O = P V with v_mfma_f32_16x16x32_bf16; the accumulator S^T is re-used as the
 //   A operand of PV without going through LDS (k-slot permutation matched in V).
-template <int DH>
-__global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
-                                                         int T, int D, int H, float scale_log2) {
-  constexpr int KS = DH + 4;       // K row stride (elements)
+constexpr int ATT_WAVES = 6;  // 12 query blocks of 16 at T = 192: two per wave
+constexpr int ATT_THREADS = 64 * ATT_WAVES;
+
+// MODE (timing ablations only, results are wrong when non-zero): 1 = staging only, 2 = no K/V
+// global loads (LDS left as is), 3 = no output stores.
+template <int DH, int MODE = 0>
+__global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const bf16_t* __restrict__ qkv,
+                                                                 bf16_t* __restrict__ out, int T, int D, int H,
+                                                                 float scale_log2) {
+  constexpr int KS = DH + 8;       // K row stride (elements): 176 B rows -> conflict-free ds_read_b64
   constexpr int NKS = DH / 16;     // k-steps of QK^T
   constexpr int MAXT = 192;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -86,33 +92,80 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
   const int img = blockIdx.x / H, h = blockIdx.x % H;
   const size_t row0 = (size_t)img * T;
   const int ld = 3 * D;
-  // stage K and V^T
-  for (int c = threadIdx.x; c < T * (DH / 8); c += blockDim.x) {
-    const int t = c / (DH / 8), ch = c % (DH / 8);
-    const bf16_t* src = qkv + (row0 + t) * ld + h * DH + ch * 8;
-    const uint4 kv = *reinterpret_cast<const uint4*>(src + D);
-    const uint4 vv = *reinterpret_cast<const uint4*>(src + 2 * D);
-    uint2* kd = reinterpret_cast<uint2*>(Ks + t * KS + ch * 8);
-    kd[0] = make_uint2(kv.x, kv.y);
-    kd[1] = make_uint2(kv.z, kv.w);
-    const unsigned vw[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      Vt[(ch * 8 + 2 * e) * VS + t] = (bf16_t)(vw[e] & 0xffff);
-      Vt[(ch * 8 + 2 * e + 1) * VS + t] = (bf16_t)(vw[e] >> 16);
-    }
-  }
-  __syncthreads();
-
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int ntb = T / 16;
-  for (int qb = wave; qb < T / 16; qb += 4) {
-    const int q = qb * 16 + l16;
-    short4v qf[NKS];
+  // this wave's query blocks (wave, wave + ATT_WAVES): Q fragments are loaded first so their
+  // latency overlaps the K/V staging
+  constexpr int QB_PER_WAVE = (MAXT / 16 + ATT_WAVES - 1) / ATT_WAVES;
+  short4v qf_all[QB_PER_WAVE][NKS];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-      qf[ks] = *reinterpret_cast<const short4v*>(qkv + (row0 + q) * ld + h * DH + ks * 16 + 4 * g);
+  for (int u = 0; u < QB_PER_WAVE; ++u) {
+    const int qb = wave + u * ATT_WAVES;
+    if (qb < ntb) {
+      const int q = qb * 16 + l16;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        qf_all[u][ks] = *reinterpret_cast<const short4v*>(qkv + (row0 + q) * ld + h * DH + ks * 16 + 4 * g);
+    }
+  }
+  // stage K and V^T.  All of a thread's global loads are issued before any LDS store (one
+  // memory latency per workgroup instead of one per loop trip); work items are token PAIRS so
+  // V^T is written as packed (t, t+1) 32-bit words.
+  constexpr int CH = DH / 8;
+  constexpr int ITEMS = (MAXT / 2) * CH;
+  constexpr int PER = (ITEMS + ATT_THREADS - 1) / ATT_THREADS;
+  const int items = (T / 2) * CH;
+  uint4 kv[PER][2], vv[PER][2];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + i * ATT_THREADS;
+    if (c < items) {
+      const int tp = c / CH, ch = c % CH;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16_t* src = qkv + (row0 + 2 * tp + u) * ld + h * DH + ch * 8;
+        if constexpr (MODE == 2) {
+          kv[i][u] = make_uint4(c, u, 0, 0);
+          vv[i][u] = make_uint4(0, c, u, 0);
+        } else {
+          kv[i][u] = *reinterpret_cast<const uint4*>(src + D);
+          vv[i][u] = *reinterpret_cast<const uint4*>(src + 2 * D);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + i * ATT_THREADS;
+    if (c < items) {
+      const int tp = c / CH, ch = c % CH;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        uint2* kd = reinterpret_cast<uint2*>(Ks + (2 * tp + u) * KS + ch * 8);
+        kd[0] = make_uint2(kv[i][u].x, kv[i][u].y);
+        kd[1] = make_uint2(kv[i][u].z, kv[i][u].w);
+      }
+      const unsigned v0[4] = {vv[i][0].x, vv[i][0].y, vv[i][0].z, vv[i][0].w};
+      const unsigned v1[4] = {vv[i][1].x, vv[i][1].y, vv[i][1].z, vv[i][1].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        *reinterpret_cast<unsigned*>(Vt + (ch * 8 + 2 * e) * VS + 2 * tp) = (v0[e] & 0xffffu) | (v1[e] << 16);
+        *reinterpret_cast<unsigned*>(Vt + (ch * 8 + 2 * e + 1) * VS + 2 * tp) = (v0[e] >> 16) | (v1[e] & 0xffff0000u);
+      }
+    }
+  }
+  __syncthreads();
+  if constexpr (MODE == 1) {
+    if (threadIdx.x == 0) out[row0 * D + h * DH] = Ks[wave] + Vt[lane];
+    return;
+  }
+
+#pragma unroll
+  for (int u = 0; u < QB_PER_WAVE; ++u) {
+    const int qb = wave + u * ATT_WAVES;
+    if (qb >= ntb) break;
+    const short4v* qf = qf_all[u];
     f32x4 S[MAXT / 16];
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb) {
@@ -139,7 +192,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
       if (tb < ntb) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float p = exp2f(S[tb][e] * scale_log2 - mb);
+          const float p = __builtin_amdgcn_exp2f(S[tb][e] * scale_log2 - mb);
           S[tb][e] = p;
           lsum += p;
         }
@@ -181,23 +234,37 @@ __global__ __launch_bounds__(256) void attention_kernel(const bf16_t* __restrict
       const float inv = 1.0f / __shfl(lsum, 4 * g + e, 64);
       const int qq = qb * 16 + 4 * g + e;
       bf16_t* orow = out + (row0 + qq) * D + h * DH;
+      if constexpr (MODE == 3) {
+        float acc3 = 0.f;
 #pragma unroll
-      for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = f32_to_bf16(O[dt][e] * inv);
+        for (int dt = 0; dt < NKS; ++dt) acc3 += O[dt][e] * inv;
+        if (acc3 == 12345.678f) orow[l16] = 1;
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = f32_to_bf16(O[dt][e] * inv);
+      }
     }
   }
 }
+
+int g_attention_ablate = 0;
 
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s) {
   const int dh = dim / heads;
   if (tokens % 32 || tokens > 192 || dh * heads != dim) return -1;
   const float scale_log2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
-  dim3 grid(n_img * heads), block(256);
+  dim3 grid(n_img * heads), block(ATT_THREADS);
   if (dh == 80) {
-    const size_t lds = (192 * (80 + 4) + 80 * (tokens + 8)) * 2;
-    hipLaunchKernelGGL(attention_kernel<80>, grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+    const size_t lds = (192 * (80 + 8) + 80 * (tokens + 8)) * 2;
+    switch (g_attention_ablate) {
+      case 1: hipLaunchKernelGGL((attention_kernel<80, 1>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
+      case 2: hipLaunchKernelGGL((attention_kernel<80, 2>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
+      case 3: hipLaunchKernelGGL((attention_kernel<80, 3>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
+      default: hipLaunchKernelGGL((attention_kernel<80, 0>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+    }
   } else if (dh == 64) {
-    const size_t lds = (192 * (64 + 4) + 64 * (tokens + 8)) * 2;
+    const size_t lds = (192 * (64 + 8) + 64 * (tokens + 8)) * 2;
     hipLaunchKernelGGL(attention_kernel<64>, grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
   } else {
     return -2;

@@ -50,14 +50,20 @@ def _run(M, N, K, epi, aux_rows=0, seed=0):
     return err, scale
 
 
-@pytest.fixture(params=[0, 1], ids=["glds", "bufload"])
+@pytest.fixture(params=[(0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 0, 1)],
+                ids=["glds", "bufload", "mfma32", "bufload-mfma32", "sched"])
 def staging(request):
-    """Both LDS-DMA staging forms of the 256x256 kernel (MQ_TUNE_GEMM_BUFLOAD)."""
+    """Every variant of the 256x256 kernel: LDS-DMA staging form (MQ_TUNE_GEMM_BUFLOAD) x
+    MFMA shape (MQ_TUNE_GEMM_MFMA32: 32x32x16 vs 16x16x32) x interleaved K-step (MQ_TUNE_GEMM_SCHED)."""
     from mqhip import _lib
     ctx = _lib.Context.get(0)
-    assert ctx.lib.mq_set_tuning(5, request.param) == 0
+    keys = (5, 6, 7)
+    old = [ctx.lib.mq_get_tuning(k) for k in keys]
+    for k, v in zip(keys, request.param):
+        assert ctx.lib.mq_set_tuning(k, v) == 0
     yield request.param
-    ctx.lib.mq_set_tuning(5, 0)
+    for k, v in zip(keys, old):
+        ctx.lib.mq_set_tuning(k, v)
 
 
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])

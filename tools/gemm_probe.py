@@ -41,11 +41,19 @@ def main():
       for var in variants:
         ctx.lib.mq_set_tuning(3, 0)
         ctx.lib.mq_set_tuning(5, 0)
-        if var.startswith("buf"):
+        ctx.lib.mq_set_tuning(6, 0)
+        ctx.lib.mq_set_tuning(7, 0)
+        var_st = var
+        if var == "sch":
+            ctx.lib.mq_set_tuning(7, 1)
+            var_st = "4"
+        if var in ("m32", "bm32"):
+            ctx.lib.mq_set_tuning(6, 1)
+            ctx.lib.mq_set_tuning(5, 1 if var == "bm32" else 0)
+            var_st = "4"
+        elif var.startswith("buf"):
             ctx.lib.mq_set_tuning(5, 1)
             var_st = var[3:]
-        else:
-            var_st = var
         if var == "torch":
             for name in names:
                 res[f"{name}/{var}/r{rnd}"] = bench_torch(torch, name, args.iters)
