@@ -66,182 +66,195 @@ int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, un
 }
 
 // ---------------------------------------------------------------- attention
-// One workgroup per (image, head).  K is staged row-major and V transposed in LDS
-// (T x DH each, <= 30 KB bf16 at T=192, DH=80).  Each wave takes 16-query blocks:
-//   S^T = K Q^T with v_mfma_f32_16x16x16_bf16 (query on the lane, tokens in regs),
-//   softmax over the 192 tokens = in-register reduction + 2 cross-lane steps,
-//   O = P V with v_mfma_f32_16x16x32_bf16; the accumulator S^T is re-used as the
-//   A operand of PV without going through LDS (k-slot permutation matched in V).
+// One workgroup (6 waves) per (image, head).  K and V are staged ROW-MAJOR in LDS by LDS-DMA
+// (global_load_lds_dwordx4: no VGPR round trip, no packing VALU, conflict-free lane-linear
+// writes); Q fragments go straight to registers.  Each wave owns two 16-query blocks and runs
+// them together:
+//   S^T = K Q^T   v_mfma_f32_16x16x16_bf16 (query on the lane, tokens in registers), K read by
+//                 rows (ds_read_b64) from an image with 11 x 16-B chunks per row (conflict-free);
+//   softmax       in registers + 2 cross-lane steps, P packed to bf16 in PV operand order;
+//   O = P V       v_mfma_f32_16x16x32_bf16 with the V operand gathered by ds_read_b64_tr_b16
+//                 (hardware transpose) from a row-major image whose row stride (40 dwords) makes
+//                 the transposed reads conflict-free.
 constexpr int ATT_WAVES = 6;  // 12 query blocks of 16 at T = 192: two per wave
 constexpr int ATT_THREADS = 64 * ATT_WAVES;
+constexpr int ATT_MAXT = 192;
 
-// MODE (timing ablations only, results are wrong when non-zero): 1 = staging only, 2 = no K/V
-// global loads (LDS left as is), 3 = no output stores.
-template <int DH, int MODE = 0>
-__global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const bf16_t* __restrict__ qkv,
-                                                                 bf16_t* __restrict__ out, int T, int D, int H,
-                                                                 float scale_log2) {
-  constexpr int KS = DH + 8;       // K row stride (elements): 176 B rows -> conflict-free ds_read_b64
-  constexpr int NKS = DH / 16;     // k-steps of QK^T
-  constexpr int MAXT = 192;
+template <int DH>
+struct AttLayout {
+  static constexpr int KCH = DH / 8 + 1;           // K row: DH/8 data chunks + 1 pad chunk
+  static constexpr int VCH = DH == 64 ? 10 : DH / 8;  // V row stride in 16-B chunks (= 8 * odd dwords mod 64)
+  static constexpr int KBYTES = (ATT_MAXT * KCH + 63) / 64 * 1024;
+  static constexpr int VBYTES = (ATT_MAXT * VCH + 63) / 64 * 1024;
+  static constexpr int LDS = KBYTES + VBYTES;
+};
+
+// MODE (timing ablations only, results are wrong when non-zero): 1 = staging only, 3 = no output
+// stores.  TT: compile-time token count (192 = the ViT-H 256x192 grid) so every per-block guard
+// folds away; 0 = runtime T (other grids / tests).
+template <int DH, int MODE = 0, int TT = 0>
+__global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t* __restrict__ qkv,
+                                                                    bf16_t* __restrict__ out, int T_rt, int D,
+                                                                    int H, float scale_log2) {
+  using L = AttLayout<DH>;
+  const int T = TT ? TT : T_rt;
+  constexpr int NKS = DH / 16;  // k-steps of QK^T
+  constexpr int DCH = DH / 8;   // data chunks per row
+  constexpr int MAXT = ATT_MAXT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
-  const int VS = T + 8;  // Vt row stride
-  bf16_t* Vt = Ks + MAXT * KS;
+  char* Kimg = smem;
+  char* Vimg = smem + L::KBYTES;
 
   const int img = blockIdx.x / H, h = blockIdx.x % H;
   const size_t row0 = (size_t)img * T;
   const int ld = 3 * D;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, g = lane >> 4;
   const int ntb = T / 16;
-  // this wave's query blocks (wave, wave + ATT_WAVES): Q fragments are loaded first so their
-  // latency overlaps the K/V staging
+
+  // K / V images by LDS-DMA: instruction i of the image writes chunks 64 i .. 64 i + 63
+  // (lane-linear); a chunk is (token, 16-B piece); pad / tail lanes re-load chunk 0.
+  const bf16_t* kbase = qkv + row0 * ld + D + h * DH;
+  const bf16_t* vbase = kbase + D;
+  const int nk_ins = (T * L::KCH + 63) / 64, nv_ins = (T * L::VCH + 63) / 64;
+  for (int ins = wave; ins < nk_ins; ins += ATT_WAVES) {
+    const int q = ins * 64 + lane;
+    int t = q / L::KCH, ch = q - (q / L::KCH) * L::KCH;
+    if (t >= T || ch >= DCH) t = 0, ch = 0;
+    __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(kbase + (size_t)t * ld + ch * 8), MQ_LDS_LOCAL(Kimg + ins * 1024),
+                                     16, 0, 0);
+  }
+  for (int ins = wave; ins < nv_ins; ins += ATT_WAVES) {
+    const int q = ins * 64 + lane;
+    int t = q / L::VCH, ch = q - (q / L::VCH) * L::VCH;
+    if (t >= T || ch >= DCH) t = 0, ch = 0;
+    __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(vbase + (size_t)t * ld + ch * 8), MQ_LDS_LOCAL(Vimg + ins * 1024),
+                                     16, 0, 0);
+  }
+  // this wave's query blocks (wave, wave + ATT_WAVES): Q fragments straight to registers
   constexpr int QB_PER_WAVE = (MAXT / 16 + ATT_WAVES - 1) / ATT_WAVES;
-  short4v qf_all[QB_PER_WAVE][NKS];
+  static_assert(QB_PER_WAVE == 2, "two query blocks per wave");
+  short4v qf[2][NKS];
 #pragma unroll
-  for (int u = 0; u < QB_PER_WAVE; ++u) {
-    const int qb = wave + u * ATT_WAVES;
-    if (qb < ntb) {
-      const int q = qb * 16 + l16;
+  for (int u = 0; u < 2; ++u) {
+    const int qb = min(wave + u * ATT_WAVES, ntb - 1);
+    const int q = qb * 16 + l16;
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        qf_all[u][ks] = *reinterpret_cast<const short4v*>(qkv + (row0 + q) * ld + h * DH + ks * 16 + 4 * g);
-    }
+    for (int ks = 0; ks < NKS; ++ks)
+      qf[u][ks] = *reinterpret_cast<const short4v*>(qkv + (row0 + q) * ld + h * DH + ks * 16 + 4 * g);
   }
-  // stage K and V^T.  All of a thread's global loads are issued before any LDS store (one
-  // memory latency per workgroup instead of one per loop trip); work items are token PAIRS so
-  // V^T is written as packed (t, t+1) 32-bit words.
-  constexpr int CH = DH / 8;
-  constexpr int ITEMS = (MAXT / 2) * CH;
-  constexpr int PER = (ITEMS + ATT_THREADS - 1) / ATT_THREADS;
-  const int items = (T / 2) * CH;
-  uint4 kv[PER][2], vv[PER][2];
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = threadIdx.x + i * ATT_THREADS;
-    if (c < items) {
-      const int tp = c / CH, ch = c % CH;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const bf16_t* src = qkv + (row0 + 2 * tp + u) * ld + h * DH + ch * 8;
-        if constexpr (MODE == 2) {
-          kv[i][u] = make_uint4(c, u, 0, 0);
-          vv[i][u] = make_uint4(0, c, u, 0);
-        } else {
-          kv[i][u] = *reinterpret_cast<const uint4*>(src + D);
-          vv[i][u] = *reinterpret_cast<const uint4*>(src + 2 * D);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = threadIdx.x + i * ATT_THREADS;
-    if (c < items) {
-      const int tp = c / CH, ch = c % CH;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        uint2* kd = reinterpret_cast<uint2*>(Ks + (2 * tp + u) * KS + ch * 8);
-        kd[0] = make_uint2(kv[i][u].x, kv[i][u].y);
-        kd[1] = make_uint2(kv[i][u].z, kv[i][u].w);
-      }
-      const unsigned v0[4] = {vv[i][0].x, vv[i][0].y, vv[i][0].z, vv[i][0].w};
-      const unsigned v1[4] = {vv[i][1].x, vv[i][1].y, vv[i][1].z, vv[i][1].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        *reinterpret_cast<unsigned*>(Vt + (ch * 8 + 2 * e) * VS + 2 * tp) = (v0[e] & 0xffffu) | (v1[e] << 16);
-        *reinterpret_cast<unsigned*>(Vt + (ch * 8 + 2 * e + 1) * VS + 2 * tp) = (v0[e] >> 16) | (v1[e] & 0xffff0000u);
-      }
-    }
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (MODE == 1) {
-    if (threadIdx.x == 0) out[row0 * D + h * DH] = Ks[wave] + Vt[lane];
+    if (threadIdx.x == 0) out[row0 * D + h * DH] = *reinterpret_cast<const bf16_t*>(Kimg + 16 * wave) + qf[0][0][0];
     return;
   }
+  if (wave >= ntb) return;
+  const bool has1 = (TT == MAXT) ? true : (wave + ATT_WAVES < ntb);
 
+  f32x4 S[2][MAXT / 16];
 #pragma unroll
-  for (int u = 0; u < QB_PER_WAVE; ++u) {
-    const int qb = wave + u * ATT_WAVES;
-    if (qb >= ntb) break;
-    const short4v* qf = qf_all[u];
-    f32x4 S[MAXT / 16];
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int tb = 0; tb < MAXT / 16; ++tb) S[u][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb) {
-      S[tb] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (tb < ntb) {
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          const short4v kf = *reinterpret_cast<const short4v*>(Ks + (tb * 16 + l16) * KS + ks * 16 + 4 * g);
-          S[tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[ks], S[tb], 0, 0, 0);
-        }
+        const short4v kf =
+            *reinterpret_cast<const short4v*>(Kimg + (tb * 16 + l16) * (L::KCH * 16) + (ks * 16 + 4 * g) * 2);
+        S[0][tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[0][ks], S[0][tb], 0, 0, 0);
+        if (has1) S[1][tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[1][ks], S[1][tb], 0, 0, 0);
       }
     }
-    // softmax over tokens for query q (column l16): values spread over regs and lanes g
+  }
+  // softmax over tokens for query (column l16): values spread over registers and lane groups g;
+  // P is packed to bf16 in the PV operand order (tokens tb0*16+4g+0..3, (tb0+1)*16+4g+0..3)
+  bf16x8 P[2][MAXT / 32];
+  float lsum[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
     float m = -INFINITY;
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb)
-      if (tb < ntb) m = fmaxf(m, fmaxf(fmaxf(S[tb][0], S[tb][1]), fmaxf(S[tb][2], S[tb][3])));
+      if (tb < ntb) m = fmaxf(m, fmaxf(fmaxf(S[u][tb][0], S[u][tb][1]), fmaxf(S[u][tb][2], S[u][tb][3])));
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
     const float mb = m * scale_log2;
-    float lsum = 0.f;
+    float ls = 0.f;
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb) {
       if (tb < ntb) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float p = __builtin_amdgcn_exp2f(S[tb][e] * scale_log2 - mb);
-          S[tb][e] = p;
-          lsum += p;
+          const float pv = __builtin_amdgcn_exp2f(S[u][tb][e] * scale_log2 - mb);
+          S[u][tb][e] = pv;
+          ls += pv;
         }
       }
     }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-
-    f32x4 O[NKS];
-#pragma unroll
-    for (int dt = 0; dt < NKS; ++dt) O[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    lsum[u] = ls;
 #pragma unroll
     for (int kst = 0; kst < MAXT / 32; ++kst) {
-      if (kst < T / 32) {
-        const int tb0 = 2 * kst;
-        bf16x8 pa;
-        pa[0] = (__bf16)S[tb0][0];
-        pa[1] = (__bf16)S[tb0][1];
-        pa[2] = (__bf16)S[tb0][2];
-        pa[3] = (__bf16)S[tb0][3];
-        pa[4] = (__bf16)S[tb0 + 1][0];
-        pa[5] = (__bf16)S[tb0 + 1][1];
-        pa[6] = (__bf16)S[tb0 + 1][2];
-        pa[7] = (__bf16)S[tb0 + 1][3];
 #pragma unroll
-        for (int dt = 0; dt < NKS; ++dt) {
-          const bf16_t* vrow = Vt + (dt * 16 + l16) * VS;
-          const uint2 v0 = *reinterpret_cast<const uint2*>(vrow + tb0 * 16 + 4 * g);
-          const uint2 v1 = *reinterpret_cast<const uint2*>(vrow + (tb0 + 1) * 16 + 4 * g);
-          const uint4 vv = make_uint4(v0.x, v0.y, v1.x, v1.y);
-          const bf16x8 vb = *reinterpret_cast<const bf16x8*>(&vv);
-          O[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, O[dt], 0, 0, 0);
-        }
+      for (int e = 0; e < 4; ++e) {
+        P[u][kst][e] = (__bf16)S[u][2 * kst][e];
+        P[u][kst][4 + e] = (__bf16)S[u][2 * kst + 1][e];
       }
     }
-    // O C-layout: col = l16 -> d, row = 4g + e -> query; normaliser lives in lane (4g + e)
+  }
+
+  f32x4 O[2][NKS];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < NKS; ++dt) O[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // transposed read: lane 4q+p of each 16-lane group addresses row r0+q, columns c0+4p..+3 and
+  // receives column c0 + (lane & 15) of those 4 rows
+  const int trq = l16 >> 2, trp = l16 & 3;
+#pragma unroll
+  for (int kst = 0; kst < MAXT / 32; ++kst) {
+    if (kst < T / 32) {
+#pragma unroll
+      for (int dt = 0; dt < NKS; ++dt) {
+        const int ra = 2 * kst * 16 + 4 * g + trq;
+        const char* pa = Vimg + ra * (L::VCH * 16) + (dt * 16 + 4 * trp) * 2;
+        const short4v v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa));
+        const short4v v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa + 16 * (L::VCH * 16)));
+        bf16x8 vb;
+        const short4v* pv0 = &v0;
+        const short4v* pv1 = &v1;
+        __builtin_memcpy(&vb, pv0, 8);
+        __builtin_memcpy(reinterpret_cast<char*>(&vb) + 8, pv1, 8);
+        O[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[0][kst], vb, O[0][dt], 0, 0, 0);
+        if (has1) O[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[1][kst], vb, O[1][dt], 0, 0, 0);
+      }
+    }
+  }
+  // O C-layout: col = l16 -> d, row = 4g + e -> query; normaliser lives in lane (4g + e)
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u == 1 && !has1) break;
+    const int qb = wave + u * ATT_WAVES;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float inv = 1.0f / __shfl(lsum, 4 * g + e, 64);
+      const float inv = 1.0f / __shfl(lsum[u], 4 * g + e, 64);
       const int qq = qb * 16 + 4 * g + e;
       bf16_t* orow = out + (row0 + qq) * D + h * DH;
       if constexpr (MODE == 3) {
         float acc3 = 0.f;
 #pragma unroll
-        for (int dt = 0; dt < NKS; ++dt) acc3 += O[dt][e] * inv;
+        for (int dt = 0; dt < NKS; ++dt) acc3 += O[u][dt][e] * inv;
         if (acc3 == 12345.678f) orow[l16] = 1;
       } else {
 #pragma unroll
-        for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = f32_to_bf16(O[dt][e] * inv);
+        for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = __builtin_bit_cast(bf16_t, (__bf16)(O[u][dt][e] * inv));
       }
     }
   }
@@ -249,26 +262,33 @@ __global__ __launch_bounds__(ATT_THREADS) void attention_kernel(const bf16_t* __
 
 int g_attention_ablate = 0;
 
+template <int DH>
+static void launch_attention(dim3 grid, dim3 block, hipStream_t s, const unsigned short* qkv, unsigned short* out,
+                             int tokens, int dim, int heads, float scale_log2) {
+  constexpr int lds = AttLayout<DH>::LDS;
+  if (tokens == ATT_MAXT) {
+    switch (g_attention_ablate) {
+      case 1: hipLaunchKernelGGL((attention_kernel<DH, 1, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
+      case 3: hipLaunchKernelGGL((attention_kernel<DH, 3, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
+      default: hipLaunchKernelGGL((attention_kernel<DH, 0, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+    }
+  } else {
+    hipLaunchKernelGGL((attention_kernel<DH, 0, 0>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+  }
+}
+
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s) {
   const int dh = dim / heads;
-  if (tokens % 32 || tokens > 192 || dh * heads != dim) return -1;
+  if (tokens % 32 || tokens > ATT_MAXT || tokens <= 0 || dh * heads != dim) return -1;
   const float scale_log2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
   dim3 grid(n_img * heads), block(ATT_THREADS);
-  if (dh == 80) {
-    const size_t lds = (192 * (80 + 8) + 80 * (tokens + 8)) * 2;
-    switch (g_attention_ablate) {
-      case 1: hipLaunchKernelGGL((attention_kernel<80, 1>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
-      case 2: hipLaunchKernelGGL((attention_kernel<80, 2>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
-      case 3: hipLaunchKernelGGL((attention_kernel<80, 3>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
-      default: hipLaunchKernelGGL((attention_kernel<80, 0>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
-    }
-  } else if (dh == 64) {
-    const size_t lds = (192 * (64 + 8) + 64 * (tokens + 8)) * 2;
-    hipLaunchKernelGGL(attention_kernel<64>, grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
-  } else {
+  if (dh == 80)
+    launch_attention<80>(grid, block, s, qkv, out, tokens, dim, heads, scale_log2);
+  else if (dh == 64)
+    launch_attention<64>(grid, block, s, qkv, out, tokens, dim, heads, scale_log2);
+  else
     return -2;
-  }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
