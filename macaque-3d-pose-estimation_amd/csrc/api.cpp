@@ -146,6 +146,16 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_GEMM_MFMA32:
       mq::g_gemm_mfma32 = value != 0;
       return 0;
+    case MQ_TUNE_GEMM_BM128:
+      mq::g_gemm_bm128 = value != 0;
+      return 0;
+    case MQ_TUNE_GEMM_SYNC2:
+      mq::g_gemm_sync2 = value != 0;
+      return 0;
+    case MQ_TUNE_GEMM_PRIO:
+      if (value < 0 || value > 2) return fail("mq_set_tuning: GEMM priority mode must be 0, 1 or 2", -2);
+      mq::g_gemm_prio = value;
+      return 0;
     case MQ_TUNE_GEMM_SCHED:
       mq::g_gemm_sched = value != 0;
       return 0;
@@ -171,6 +181,9 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_GEMM_BUFLOAD: return mq::g_gemm_bufload;
     case MQ_TUNE_GEMM_MFMA32: return mq::g_gemm_mfma32;
     case MQ_TUNE_GEMM_SCHED: return mq::g_gemm_sched;
+    case MQ_TUNE_GEMM_BM128: return mq::g_gemm_bm128;
+    case MQ_TUNE_GEMM_PRIO: return mq::g_gemm_prio;
+    case MQ_TUNE_GEMM_SYNC2: return mq::g_gemm_sync2;
     case MQ_TUNE_ATTENTION_ABLATE: return mq::g_attention_ablate;
     default: return fail("mq_get_tuning: unknown key", -2);
   }

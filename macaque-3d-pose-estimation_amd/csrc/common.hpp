@@ -24,8 +24,12 @@ __device__ __forceinline__ bf16_t f32_to_bf16(float f) {
   return (bf16_t)(u >> 16);
 }
 
+// two f32 -> packed bf16 pair, round-to-nearest-even: one v_cvt_pk_bf16_f32 on gfx950
+// (bit-identical to f32_to_bf16 on every non-NaN input; a NaN stays a NaN)
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
-  return (unsigned)f32_to_bf16(a) | ((unsigned)f32_to_bf16(b) << 16);
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(unsigned, v);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -198,20 +198,16 @@ __device__ __forceinline__ bf16x8 frag256(const char* lds_op, int row, int chunk
   return *reinterpret_cast<const bf16x8*>(lds_op + row * 64 + ((chunk ^ swz2(row)) << 4));
 }
 
+// s_waitcnt vmcnt(N) for any N < 64 (the wait leaves the wave's N youngest VMEM ops in flight)
 template <int N_IN_FLIGHT>
 __device__ __forceinline__ void wait_vm() {
-  if constexpr (N_IN_FLIGHT == 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-  else if constexpr (N_IN_FLIGHT == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-  else if constexpr (N_IN_FLIGHT == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if constexpr (N_IN_FLIGHT == 40) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-  else if constexpr (N_IN_FLIGHT == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if constexpr (N_IN_FLIGHT == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if constexpr (N_IN_FLIGHT == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  static_assert(N_IN_FLIGHT >= 0 && N_IN_FLIGHT < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_IN_FLIGHT) : "memory");
 }
 
 // Tile -> (m0, n0): grouped ordering (8 M-tiles per group) so the tiles an XCD works
-// on concurrently share A and W panels in its L2.
+// on concurrently share A and W panels in its L2.  BM = tile rows (256 or 128).
+template <int BM_ = B2M>
 __device__ __forceinline__ void tile_coords(int wid, int tiles_m, int tiles_n, int& m0, int& n0) {
   constexpr int GROUP_M = 8;
   const int per_group = GROUP_M * tiles_n;
@@ -219,19 +215,31 @@ __device__ __forceinline__ void tile_coords(int wid, int tiles_m, int tiles_n, i
   const int first_m = grp * GROUP_M;
   const int gsize = min(tiles_m - first_m, GROUP_M);
   const int in_g = wid - grp * per_group;
-  m0 = (first_m + in_g % gsize) * B2M;
+  m0 = (first_m + in_g % gsize) * BM_;
   n0 = (in_g / gsize) * B2N;
 }
 
 // Persistent: one 512-thread block per CU walks its tiles; the DMA stream and the
 // fragment pipeline run straight across tile boundaries (the first stages of the
 // next tile are in flight while the current tile's epilogue stores drain).
+// MI = 16-row A fragments per wave: 8 -> 256x256 tile (wave 128x64), 4 -> 128x256 tile
+// (wave 64x64).  The 128-row tile is for narrow-N GEMMs (N = 1280: proj, fc2) where the
+// 256x256 grid is one tile per CU and the f32 residual epilogue (a 256 KiB read-modify-write
+// per tile) would run exposed after the K-loop; with two 128-row tiles per CU the first
+// tile's epilogue drains behind the second tile's K-loop.
 // ABL (timing ablations only, outputs are wrong when non-zero): bit0 no steady-state
 // DMA, bit1 no per-step barrier, bit2 no fragment re-reads.
 // BUF: stage with buffer_load_dwordx4 ... lds (32-bit per-lane offset fixed per tile, K advance in
 // soffset) instead of global_load_lds_dwordx4 (64-bit per-lane address rebuilt every stage).
-template <int EPI, int NS, int ABL = 0, bool BUF = false, bool SCHED = false>
+template <int EPI, int NS, int ABL = 0, bool BUF = false, bool SCHED = false, int MI = 8, int PRIO = 0, bool SYNC2 = false>
 __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m, int tiles_n) {
+  static_assert(MI == 8 || MI == 4, "tile rows 256 or 128");
+  constexpr int BMT = 32 * MI;              // tile rows
+  constexpr int NA = BMT / 128;             // A-operand DMA instructions per wave per stage
+  constexpr int A_BYTES = BMT * B2K * 2;    // A operand bytes per stage
+  constexpr int STAGE = A_BYTES + B2_OP_BYTES;
+  constexpr int DMA_PER_STAGE = NA + 2;     // per wave
+  constexpr int WROWS = BMT / 2;            // A rows per wave (2 waves along M)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
@@ -268,36 +276,43 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
   auto set_tile_ptrs = [&](int ti) {
     int m0, n0;
-    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+    tile_coords<BMT>(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int row = (wave * NA + i) * 16 + (lane >> 2);
+      const int chunk = (lane & 3) ^ swz2(row);
+      const int ga = min(m0 + row, p.M - 1);
+      if constexpr (BUF)
+        va[i] = (unsigned)(((size_t)ga * p.lda + chunk * 8) * 2);
+      else
+        pa[i] = p.A + (size_t)ga * p.lda + chunk * 8;
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = (wave * 2 + i) * 16 + (lane >> 2);
       const int chunk = (lane & 3) ^ swz2(row);
-      const int ga = min(m0 + row, p.M - 1), gw = min(n0 + row, p.N - 1);
-      if constexpr (BUF) {
-        va[i] = (unsigned)(((size_t)ga * p.lda + chunk * 8) * 2);
+      const int gw = min(n0 + row, p.N - 1);
+      if constexpr (BUF)
         vw[i] = (unsigned)(((size_t)gw * p.ldw + chunk * 8) * 2);
-      } else {
-        pa[i] = p.A + (size_t)ga * p.lda + chunk * 8;
+      else
         pw[i] = p.W + (size_t)gw * p.ldw + chunk * 8;
-      }
     }
   };
   set_tile_ptrs(0);
   auto issue_a = [&]() {
-    char* sb = smem + iss_slot * B2_STAGE_BYTES;
+    char* sb = smem + iss_slot * STAGE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NA; ++i) {
       if constexpr (BUF)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, va[i],
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(sb + (wave * NA + i) * 16 * 64), 16, va[i],
                                                  iss_k * B2K * 2, 0, 0);
       else
         __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pa[i] + iss_k * B2K),
-                                         MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
+                                         MQ_LDS_LOCAL(sb + (wave * NA + i) * 16 * 64), 16, 0, 0);
     }
   };
   auto issue_w = [&]() {
-    char* sb = smem + iss_slot * B2_STAGE_BYTES + B2_OP_BYTES;
+    char* sb = smem + iss_slot * STAGE + A_BYTES;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if constexpr (BUF)
@@ -322,11 +337,11 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     issue_w();
     advance();
   };
-  auto stage_ptr = [&](int g) { return smem + (g % NS) * B2_STAGE_BYTES; };
+  auto stage_ptr = [&](int g) { return smem + (g % NS) * STAGE; };
 
-  f32x4 acc[8][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -336,21 +351,21 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     issue_a();
     issue_w_and_advance();
   }
-  wait_vm<4 * (NS - 3)>();  // stages 0 and 1 landed (this wave)
+  wait_vm<DMA_PER_STAGE * (NS - 3)>();  // stages 0 and 1 landed (this wave)
   __builtin_amdgcn_s_barrier();
 
-  bf16x8 a[8], b0[4], b1[4];
+  bf16x8 a[MI], b0[4], b1[4];
   {
     const char* As = stage_ptr(0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b0[j] = frag256(As + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
+    for (int j = 0; j < 4; ++j) b0[j] = frag256(As + A_BYTES, wn * 64 + j * 16 + frow, fk);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = frag256(As, wm * 128 + i * 16 + frow, fk);
+    for (int i = 0; i < MI; ++i) a[i] = frag256(As, wm * WROWS + i * 16 + frow, fk);
   }
 
   auto epilogue = [&](int ti) {
     int m0, n0;
-    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+    tile_coords<BMT>(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
     // lane holds D[n][m] with m = l & 15 (col of D) and n = 4 * (l >> 4) + e
     const int mm = lane & 15;
     const int nn = 4 * (lane >> 4);
@@ -368,16 +383,14 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
         bias[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int m = m0 + wm * 128 + i * 16 + mm;
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wm * WROWS + i * 16 + mm;
 #pragma unroll
         for (int jp = 0; jp < 4; jp += 2) {
           unsigned pk[2][2];
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             const int j = jp + h;
-            const int n = n0 + wn * 64 + j * 16 + nn;
-            (void)n;
             float v[4] = {acc[i][j][0] + bias[j].x, acc[i][j][1] + bias[j].y, acc[i][j][2] + bias[j].z,
                           acc[i][j][3] + bias[j].w};
             acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -400,9 +413,71 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       }
       return;
     }
+    if constexpr (EPI == EPI_RESID_F32) {
+      // issue every residual load of the wave's tile first (MI*4 independent 16-B loads in
+      // flight), then add and store: one HBM round trip per tile instead of one per fragment
+      float4 bias[4];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wm * 128 + i * 16 + mm;
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + nn;
+        bias[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      const bool full = (m0 + BMT <= p.M) && (n0 + B2N <= p.N);
+      if (full) {
+        // CH fragment rows of loads in flight at a time (register budget: the accumulators
+        // stay live for the next tile)
+        constexpr int CH = MI == 8 ? 1 : 4;
+#pragma unroll
+        for (int i0 = 0; i0 < MI; i0 += CH) {
+          float4 x[CH][4];
+#pragma unroll
+          for (int c = 0; c < CH; ++c) {
+            const int m = m0 + wm * WROWS + (i0 + c) * 16 + mm;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              x[c][j] = *reinterpret_cast<const float4*>((const float*)p.C + (size_t)m * p.ldc + n0 + wn * 64 + j * 16 + nn);
+          }
+#pragma unroll
+          for (int c = 0; c < CH; ++c) {
+          const int i = i0 + c;
+          const int m = m0 + wm * WROWS + i * 16 + mm;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            float4 o = x[c][j];
+            o.x += acc[i][j][0] + bias[j].x;
+            o.y += acc[i][j][1] + bias[j].y;
+            o.z += acc[i][j][2] + bias[j].z;
+            o.w += acc[i][j][3] + bias[j].w;
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n0 + wn * 64 + j * 16 + nn) = o;
+          }
+          }
+        }
+        return;
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wm * WROWS + i * 16 + mm;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + wn * 64 + j * 16 + nn;
+          if (m < p.M && n < p.N) {
+            float4* c = reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n);
+            float4 o = *c;
+            o.x += acc[i][j][0] + bias[j].x;
+            o.y += acc[i][j][1] + bias[j].y;
+            o.z += acc[i][j][2] + bias[j].z;
+            o.w += acc[i][j][3] + bias[j].w;
+            *c = o;
+          }
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * WROWS + i * 16 + mm;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = n0 + wn * 64 + j * 16 + nn;
@@ -416,15 +491,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
           v[2] += bias.z;
           v[3] += bias.w;
         }
-        if constexpr (EPI == EPI_RESID_F32) {
-          float4* c = reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n);
-          float4 x = *c;
-          x.x += v[0];
-          x.y += v[1];
-          x.z += v[2];
-          x.w += v[3];
-          *c = x;
-        } else if constexpr (EPI == EPI_POS_F32) {
+        if constexpr (EPI == EPI_POS_F32) {
           const float4 ps = *reinterpret_cast<const float4*>(p.aux + (size_t)(m % p.aux_rows) * p.N + n);
           *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) =
               make_float4(v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w);
@@ -435,66 +502,101 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     }
   };
 
+  // >= this many VMEM ops of a full tile's epilogue are younger than the DMA of the stage a
+  // K-step waits for (bf16: 2 stores per fragment row; f32: 4 stores (+ loads) per row)
+  constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 2 * MI : 4 * MI;
   bool stores_pending = false;
+  int kt = 0, ct = 0, cm0 = 0, cn0 = 0;  // K-step within the current tile, tile index, its origin
+  auto tile_start = [&]() { tile_coords<BMT>(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0); };
+  tile_start();
+  auto end_step = [&]() {
+    if constexpr (SYNC2) {
+      // one wait + barrier per TWO K-steps (an effective BK = 64 step; needs NS = 5 and even
+      // nk): after odd step h, stages up to h+3 landed (the reads of steps h+1, h+2), stage h+4
+      // (issued in step h) in flight; slots refilled in steps h+1, h+2 were last read in h-1, h.
+      static_assert(!SYNC2 || NS == 5, "SYNC2 needs a 5-stage ring");
+      if (kt & 1) {
+        wait_vm<DMA_PER_STAGE * (NS - 4)>();
+        __builtin_amdgcn_s_barrier();
+      }
+      stores_pending = false;
+      if (++kt == nk) {
+        epilogue(ct);
+        kt = 0;
+        ++ct;
+        tile_start();
+      }
+      return;
+    }
+    if constexpr (!(ABL & 1) && !(ABL & 8)) {
+      // stage g+2 landed; g+3 .. g+NS-1 in flight.  Right after a full tile's epilogue its
+      // stores sit between those DMAs in the in-order vmcnt queue: let them drain behind
+      // this step instead of stalling the MFMAs on them.
+      if (stores_pending)
+        wait_vm<DMA_PER_STAGE * (NS - 3) + EPI_OPS>();
+      else
+        wait_vm<DMA_PER_STAGE * (NS - 3)>();
+    }
+    stores_pending = false;
+    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();
+    if (++kt == nk) {
+      epilogue(ct);
+      stores_pending = (cm0 + BMT <= p.M) && (cn0 + B2N <= p.N);
+      kt = 0;
+      ++ct;
+      tile_start();
+    }
+  };
   // SCHED: one basic block per K-step body with the DMAs and fragment reads spread between the
   // MFMAs (sched_group_barrier), instead of DMA issue right after the barrier.
   auto kstep_sched = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
     const char* An = stage_ptr(g + 1);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI / 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
     issue_a();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bn[j] = frag256(An + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
+    for (int j = 0; j < 4; ++j) bn[j] = frag256(An + A_BYTES, wn * 64 + j * 16 + frow, fk);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
-    __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
-    __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+    for (int i = 0; i < MI / 2; ++i) a[i] = frag256(An, wm * WROWS + i * 16 + frow, fk);
+    // first half: 4 MI MFMAs, NA DMAs, 4 + MI/2 fragment reads
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
+    for (int t = 0; t < NA; ++t) {
+      __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < 4 + MI / 2; ++t) {
       __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+    if constexpr (2 * MI - 2 * NA - 4 - MI / 2 > 0)
+      __builtin_amdgcn_sched_group_barrier(0x8, 2 * MI - 2 * NA - 4 - MI / 2, 0);
 #pragma unroll
-    for (int i = 4; i < 8; ++i)
+    for (int i = MI / 2; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
     issue_w();
 #pragma unroll
-    for (int i = 4; i < 8; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+    for (int i = MI / 2; i < MI; ++i) a[i] = frag256(An, wm * WROWS + i * 16 + frow, fk);
+    // second half: 2 MI MFMAs, 2 DMAs, MI/2 fragment reads
     __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
     __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
     __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < MI / 2; ++t) {
       __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (MI - 4 > 0) __builtin_amdgcn_sched_group_barrier(0x8, MI - 4, 0);
+    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
     advance();
-    constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
-    if (stores_pending)
-      wait_vm<4 * (NS - 3) + EPI_OPS>();
-    else
-      wait_vm<4 * (NS - 3)>();
-    stores_pending = false;
-    __builtin_amdgcn_s_barrier();
-    const int ti = g / nk;
-    if (g - ti * nk == nk - 1) {
-      epilogue(ti);
-      int m0, n0;
-      tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
-      stores_pending = (m0 + B2M <= p.M) && (n0 + B2N <= p.N);
-    }
+    end_step();
   };
   auto kstep = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
     if constexpr (SCHED) {
@@ -505,16 +607,16 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     if constexpr (!(ABL & 1)) issue_a();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI / 2; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     if constexpr (!(ABL & 4)) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+      for (int i = 0; i < MI / 2; ++i) a[i] = frag256(An, wm * WROWS + i * 16 + frow, fk);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bn[j] = frag256(An + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
+      for (int j = 0; j < 4; ++j) bn[j] = frag256(An + A_BYTES, wn * 64 + j * 16 + frow, fk);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) bn[j] = bc[j];
@@ -522,36 +624,22 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     if constexpr (!(ABL & 1)) issue_w_and_advance();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 4; i < 8; ++i)
+    for (int i = MI / 2; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     if constexpr (!(ABL & 4)) {
 #pragma unroll
-      for (int i = 4; i < 8; ++i) a[i] = frag256(An, wm * 128 + i * 16 + frow, fk);
+      for (int i = MI / 2; i < MI; ++i) a[i] = frag256(An, wm * WROWS + i * 16 + frow, fk);
     }
-    // stage g+2 landed; g+3 .. g+NS-1 in flight.  Right after a full tile's epilogue its
-    // 32 stores per wave sit between those DMAs in the in-order vmcnt queue: let them
-    // drain behind this step instead of stalling the MFMAs on them.
-    if constexpr (!(ABL & 1) && !(ABL & 8)) {
-      // >= this many VMEM ops of a full tile's epilogue are younger than stage g+2's DMA
-      constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
-      if (stores_pending)
-        wait_vm<4 * (NS - 3) + EPI_OPS>();
-      else
-        wait_vm<4 * (NS - 3)>();
-    }
-    stores_pending = false;
-    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();
-    const int ti = g / nk;
-    if (g - ti * nk == nk - 1) {
-      epilogue(ti);
-      int m0, n0;
-      tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
-      stores_pending = (m0 + B2M <= p.M) && (n0 + B2N <= p.N);
-    }
+    end_step();
   };
+  // PRIO 1: static priority for the second-dispatched half (waves 4-7 lose VALU/issue
+  // arbitration to the older half on every segment); PRIO 0: flips around each MFMA cluster
+  if constexpr (PRIO == 1) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   int g = 0;
   for (; g + 1 < total; g += 2) {
     kstep(g, b0, b1);
@@ -843,18 +931,21 @@ int g_gemm_ablate = 0;  // timing ablation knob (MQ_TUNE_GEMM_ABLATE)
 int g_gemm_bufload = 1; // MQ_TUNE_GEMM_BUFLOAD: stage with buffer_load ... lds (default: +3-11 % over glds)
 int g_gemm_sched = 1;   // MQ_TUNE_GEMM_SCHED: K-step with DMAs/reads interleaved between MFMAs (default: +1-3 %)
 int g_gemm_mfma32 = 0;  // MQ_TUNE_GEMM_MFMA32: 32x32x16 MFMA variant of the 256x256 kernel
+int g_gemm_sync2 = 0;   // MQ_TUNE_GEMM_SYNC2: with 5 stages, one wait + barrier per two K-steps
+int g_gemm_prio = 0;    // MQ_TUNE_GEMM_PRIO: 0 setprio flips per MFMA cluster, 1 static priority for waves 4-7, 2 none
+int g_gemm_bm128 = 0;   // MQ_TUNE_GEMM_BM128: 128x256 tiles for grids of at most one 256x256 tile per CU (measured slower: 16 MFMAs per wave per K-step do not cover the step overheads)
 
-template <int EPI, int NS, int ABL, bool BUF = false, bool SCHED = false>
+template <int EPI, int NS, int ABL, bool BUF = false, bool SCHED = false, int MI = 8, int PRIO = 0, bool SYNC2 = false>
 static void launch256(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
-  const int lds = NS * B2_STAGE_BYTES;
+  const int lds = NS * (32 * MI * B2K * 2 + B2_OP_BYTES);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS, ABL, BUF, SCHED>,
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS, ABL, BUF, SCHED, MI, PRIO, SYNC2>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<EPI, NS, ABL, BUF, SCHED>), grid, dim3(B2T), lds, stream, p, tiles_m,
-                     tiles_n);
+  hipLaunchKernelGGL((gemm256_kernel<EPI, NS, ABL, BUF, SCHED, MI, PRIO, SYNC2>), grid, dim3(B2T), lds, stream, p,
+                     tiles_m, tiles_n);
 }
 
 template <int EPI, int NS, bool BUF>
@@ -890,7 +981,16 @@ static void launch256s(dim3 grid, hipStream_t stream, const GemmArgs& p, int til
     }
   }
   if (g_gemm_sched) {
-    launch256<EPI, 4, 0, true, true>(grid, stream, p, tiles_m, tiles_n);
+    if (g_gemm_stages == 5 && g_gemm_sync2 && (p.K / B2K) % 2 == 0)
+      launch256<EPI, 5, 0, true, true, 8, 0, true>(grid, stream, p, tiles_m, tiles_n);
+    else if (g_gemm_stages == 5)
+      launch256<EPI, 5, 0, true, true>(grid, stream, p, tiles_m, tiles_n);
+    else if (g_gemm_prio == 1)
+      launch256<EPI, 4, 0, true, true, 8, 1>(grid, stream, p, tiles_m, tiles_n);
+    else if (g_gemm_prio == 2)
+      launch256<EPI, 4, 0, true, true, 8, 2>(grid, stream, p, tiles_m, tiles_n);
+    else
+      launch256<EPI, 4, 0, true, true>(grid, stream, p, tiles_m, tiles_n);
     return;
   }
   if (g_gemm_bufload) {
@@ -906,6 +1006,19 @@ static void launch256s(dim3 grid, hipStream_t stream, const GemmArgs& p, int til
     launch256<EPI, 4, 0>(grid, stream, p, tiles_m, tiles_n);
 }
 
+// 128x256 tiles: grid = tiles / rounds so every block walks the same number of tiles
+template <int EPI>
+static void launch128(hipStream_t stream, const GemmArgs& p) {
+  const int tiles_m = (p.M + 127) / 128, tiles_n = (p.N + B2N - 1) / B2N;
+  const int tiles = tiles_m * tiles_n;
+  const int rounds = (tiles + g_num_cus - 1) / g_num_cus;
+  dim3 grid((tiles + rounds - 1) / rounds);
+  if (g_gemm_sched)
+    launch256<EPI, 4, 0, true, true, 4>(grid, stream, p, tiles_m, tiles_n);
+  else
+    launch256<EPI, 4, 0, true, false, 4>(grid, stream, p, tiles_m, tiles_n);
+}
+
 static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
   if (!g_num_cus) {
     int dev = 0;
@@ -915,6 +1028,19 @@ static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
   }
   const int tiles_m = (p.M + B2M - 1) / B2M, tiles_n = (p.N + B2N - 1) / B2N;
   const int tiles = tiles_m * tiles_n;
+  // narrow grids (at most one 256x256 tile per CU, e.g. N = 1280): 128-row tiles, two or more
+  // per CU, so epilogues overlap the next tile's K-loop
+  if (g_gemm_bm128 && tiles <= g_num_cus && !g_gemm_mfma32 && !g_gemm_ablate) {
+    switch (epi) {
+      case EPI_BF16: launch128<EPI_BF16>(stream, p); break;
+      case EPI_GELU_BF16: launch128<EPI_GELU_BF16>(stream, p); break;
+      case EPI_RESID_F32: launch128<EPI_RESID_F32>(stream, p); break;
+      case EPI_POS_F32: launch128<EPI_POS_F32>(stream, p); break;
+      case EPI_F32: launch128<EPI_F32>(stream, p); break;
+      default: return -3;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -4;
+  }
   dim3 grid(tiles < g_num_cus ? tiles : g_num_cus);
   switch (epi) {
     case EPI_BF16: launch256s<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;

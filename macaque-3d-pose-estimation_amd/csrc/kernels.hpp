@@ -31,6 +31,9 @@ extern int g_gemm_ablate;
 extern int g_gemm_bufload;
 extern int g_gemm_mfma32;
 extern int g_gemm_sched;
+extern int g_gemm_bm128;
+extern int g_gemm_prio;
+extern int g_gemm_sync2;
 extern bool g_gemm_force_small;
 
 // ViT ops (vit_ops.hip)

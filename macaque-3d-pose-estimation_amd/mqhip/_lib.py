@@ -105,6 +105,17 @@ def stream_ptr(device=None):
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+def apply_tuning_env(lib) -> None:
+    """MQ_TUNING="key=value,key=value" (include/mq_hip.h MQ_TUNE_* keys): kernel-variant knobs for
+    A/B runs of the unchanged bench / tests; unset means the library defaults."""
+    spec = os.environ.get("MQ_TUNING", "").strip()
+    if not spec:
+        return
+    for item in spec.split(","):
+        k, v = item.split("=")
+        check(lib.mq_set_tuning(int(k), int(v)), f"mq_set_tuning({k}, {v})")
+
+
 class Context:
     """One mq_ctx per device (threading)."""
 
@@ -119,6 +130,7 @@ class Context:
         h = C.c_void_p()
         check(self.lib.mq_create(device, C.byref(h)), "mq_create")
         self.handle = h
+        apply_tuning_env(self.lib)
 
     @classmethod
     def get(cls, device: int = 0) -> "Context":

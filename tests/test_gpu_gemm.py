@@ -50,14 +50,19 @@ def _run(M, N, K, epi, aux_rows=0, seed=0):
     return err, scale
 
 
-@pytest.fixture(params=[(0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 0, 1)],
-                ids=["glds", "bufload", "mfma32", "bufload-mfma32", "sched"])
+@pytest.fixture(params=[(0, 0, 0, 0, 4, 0), (1, 0, 0, 0, 4, 0), (0, 1, 0, 0, 4, 0), (1, 1, 0, 0, 4, 0),
+                        (1, 0, 1, 0, 4, 0), (1, 0, 0, 1, 4, 0), (1, 0, 1, 1, 4, 0), (1, 0, 1, 0, 5, 0),
+                        (1, 0, 1, 0, 5, 1)],
+                ids=["glds", "bufload", "mfma32", "bufload-mfma32", "sched", "bufload-bm128", "sched-bm128",
+                     "sched-5stage", "sched-5stage-sync2"])
 def staging(request):
-    """Every variant of the 256x256 kernel: LDS-DMA staging form (MQ_TUNE_GEMM_BUFLOAD) x
-    MFMA shape (MQ_TUNE_GEMM_MFMA32: 32x32x16 vs 16x16x32) x interleaved K-step (MQ_TUNE_GEMM_SCHED)."""
+    """Every variant of the persistent kernel: LDS-DMA staging form (MQ_TUNE_GEMM_BUFLOAD) x
+    MFMA shape (MQ_TUNE_GEMM_MFMA32: 32x32x16 vs 16x16x32) x interleaved K-step (MQ_TUNE_GEMM_SCHED)
+    x 128-row tiles for narrow grids (MQ_TUNE_GEMM_BM128) x ring depth (MQ_TUNE_GEMM_STAGES) x one
+    barrier per two K-steps (MQ_TUNE_GEMM_SYNC2)."""
     from mqhip import _lib
     ctx = _lib.Context.get(0)
-    keys = (5, 6, 7)
+    keys = (5, 6, 7, 9, 1, 11)
     old = [ctx.lib.mq_get_tuning(k) for k in keys]
     for k, v in zip(keys, request.param):
         assert ctx.lib.mq_set_tuning(k, v) == 0
@@ -73,10 +78,20 @@ def test_gemm_256_path_all_epilogues(epi, staging):
     assert err <= tol, (err, tol)
 
 
-@pytest.mark.parametrize("M,N,K", [(12288, 1280, 1280), (1024, 3840, 1280), (512, 5120, 256)])
+@pytest.mark.parametrize("M,N,K", [(12288, 1280, 1280), (1024, 3840, 1280), (512, 5120, 256), (4196, 5120, 256)])
 def test_gemm_vit_shapes(M, N, K, staging):
     err, scale = _run(M, N, K, 4)
     assert err <= 2e-3 * scale
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M,N", [(12288, 1280), (1000, 1280), (4196, 5120)])
+def test_gemm_tile_rows_default_policy(epi, M, N):
+    """Default policy (256x256 tiles, interleaved K-step) on narrow (one tile per CU) and wide
+    grids: every epilogue, ragged M, residual read-modify-write."""
+    err, scale = _run(M, N, 256, epi, aux_rows=192)
+    tol = 2e-3 * scale + (0.01 * scale if epi in (0, 1) else 0.0)
+    assert err <= tol, (err, tol)
 
 
 def test_gemm_small_path_nchw():

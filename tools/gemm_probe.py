@@ -10,6 +10,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "macaque-3d-pose-estimation_amd"))
 
+COLD = False
 SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
     "qkv": (12288, 3840, 1280, 0),
     "proj": (12288, 1280, 1280, 2),
@@ -30,7 +31,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shape", default="all")
     ap.add_argument("--variants", default="4,5,small", help="GEMM variants to A/B in this process")
+    ap.add_argument("--cold", action="store_true",
+                    help="evict L2/Infinity Cache (384 MB write) before every launch; time each launch alone")
     args = ap.parse_args()
+    global COLD
+    COLD = args.cold
     import torch
     from mqhip import _lib
     ctx = _lib.Context.get(0)
@@ -42,10 +47,24 @@ def main():
         ctx.lib.mq_set_tuning(3, 0)
         ctx.lib.mq_set_tuning(5, 0)
         ctx.lib.mq_set_tuning(6, 0)
-        ctx.lib.mq_set_tuning(7, 0)
+        ctx.lib.mq_set_tuning(7, 1)
+        ctx.lib.mq_set_tuning(9, 0)
         var_st = var
-        if var == "sch":
-            ctx.lib.mq_set_tuning(7, 1)
+        ctx.lib.mq_set_tuning(10, 0)
+        if var in ("p1", "p2"):  # static young-half priority / no priority
+            ctx.lib.mq_set_tuning(10, int(var[1]))
+            var_st = "4"
+        ctx.lib.mq_set_tuning(11, 0)
+        if var == "s5":  # 5-stage ring on the interleaved K-step
+            var_st = "5"
+        if var == "y2":  # 5 stages, one wait + barrier per two K-steps
+            ctx.lib.mq_set_tuning(11, 1)
+            var_st = "5"
+        if var == "b128":  # 128-row tiles for narrow grids
+            ctx.lib.mq_set_tuning(9, 1)
+            var_st = "4"
+        if var == "nosch":
+            ctx.lib.mq_set_tuning(7, 0)
             var_st = "4"
         if var in ("m32", "bm32"):
             ctx.lib.mq_set_tuning(6, 1)
@@ -108,13 +127,24 @@ def bench_one(ctx, _lib, torch, name, iters):
         for _ in range(3):
             run()
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(iters):
-            run()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / iters
+        if COLD:
+            flush = torch.empty((384 << 20) // 4, device="cuda")
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+            for a, b in ev:
+                flush.fill_(1.0)
+                a.record()
+                run()
+                b.record()
+            torch.cuda.synchronize()
+            ms = sum(a.elapsed_time(b) for a, b in ev) / iters
+        else:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(iters):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / iters
         tf = 2 * M * N * K / (ms * 1e-3) / 1e12
         return {"M": M, "N": N, "K": K, "ms": round(ms, 4), "tflops": round(tf, 1)}
 

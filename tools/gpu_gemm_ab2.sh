@@ -1,0 +1,18 @@
+# GEMM numerics tests + warm and cold GEMM probe A/B of the variants in $2.  First failure ends the call.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=${1:-ab}
+VARS=${2:-4,p1}
+SHAPES=${3:-qkv,proj,fc1,fc2,dc1,dc2}
+mkdir -p gpurun_out/$OUT
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_gemm.py -x -q --timeout 200 --timeout-method thread > gpurun_out/$OUT/pytest_gemm.log 2>&1 || { echo GEMM TESTS FAILED; tail -30 gpurun_out/$OUT/pytest_gemm.log; exit 1; }
+tail -1 gpurun_out/$OUT/pytest_gemm.log
+timeout -k 10 300 python3 tools/gemm_probe.py --iters 20 --shape $SHAPES --variants $VARS > gpurun_out/$OUT/gemm_probe.log 2>&1 || { echo PROBE FAILED; tail -20 gpurun_out/$OUT/gemm_probe.log; exit 1; }
+grep " r=1" gpurun_out/$OUT/gemm_probe.log
+timeout -k 10 300 python3 tools/gemm_probe.py --cold --iters 20 --shape $SHAPES --variants $VARS > gpurun_out/$OUT/gemm_probe_cold.log 2>&1 || { echo PROBE FAILED; tail -20 gpurun_out/$OUT/gemm_probe_cold.log; exit 1; }
+echo COLD; grep " r=1" gpurun_out/$OUT/gemm_probe_cold.log
+if [ -n "$4" ]; then
+timeout -k 10 300 python3 bench.py --no-cpu-baseline > gpurun_out/$OUT/bench.json 2> gpurun_out/$OUT/bench.err || { echo BENCH FAILED; tail -20 gpurun_out/$OUT/bench.err; exit 1; }
+python3 -c "import json;d=json.load(open('gpurun_out/$OUT/bench.json'));print('BENCH', d['value'], d['ms_per_step'], d['roofline']['achieved'])"
+fi
