@@ -47,7 +47,9 @@ const char* mq_last_error(void);
 #define MQ_TUNE_GEMM_BM128 9        /* 1: 128x256 tiles when the 256x256 grid has at most one tile per CU (default 0) */
 #define MQ_TUNE_GEMM_PRIO 10        /* MFMA priority: 0 (default) s_setprio flips per MFMA cluster, 1 static priority for waves 4-7, 2 none */
 #define MQ_TUNE_GEMM_SYNC2 11       /* 1: with MQ_TUNE_GEMM_STAGES 5, one vmcnt wait + barrier per two K-steps (default 0) */
-#define MQ_TUNE_OPTIM_PCG_ITERS 4   /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
+#define MQ_TUNE_GEMM_PINGPONG 12    /* 1 (default): 256x256 GEMMs with K % 64 == 0 on the ping-pong kernel (wave groups alternate
+                                       LDS traffic and MFMA, gemm_pp.hip); 0: the interleaved-K-step kernel */
+#define MQ_TUNE_OPTIM_PCG_ITERS 4  /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

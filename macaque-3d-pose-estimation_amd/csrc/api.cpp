@@ -159,6 +159,9 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_GEMM_SCHED:
       mq::g_gemm_sched = value != 0;
       return 0;
+    case MQ_TUNE_GEMM_PINGPONG:
+      mq::g_gemm_pingpong = value != 0;
+      return 0;
     case MQ_TUNE_ATTENTION_ABLATE:
       if (value < 0 || value > 3) return fail("mq_set_tuning: attention ablation must be 0..3", -2);
       mq::g_attention_ablate = value;
@@ -184,6 +187,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_GEMM_BM128: return mq::g_gemm_bm128;
     case MQ_TUNE_GEMM_PRIO: return mq::g_gemm_prio;
     case MQ_TUNE_GEMM_SYNC2: return mq::g_gemm_sync2;
+    case MQ_TUNE_GEMM_PINGPONG: return mq::g_gemm_pingpong;
     case MQ_TUNE_ATTENTION_ABLATE: return mq::g_attention_ablate;
     default: return fail("mq_get_tuning: unknown key", -2);
   }

@@ -170,8 +170,10 @@ __global__ void project_kernel(const double* __restrict__ cams, int C, const dou
 }
 
 // CameraGroup.triangulate (cameras.py:593-637): optional undistort, >= 2 views.
+// 64-thread launches: the bound lifts the default 1024-thread VGPR cap, under which the 2C x 4
+// f64 DLT matrix of the Jacobi SVD spilled to scratch (115 us for one frame's 68 points).
 template <int MAXC>
-__global__ void triangulate_kernel(const double* __restrict__ cams, int C, const double* __restrict__ pts, int N,
+__global__ __launch_bounds__(64) void triangulate_kernel(const double* __restrict__ cams, int C, const double* __restrict__ pts, int N,
                                    int undistort, double* __restrict__ out) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;

@@ -35,6 +35,10 @@ extern int g_gemm_bm128;
 extern int g_gemm_prio;
 extern int g_gemm_sync2;
 extern bool g_gemm_force_small;
+// ping-pong 256x256 kernel (gemm_pp.hip): the two wave groups of a block alternate LDS traffic and MFMA
+extern int g_gemm_pingpong;
+bool gemm_pingpong_fits(const GemmArgs& p, int epi);
+int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,

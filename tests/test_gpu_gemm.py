@@ -50,19 +50,19 @@ def _run(M, N, K, epi, aux_rows=0, seed=0):
     return err, scale
 
 
-@pytest.fixture(params=[(0, 0, 0, 0, 4, 0), (1, 0, 0, 0, 4, 0), (0, 1, 0, 0, 4, 0), (1, 1, 0, 0, 4, 0),
-                        (1, 0, 1, 0, 4, 0), (1, 0, 0, 1, 4, 0), (1, 0, 1, 1, 4, 0), (1, 0, 1, 0, 5, 0),
-                        (1, 0, 1, 0, 5, 1)],
+@pytest.fixture(params=[(0, 0, 0, 0, 4, 0, 0), (1, 0, 0, 0, 4, 0, 0), (0, 1, 0, 0, 4, 0, 0), (1, 1, 0, 0, 4, 0, 0),
+                        (1, 0, 1, 0, 4, 0, 0), (1, 0, 0, 1, 4, 0, 0), (1, 0, 1, 1, 4, 0, 0), (1, 0, 1, 0, 5, 0, 0),
+                        (1, 0, 1, 0, 5, 1, 0), (1, 0, 1, 0, 4, 0, 1)],
                 ids=["glds", "bufload", "mfma32", "bufload-mfma32", "sched", "bufload-bm128", "sched-bm128",
-                     "sched-5stage", "sched-5stage-sync2"])
+                     "sched-5stage", "sched-5stage-sync2", "pingpong"])
 def staging(request):
     """Every variant of the persistent kernel: LDS-DMA staging form (MQ_TUNE_GEMM_BUFLOAD) x
     MFMA shape (MQ_TUNE_GEMM_MFMA32: 32x32x16 vs 16x16x32) x interleaved K-step (MQ_TUNE_GEMM_SCHED)
     x 128-row tiles for narrow grids (MQ_TUNE_GEMM_BM128) x ring depth (MQ_TUNE_GEMM_STAGES) x one
-    barrier per two K-steps (MQ_TUNE_GEMM_SYNC2)."""
+    barrier per two K-steps (MQ_TUNE_GEMM_SYNC2) x the ping-pong kernel (MQ_TUNE_GEMM_PINGPONG)."""
     from mqhip import _lib
     ctx = _lib.Context.get(0)
-    keys = (5, 6, 7, 9, 1, 11)
+    keys = (5, 6, 7, 9, 1, 11, 12)
     old = [ctx.lib.mq_get_tuning(k) for k in keys]
     for k, v in zip(keys, request.param):
         assert ctx.lib.mq_set_tuning(k, v) == 0
@@ -92,6 +92,49 @@ def test_gemm_tile_rows_default_policy(epi, M, N):
     err, scale = _run(M, N, 256, epi, aux_rows=192)
     tol = 2e-3 * scale + (0.01 * scale if epi in (0, 1) else 0.0)
     assert err <= tol, (err, tol)
+
+
+def _run_pair(M, N, K, epi, aux_rows, seed=0):
+    """The same GEMM through the interleaved-K-step kernel and the ping-pong kernel."""
+    import torch
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    A = torch.randn((M, K), generator=g, device="cuda").to(torch.bfloat16)
+    W = (torch.randn((N, K), generator=g, device="cuda") * 0.05).to(torch.bfloat16)
+    bias = torch.randn((N,), generator=g, device="cuda")
+    aux = torch.randn((aux_rows, N), generator=g, device="cuda")
+    C0 = torch.randn((M, N), generator=g, device="cuda")
+    if epi in (0, 1):
+        C0 = C0.to(torch.bfloat16)
+    outs = []
+    old = ctx.lib.mq_get_tuning(12)
+    try:
+        for pp in (0, 1):
+            assert ctx.lib.mq_set_tuning(12, pp) == 0
+            Cm = C0.clone()
+            _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), _lib.ptr(bias),
+                                            _lib.ptr(aux), M, N, K, K, K, N, aux_rows, epi, _lib.stream_ptr()),
+                       "mq_gemm_bf16")
+            outs.append(Cm)
+    finally:
+        ctx.lib.mq_set_tuning(12, old)
+    torch.cuda.synchronize()
+    return outs
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(12288, 1280, 1280), (700, 512, 320), (4196, 5120, 256), (2048, 3840, 1280),
+                                   (1000, 1280, 2048), (3000, 1280, 5120)])
+def test_gemm_pingpong_bitwise_equals_interleaved(epi, M, N, K):
+    """Both kernels accumulate every output in the same order (32-deep MFMA steps in ascending K,
+    then bias, then the epilogue op), so the ping-pong kernel must reproduce the other bit for bit,
+    on full and ragged tiles and multi-tile persistent walks."""
+    import torch
+    a, b = _run_pair(M, N, K, epi, aux_rows=192)
+    assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                       b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
 
 
 def test_gemm_small_path_nchw():

@@ -55,6 +55,10 @@ def main():
             ctx.lib.mq_set_tuning(10, int(var[1]))
             var_st = "4"
         ctx.lib.mq_set_tuning(11, 0)
+        ctx.lib.mq_set_tuning(12, 0)
+        if var == "pp":  # ping-pong kernel (gemm_pp.hip)
+            ctx.lib.mq_set_tuning(12, 1)
+            var_st = "4"
         if var == "s5":  # 5-stage ring on the interleaved K-step
             var_st = "5"
         if var == "y2":  # 5 stages, one wait + barrier per two K-steps
