@@ -49,6 +49,9 @@ const char* mq_last_error(void);
 #define MQ_TUNE_GEMM_SYNC2 11       /* 1: with MQ_TUNE_GEMM_STAGES 5, one vmcnt wait + barrier per two K-steps (default 0) */
 #define MQ_TUNE_GEMM_PINGPONG 12    /* 1 (default): 256x256 GEMMs with K % 64 == 0 on the ping-pong kernel (wave groups alternate
                                        LDS traffic and MFMA, gemm_pp.hip); 0: the interleaved-K-step kernel */
+#define MQ_TUNE_GEMM_PP_ABLATE 13   /* ping-pong GEMM timing ablations, bf16 epilogue only (WRONG results): 1 no vmcnt
+                                       waits, 2 no steady-state DMA, 3 both, 4 no fragment re-reads, 8 no barriers,
+                                       15 all */
 #define MQ_TUNE_OPTIM_PCG_ITERS 4  /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */

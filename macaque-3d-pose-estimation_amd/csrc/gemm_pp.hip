@@ -40,6 +40,7 @@
 namespace mq {
 
 int g_gemm_pingpong = 1;
+int g_gemm_pp_ablate = 0;
 
 namespace {
 
@@ -53,6 +54,12 @@ __device__ __forceinline__ int pp_swz(int row) { return (row >> 1) & 7; }
 
 __device__ __forceinline__ bf16x8 pp_frag(const char* op, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(op + row * 128 + ((chunk ^ pp_swz(row)) << 4));
+}
+
+template <int N_IN_FLIGHT, int ABL = 0>
+__device__ __forceinline__ void pp_wait_vm_loop() {
+  if constexpr ((ABL & 1) == 0)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_IN_FLIGHT) : "memory");
 }
 
 template <int N_IN_FLIGHT>
@@ -213,7 +220,10 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
   }
 }
 
-template <int EPI>
+// ABL (timing ablations, WRONG results when non-zero; EPI_BF16 only): bit0 no vmcnt waits in the
+// K-loop, bit1 no steady-state DMA, bit2 no fragment re-reads after the first K-step, bit3 no barriers
+// in the K-loop.
+template <int EPI, int ABL = 0>
 __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -245,6 +255,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, p.bias ? p.N * 4 : 0, 0x00020000);
 
+  bool g_abl_started = false;  // ablation builds: the prologue DMA has landed
   // DMA issue cursor: (tile, k) of the next stage to load and this lane's source offsets for
   // that tile.  Past the end it stays on the last stage (re-loaded into the idle buffer), which
   // keeps every wait count uniform.
@@ -265,6 +276,9 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   };
   set_tile_ptrs(0);
   auto issue = [&](int i, int slot) {
+    if constexpr ((ABL & 2) != 0) {
+      if (g_abl_started) return;
+    }
     char* dst = smem + slot * PP_STAGE + (pp_slot_is_w(i) ? PP_OP : 0) + pp_group_row(wave, i) * 128;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(pp_slot_is_w(i) ? rsW : rsA, MQ_LDS_LOCAL(dst), 16, voff[i],
                                              iss_k * PP_BK * 2, 0, 0);
@@ -305,8 +319,11 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     __builtin_amdgcn_s_setprio(0);
   };
   // barrier that opens an MFMA segment: the segment's fragment reads are complete
+  auto bar = [&]() {
+    if constexpr ((ABL & 8) == 0) pp_barrier();
+  };
   auto open_mfma = [&]() {
-    pp_barrier();
+    bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
@@ -315,6 +332,10 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   for (int i = 0; i < 8; ++i) issue(i, 0);
   advance();
   pp_wait_vm<4>();
+  if constexpr (ABL != 0) {
+    pp_wait_vm<0>();
+    g_abl_started = true;
+  }
   pp_barrier();
   if (wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
 
@@ -329,53 +350,58 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b0[j][kk] = pp_frag(Ws, wn * 64 + j * 16 + frow, kk * 4 + fk);
+      for (int j = 0; j < 2; ++j)
+        if (!(ABL & 4) || g == 0) b0[j][kk] = pp_frag(Ws, wn * 64 + j * 16 + frow, kk * 4 + fk);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, wm * 128 + i * 16 + frow, kk * 4 + fk);
+      for (int i = 0; i < 4; ++i)
+        if (!(ABL & 4) || g == 0) a[i][kk] = pp_frag(As, wm * 128 + i * 16 + frow, kk * 4 + fk);
     }
     issue(0, slot ^ 1);
     issue(1, slot ^ 1);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
+    if constexpr ((ABL & 2) == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
     if (stores_pending)
-      pp_wait_vm<5 + EPI_OPS>();
+      pp_wait_vm_loop<5 + EPI_OPS, ABL>();
     else
-      pp_wait_vm<5>();
+      pp_wait_vm_loop<5, ABL>();
     open_mfma();
     mfma_quadrant(0, 0, b0);
-    pp_barrier();
+    bar();
     // ---- phase 1: quadrant (0,1)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b1[j][kk] = pp_frag(Ws, wn * 64 + 32 + j * 16 + frow, kk * 4 + fk);
+      for (int j = 0; j < 2; ++j)
+        if (!(ABL & 4) || g == 0) b1[j][kk] = pp_frag(Ws, wn * 64 + 32 + j * 16 + frow, kk * 4 + fk);
     issue(2, slot ^ 1);
     issue(3, slot ^ 1);
     if (stores_pending)
-      pp_wait_vm<5 + EPI_OPS>();
+      pp_wait_vm_loop<5 + EPI_OPS, ABL>();
     else
-      pp_wait_vm<5>();
+      pp_wait_vm_loop<5, ABL>();
     stores_pending = false;
     open_mfma();
     mfma_quadrant(0, 1, b1);
-    pp_barrier();
+    bar();
     // ---- phase 2: quadrant (1,0)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
+      for (int i = 0; i < 4; ++i)
+        if (!(ABL & 4) || g == 0) a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
     issue(4, slot ^ 1);
     issue(5, slot ^ 1);
     open_mfma();
     mfma_quadrant(1, 0, b0);
-    pp_barrier();
+    bar();
     // ---- phase 3: quadrant (1,1)
     issue(6, slot ^ 1);
     issue(7, slot ^ 1);
     advance();
-    pp_wait_vm<4>();
+    pp_wait_vm_loop<4, ABL>();
     open_mfma();
     mfma_quadrant(1, 1, b1);
-    pp_barrier();
+    bar();
     if (++kt == nk) {
       pp_epilogue<EPI>(p, acc, reinterpret_cast<const float*>(bias_lds), cm0, cn0, wm, wn, lane);
       stores_pending = (cm0 + PP_BM <= p.M) && (cn0 + PP_BN <= p.N);
@@ -391,14 +417,15 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-template <int EPI>
+template <int EPI, int ABL = 0>
 void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              PP_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL(gemm_pp_kernel<EPI>, grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
 }
 
 }  // namespace
@@ -417,6 +444,18 @@ int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
   const int tiles_m = (p.M + PP_BM - 1) / PP_BM, tiles_n = (p.N + PP_BN - 1) / PP_BN;
   const int tiles = tiles_m * tiles_n;
   dim3 grid(tiles < num_cus ? tiles : num_cus);
+  if (g_gemm_pp_ablate && epi == EPI_BF16) {
+    switch (g_gemm_pp_ablate) {
+      case 1: launch_pp<EPI_BF16, 1>(grid, stream, p, tiles_m, tiles_n); break;
+      case 2: launch_pp<EPI_BF16, 2>(grid, stream, p, tiles_m, tiles_n); break;
+      case 3: launch_pp<EPI_BF16, 3>(grid, stream, p, tiles_m, tiles_n); break;
+      case 4: launch_pp<EPI_BF16, 4>(grid, stream, p, tiles_m, tiles_n); break;
+      case 8: launch_pp<EPI_BF16, 8>(grid, stream, p, tiles_m, tiles_n); break;
+      case 15: launch_pp<EPI_BF16, 15>(grid, stream, p, tiles_m, tiles_n); break;
+      default: return -3;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -4;
+  }
   switch (epi) {
     case EPI_BF16: launch_pp<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;

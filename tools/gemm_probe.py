@@ -56,6 +56,11 @@ def main():
             var_st = "4"
         ctx.lib.mq_set_tuning(11, 0)
         ctx.lib.mq_set_tuning(12, 0)
+        ctx.lib.mq_set_tuning(13, 0)
+        if var.startswith("pa"):  # ping-pong timing ablations (bf16 epilogue shapes only; wrong results)
+            ctx.lib.mq_set_tuning(12, 1)
+            ctx.lib.mq_set_tuning(13, int(var[2:]))
+            var_st = "4"
         if var == "pp":  # ping-pong kernel (gemm_pp.hip)
             ctx.lib.mq_set_tuning(12, 1)
             var_st = "4"
