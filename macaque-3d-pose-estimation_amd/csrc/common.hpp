@@ -32,6 +32,29 @@ __device__ __forceinline__ unsigned pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(unsigned, v);
 }
 
+// Exact-erf GELU on two values at once, erfc by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7,
+// far below the bf16 rounding of the GEMM output):
+//   0.5 x (1 + erf(x / sqrt2)) = max(x, 0) - h,   h = 0.5 |x| erfc(|x| / sqrt2) = |x| P(t) exp(-x^2 / 2)
+// with t = 1 / (1 + p |x| / sqrt2) and P = 0.5 * (A&S polynomial in t).  Written on float pairs so the
+// polynomial, products and the difference are packed v_pk_*_f32 ops; per pair two v_rcp_f32 and two
+// v_exp_f32 (exp2 with the log2(e) factor folded into the constant).  ~8.5 VALU ops per value.
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 ax = __builtin_elementwise_abs(x);
+  const f32x2 den = ax * (f32x2){0.23164190f, 0.23164190f} + (f32x2){1.f, 1.f};  // 1 + p |x| / sqrt2
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 poly = t * 0.5307027145f + -0.7265760135f;  // 0.5 * A&S a5, a4
+  poly = poly * t + 0.7107068705f;
+  poly = poly * t + -0.142248368f;
+  poly = poly * t + 0.127414796f;
+  poly = poly * t;
+  const f32x2 u = (x * x) * -0.72134752044448170368f;  // -x^2 / 2 * log2(e)
+  const f32x2 e = {__builtin_amdgcn_exp2f(u.x), __builtin_amdgcn_exp2f(u.y)};
+  const f32x2 h = (ax * poly) * e;
+  const f32x2 pos = {fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)};
+  return pos - h;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -30,23 +30,6 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
-// Exact-erf GELU with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, far below
-// the bf16 rounding of the output): one v_rcp, one v_exp and a degree-5 Horner chain
-// instead of the library erff (the GELU epilogue was 20 % of the fc1 GEMM).
-__device__ __forceinline__ float gelu_fast(float x) {
-  const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
-  float poly = 1.061405429f;
-  poly = poly * t - 1.453152027f;
-  poly = poly * t + 1.421413741f;
-  poly = poly * t - 0.284496736f;
-  poly = poly * t + 0.254829592f;
-  poly = poly * t;
-  const float erf_abs = 1.0f - poly * __expf(-z * z);
-  const float erf_v = copysignf(erf_abs, x);
-  return 0.5f * x * (1.0f + erf_v);
-}
-
 // Issue the DMA of one 128x64 bf16 tile (rows [r0, r0+128) of a K-contiguous
 // matrix with leading dimension ld, columns [k0, k0+64)) into LDS.
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int ld, int r0, int rmax, int k0,
@@ -395,8 +378,11 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
                           acc[i][j][3] + bias[j].w};
             acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             if constexpr (EPI == EPI_GELU_BF16) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+              const f32x2 g0 = gelu_erf2((f32x2){v[0], v[1]}), g1 = gelu_erf2((f32x2){v[2], v[3]});
+              v[0] = g0.x;
+              v[1] = g0.y;
+              v[2] = g1.x;
+              v[3] = g1.y;
             }
             pk[h][0] = pack_bf16x2(v[0], v[1]);
             pk[h][1] = pack_bf16x2(v[2], v[3]);
@@ -807,8 +793,11 @@ __global__ __launch_bounds__(B2T, 2) void gemm256m32_kernel(GemmArgs p, int tile
               float v[4] = {acc[i][j][4 * g4 + 0] + bb.x, acc[i][j][4 * g4 + 1] + bb.y,
                             acc[i][j][4 * g4 + 2] + bb.z, acc[i][j][4 * g4 + 3] + bb.w};
               if constexpr (EPI == EPI_GELU_BF16) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = gelu_fast(v[e]);
+                const f32x2 g0 = gelu_erf2((f32x2){v[0], v[1]}), g1 = gelu_erf2((f32x2){v[2], v[3]});
+                v[0] = g0.x;
+                v[1] = g0.y;
+                v[2] = g1.x;
+                v[3] = g1.y;
               }
               pk[h][0] = pack_bf16x2(v[0], v[1]);
               pk[h][1] = pack_bf16x2(v[2], v[3]);

@@ -41,6 +41,7 @@ namespace mq {
 
 int g_gemm_pingpong = 1;
 int g_gemm_pp_ablate = 0;
+int g_gemm_pp_bal = 0;
 
 namespace {
 
@@ -48,7 +49,7 @@ constexpr int PP_BM = 256, PP_BN = 256, PP_BK = 64, PP_T = 512;
 constexpr int PP_OP = PP_BM * PP_BK * 2;  // 32 KiB: one operand slice of a stage
 constexpr int PP_STAGE = 2 * PP_OP;       // 64 KiB
 constexpr int PP_BIAS = 2 * PP_STAGE;     // bias area: 8 waves x 256 B
-constexpr int PP_LDS = PP_BIAS + 8 * 256;
+constexpr int PP_LDS = PP_BIAS + 2 * 8 * 256;  // two bias slots (stage parity) for the balanced schedule
 
 __device__ __forceinline__ int pp_swz(int row) { return (row >> 1) & 7; }
 
@@ -73,21 +74,6 @@ __device__ __forceinline__ void pp_wait_vm() {
 __device__ __forceinline__ void pp_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
-}
-
-// exact-erf GELU, erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7; same as gemm_bf16.hip)
-__device__ __forceinline__ float pp_gelu(float x) {
-  const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(1.0f + 0.3275911f * z);
-  float poly = 1.061405429f;
-  poly = poly * t - 1.453152027f;
-  poly = poly * t + 1.421413741f;
-  poly = poly * t - 0.284496736f;
-  poly = poly * t + 0.254829592f;
-  poly = poly * t;
-  const float erf_abs = 1.0f - poly * __expf(-z * z);
-  const float erf_v = copysignf(erf_abs, x);
-  return 0.5f * x * (1.0f + erf_v);
 }
 
 __device__ __forceinline__ void pp_tile_coords(int wid, int tiles_m, int tiles_n, int& m0, int& n0) {
@@ -121,9 +107,22 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
                                             int n0, int wm, int wn, int lane) {
   const int mm = lane & 15;
   const int nn = 4 * (lane >> 4);
+  // The bias slice was LDS-DMA'd and retired by this wave's own counted vmcnt.  Read it in inline asm:
+  // a plain LDS read here makes the compiler wait vmcnt(0) for every DMA in flight (it cannot tell the
+  // bias slot from the stage buffers the in-flight DMAs write).
+  f32x4 bv[4];
+  {
+    const unsigned addr = (unsigned)(uintptr_t)MQ_LDS_LOCAL(bias_lds + nn);
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
+        "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
+        : "v"(addr)
+        : "memory");
+  }
   float4 bias[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bias[j] = *reinterpret_cast<const float4*>(bias_lds + j * 16 + nn);
+  for (int j = 0; j < 4; ++j) bias[j] = make_float4(bv[j][0], bv[j][1], bv[j][2], bv[j][3]);
   const bool full = (m0 + PP_BM <= p.M) && (n0 + PP_BN <= p.N);
   if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
     // pair fragments (j, j+1): v_permlane16_swap gives every lane 8 consecutive columns -> one
@@ -143,8 +142,11 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
                         acc[i][j][3] + bias[j].w};
           acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
           if constexpr (EPI == EPI_GELU_BF16) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = pp_gelu(v[e]);
+            const f32x2 g0 = gelu_erf2((f32x2){v[0], v[1]}), g1 = gelu_erf2((f32x2){v[2], v[3]});
+            v[0] = g0.x;
+            v[1] = g0.y;
+            v[2] = g1.x;
+            v[3] = g1.y;
           }
           pk[h][0] = pack_bf16x2(v[0], v[1]);
           pk[h][1] = pack_bf16x2(v[2], v[3]);
@@ -223,7 +225,12 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
 // ABL (timing ablations, WRONG results when non-zero; EPI_BF16 only): bit0 no vmcnt waits in the
 // K-loop, bit1 no steady-state DMA, bit2 no fragment re-reads after the first K-step, bit3 no barriers
 // in the K-loop.
-template <int EPI, int ABL = 0>
+// BAL: the balanced schedule -- the (0,0) quadrant's W fragments of stage g+1 are read in phase 3 of
+// stage g (P0(g+1) is then issued whole in phase 0 and waited in phase 2), so every phase reads 4 or 8
+// fragments (8/4/8/4 instead of 12/4/8/0); the bias DMA moves to phase 3 (for stage g+1, two bias
+// slots by stage parity).  DMA per phase 4/2/2/1; waits: phase 0 vmcnt(7) retires P1(g), phase 1
+// vmcnt(7) P2(g), phase 2 vmcnt(4) P0(g+1) and the bias of stage g.
+template <int EPI, int ABL = 0, bool BAL = false>
 __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -327,6 +334,97 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
+  if constexpr (BAL) {
+    // prologue: stage 0 into buffer 0 + its bias into bias slot 0; P0(0) lands before the first reads
+#pragma unroll
+    for (int i = 0; i < 8; ++i) issue(i, 0);
+    advance();
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
+    pp_wait_vm<5>();
+    pp_barrier();
+    if (wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[j][kk] = pp_frag(smem + PP_OP, wn * 64 + j * 16 + frow, kk * 4 + fk);
+    constexpr int EPI_OPS_B = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
+    bool pend = false;
+    for (int g = 0; g < total; ++g) {
+      const int slot = g & 1;
+      const char* As = smem + slot * PP_STAGE;
+      const char* Ws = As + PP_OP;
+      // ---- phase 0: quadrant (0,0); DMA P0(g+1)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, wm * 128 + i * 16 + frow, kk * 4 + fk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) issue(i, slot ^ 1);
+      if (pend)
+        pp_wait_vm<7 + EPI_OPS_B>();
+      else
+        pp_wait_vm<7>();
+      open_mfma();
+      mfma_quadrant(0, 0, b0);
+      bar();
+      // ---- phase 1: quadrant (0,1); DMA P1(g+1)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b1[j][kk] = pp_frag(Ws, wn * 64 + 32 + j * 16 + frow, kk * 4 + fk);
+      issue(4, slot ^ 1);
+      issue(5, slot ^ 1);
+      if (pend)
+        pp_wait_vm<7 + EPI_OPS_B>();
+      else
+        pp_wait_vm<7>();
+      pend = false;
+      open_mfma();
+      mfma_quadrant(0, 1, b1);
+      bar();
+      // ---- phase 2: quadrant (1,0); DMA P2(g+1); P0(g+1) (and the bias of stage g) retired
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
+      issue(6, slot ^ 1);
+      issue(7, slot ^ 1);
+      advance();
+      pp_wait_vm<4>();
+      open_mfma();
+      mfma_quadrant(1, 0, b0);
+      bar();
+      // ---- phase 3: quadrant (1,1); stage g+1's (0,0) W fragments; bias of stage g+1
+      {
+        const char* Wn = smem + (slot ^ 1) * PP_STAGE + PP_OP;  // past the end: a harmless re-read
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) b0[j][kk] = pp_frag(Wn, wn * 64 + j * 16 + frow, kk * 4 + fk);
+        int nn0 = cn0;  // origin column of the tile stage g+1 belongs to
+        if (kt + 1 == nk && ct + 1 < my_tiles) {
+          int m_;
+          pp_tile_coords(lo + xb + (ct + 1) * nbx, tiles_m, tiles_n, m_, nn0);
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds + (slot ^ 1) * 2048), 4,
+                                                 (unsigned)((nn0 + wn * 64 + lane) * 4), 0, 0, 0);
+      }
+      open_mfma();
+      mfma_quadrant(1, 1, b1);
+      bar();
+      if (++kt == nk) {
+        pp_epilogue<EPI>(p, acc, reinterpret_cast<const float*>(bias_lds + slot * 2048), cm0, cn0, wm, wn, lane);
+        pend = (cm0 + PP_BM <= p.M) && (cn0 + PP_BN <= p.N);
+        kt = 0;
+        ++ct;
+        if (ct < my_tiles) pp_tile_coords(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
+      }
+    }
+    if (wm == 0) pp_barrier();  // balance the stagger
+    pp_wait_vm<0>();            // no DMA may outlive the block
+    return;
+  }
+
   // prologue: stage 0 into buffer 0; P0 (the 4 oldest DMAs) must land before the first reads
 #pragma unroll
   for (int i = 0; i < 8; ++i) issue(i, 0);
@@ -417,15 +515,23 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-template <int EPI, int ABL = 0>
-void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
+template <int EPI, int ABL = 0, bool BAL = false>
+void launch_pp1(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, ABL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              PP_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, ABL, BAL>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, BAL>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
+}
+
+template <int EPI, int ABL = 0>
+void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
+  if (ABL == 0 && g_gemm_pp_bal)
+    launch_pp1<EPI, 0, true>(grid, stream, p, tiles_m, tiles_n);
+  else
+    launch_pp1<EPI, ABL, false>(grid, stream, p, tiles_m, tiles_n);
 }
 
 }  // namespace

@@ -109,17 +109,19 @@ def _run_pair(M, N, K, epi, aux_rows, seed=0):
     if epi in (0, 1):
         C0 = C0.to(torch.bfloat16)
     outs = []
-    old = ctx.lib.mq_get_tuning(12)
+    old = ctx.lib.mq_get_tuning(12), ctx.lib.mq_get_tuning(14)
     try:
-        for pp in (0, 1):
+        for pp, bal in ((0, 0), (1, 0), (1, 1)):
             assert ctx.lib.mq_set_tuning(12, pp) == 0
+            assert ctx.lib.mq_set_tuning(14, bal) == 0
             Cm = C0.clone()
             _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), _lib.ptr(bias),
                                             _lib.ptr(aux), M, N, K, K, K, N, aux_rows, epi, _lib.stream_ptr()),
                        "mq_gemm_bf16")
             outs.append(Cm)
     finally:
-        ctx.lib.mq_set_tuning(12, old)
+        ctx.lib.mq_set_tuning(12, old[0])
+        ctx.lib.mq_set_tuning(14, old[1])
     torch.cuda.synchronize()
     return outs
 
@@ -132,9 +134,10 @@ def test_gemm_pingpong_bitwise_equals_interleaved(epi, M, N, K):
     then bias, then the epilogue op), so the ping-pong kernel must reproduce the other bit for bit,
     on full and ragged tiles and multi-tile persistent walks."""
     import torch
-    a, b = _run_pair(M, N, K, epi, aux_rows=192)
-    assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
-                       b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32))
+    outs = _run_pair(M, N, K, epi, aux_rows=192)
+    bits = [o.view(torch.int16) if o.dtype == torch.bfloat16 else o.view(torch.int32) for o in outs]
+    assert torch.equal(bits[0], bits[1])   # ping-pong, first schedule
+    assert torch.equal(bits[0], bits[2])   # ping-pong, balanced schedule
 
 
 def test_gemm_small_path_nchw():

@@ -57,6 +57,11 @@ def main():
         ctx.lib.mq_set_tuning(11, 0)
         ctx.lib.mq_set_tuning(12, 0)
         ctx.lib.mq_set_tuning(13, 0)
+        ctx.lib.mq_set_tuning(14, 0)
+        if var == "pb":  # ping-pong, balanced phase schedule
+            ctx.lib.mq_set_tuning(12, 1)
+            ctx.lib.mq_set_tuning(14, 1)
+            var_st = "4"
         if var.startswith("pa"):  # ping-pong timing ablations (bf16 epilogue shapes only; wrong results)
             ctx.lib.mq_set_tuning(12, 1)
             ctx.lib.mq_set_tuning(13, int(var[2:]))

@@ -1,0 +1,11 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=${1:-gelu}
+mkdir -p gpurun_out/$OUT
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_pose.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$OUT/pytest.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/$OUT/pytest.log; exit 1; }
+tail -1 gpurun_out/$OUT/pytest.log
+timeout -k 10 300 python3 tools/gemm_probe.py --iters 20 --shape fc1,fc1_bf16,fc2,proj --variants pp > gpurun_out/$OUT/gemm_probe.log 2>&1 || { echo PROBE FAILED; tail -20 gpurun_out/$OUT/gemm_probe.log; exit 1; }
+grep " r=1" gpurun_out/$OUT/gemm_probe.log
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 20 > gpurun_out/$OUT/b.json 2> gpurun_out/$OUT/b.err || { echo BENCH FAILED; tail -20 gpurun_out/$OUT/b.err; exit 1; }
+python3 -c "import json;d=json.load(open('gpurun_out/$OUT/b.json'));print('bench', d['value'], d['ms_per_step'], d['roofline']['achieved'])"
