@@ -52,7 +52,7 @@ const char* mq_last_error(void);
 #define MQ_TUNE_GEMM_PP_ABLATE 13   /* ping-pong GEMM timing ablations, bf16 epilogue only (WRONG results): 1 no vmcnt
                                        waits, 2 no steady-state DMA, 3 both, 4 no fragment re-reads, 8 no barriers,
                                        15 all */
-#define MQ_TUNE_GEMM_PP_BALANCED 14 /* 1: ping-pong GEMM with the balanced phase schedule (8/4/8/4 fragment reads per phase) */
+#define MQ_TUNE_GEMM_PP_DMA_IN_MFMA 14 /* 1: ping-pong GEMM issuing each phase's LDS-DMA between the issuing wave's own MFMAs */
 #define MQ_TUNE_OPTIM_PCG_ITERS 4  /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */

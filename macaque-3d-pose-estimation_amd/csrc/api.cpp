@@ -162,8 +162,8 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_GEMM_PINGPONG:
       mq::g_gemm_pingpong = value != 0;
       return 0;
-    case MQ_TUNE_GEMM_PP_BALANCED:
-      mq::g_gemm_pp_bal = value != 0;
+    case MQ_TUNE_GEMM_PP_DMA_IN_MFMA:
+      mq::g_gemm_pp_dim = value != 0;
       return 0;
     case MQ_TUNE_GEMM_PP_ABLATE:
       if (value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 8 && value != 15)
@@ -197,7 +197,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_GEMM_SYNC2: return mq::g_gemm_sync2;
     case MQ_TUNE_GEMM_PINGPONG: return mq::g_gemm_pingpong;
     case MQ_TUNE_GEMM_PP_ABLATE: return mq::g_gemm_pp_ablate;
-    case MQ_TUNE_GEMM_PP_BALANCED: return mq::g_gemm_pp_bal;
+    case MQ_TUNE_GEMM_PP_DMA_IN_MFMA: return mq::g_gemm_pp_dim;
     case MQ_TUNE_ATTENTION_ABLATE: return mq::g_attention_ablate;
     default: return fail("mq_get_tuning: unknown key", -2);
   }

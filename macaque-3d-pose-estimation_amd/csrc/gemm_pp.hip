@@ -41,7 +41,7 @@ namespace mq {
 
 int g_gemm_pingpong = 1;
 int g_gemm_pp_ablate = 0;
-int g_gemm_pp_bal = 0;
+int g_gemm_pp_dim = 0;
 
 namespace {
 
@@ -49,7 +49,7 @@ constexpr int PP_BM = 256, PP_BN = 256, PP_BK = 64, PP_T = 512;
 constexpr int PP_OP = PP_BM * PP_BK * 2;  // 32 KiB: one operand slice of a stage
 constexpr int PP_STAGE = 2 * PP_OP;       // 64 KiB
 constexpr int PP_BIAS = 2 * PP_STAGE;     // bias area: 8 waves x 256 B
-constexpr int PP_LDS = PP_BIAS + 2 * 8 * 256;  // two bias slots (stage parity) for the balanced schedule
+constexpr int PP_LDS = PP_BIAS + 8 * 256;
 
 __device__ __forceinline__ int pp_swz(int row) { return (row >> 1) & 7; }
 
@@ -225,12 +225,8 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
 // ABL (timing ablations, WRONG results when non-zero; EPI_BF16 only): bit0 no vmcnt waits in the
 // K-loop, bit1 no steady-state DMA, bit2 no fragment re-reads after the first K-step, bit3 no barriers
 // in the K-loop.
-// BAL: the balanced schedule -- the (0,0) quadrant's W fragments of stage g+1 are read in phase 3 of
-// stage g (P0(g+1) is then issued whole in phase 0 and waited in phase 2), so every phase reads 4 or 8
-// fragments (8/4/8/4 instead of 12/4/8/0); the bias DMA moves to phase 3 (for stage g+1, two bias
-// slots by stage parity).  DMA per phase 4/2/2/1; waits: phase 0 vmcnt(7) retires P1(g), phase 1
-// vmcnt(7) P2(g), phase 2 vmcnt(4) P0(g+1) and the bias of stage g.
-template <int EPI, int ABL = 0, bool BAL = false>
+// DIM: the DMA pieces of a phase are issued inside the issuing wave's MFMA segment (see below).
+template <int EPI, int ABL = 0, bool DIM = false>
 __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -334,90 +330,141 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
-  if constexpr (BAL) {
-    // prologue: stage 0 into buffer 0 + its bias into bias slot 0; P0(0) lands before the first reads
+  if constexpr (DIM) {
+    // DMA-in-MFMA schedule: each phase's DMA pieces are issued between the issuing wave's own MFMAs
+    // (after MFMA 4/8/12 or 6/12 of the quadrant) instead of in its load segment, so the TA issue cost
+    // of a piece overlaps the wave's MFMA stream and the partner's load segment holds only fragment
+    // reads.  Every piece lands one segment later than in the base schedule; waits: phase 0
+    // vmcnt(2) retires P1(g), phase 1 vmcnt(3) P2(g), phase 3 vmcnt(2) P0(g+1).
+    auto mf = [&](int qm, int qn, bf16x8 (&bb)[2][2], int t) {
+      const int kk = t >> 3, i = (t >> 1) & 3, j = t & 1;
+      acc[qm * 4 + i][qn * 2 + j] =
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][kk], a[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+    };
 #pragma unroll
     for (int i = 0; i < 8; ++i) issue(i, 0);
     advance();
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
-    pp_wait_vm<5>();
+    pp_wait_vm<4>();
     pp_barrier();
     if (wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b0[j][kk] = pp_frag(smem + PP_OP, wn * 64 + j * 16 + frow, kk * 4 + fk);
-    constexpr int EPI_OPS_B = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
+    constexpr int EPI_OPS_D = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
     bool pend = false;
     for (int g = 0; g < total; ++g) {
       const int slot = g & 1;
       const char* As = smem + slot * PP_STAGE;
       const char* Ws = As + PP_OP;
-      // ---- phase 0: quadrant (0,0); DMA P0(g+1)
+      // ---- phase 0: quadrant (0,0); DMA P0 slots 0,1 + bias inside the MFMA segment
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b0[j][kk] = pp_frag(Ws, wn * 64 + j * 16 + frow, kk * 4 + fk);
 #pragma unroll
         for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, wm * 128 + i * 16 + frow, kk * 4 + fk);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) issue(i, slot ^ 1);
+      }
       if (pend)
-        pp_wait_vm<7 + EPI_OPS_B>();
+        pp_wait_vm<2 + EPI_OPS_D>();
       else
-        pp_wait_vm<7>();
+        pp_wait_vm<2>();
       open_mfma();
-      mfma_quadrant(0, 0, b0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) mf(0, 0, b0, t);
+      issue(0, slot ^ 1);
+#pragma unroll
+      for (int t = 4; t < 8; ++t) mf(0, 0, b0, t);
+      issue(1, slot ^ 1);
+#pragma unroll
+      for (int t = 8; t < 12; ++t) mf(0, 0, b0, t);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
+#pragma unroll
+      for (int t = 12; t < 16; ++t) mf(0, 0, b0, t);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      __builtin_amdgcn_s_setprio(0);
       bar();
-      // ---- phase 1: quadrant (0,1); DMA P1(g+1)
+      // ---- phase 1: quadrant (0,1); DMA P0 slots 2,3
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int j = 0; j < 2; ++j) b1[j][kk] = pp_frag(Ws, wn * 64 + 32 + j * 16 + frow, kk * 4 + fk);
-      issue(4, slot ^ 1);
-      issue(5, slot ^ 1);
       if (pend)
-        pp_wait_vm<7 + EPI_OPS_B>();
+        pp_wait_vm<3 + EPI_OPS_D>();
       else
-        pp_wait_vm<7>();
+        pp_wait_vm<3>();
       pend = false;
       open_mfma();
-      mfma_quadrant(0, 1, b1);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) mf(0, 1, b1, t);
+      issue(2, slot ^ 1);
+#pragma unroll
+      for (int t = 6; t < 12; ++t) mf(0, 1, b1, t);
+      issue(3, slot ^ 1);
+#pragma unroll
+      for (int t = 12; t < 16; ++t) mf(0, 1, b1, t);
+      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      __builtin_amdgcn_s_setprio(0);
       bar();
-      // ---- phase 2: quadrant (1,0); DMA P2(g+1); P0(g+1) (and the bias of stage g) retired
+      // ---- phase 2: quadrant (1,0); DMA P1 slots 4,5
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
+      open_mfma();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) mf(1, 0, b0, t);
+      issue(4, slot ^ 1);
+#pragma unroll
+      for (int t = 6; t < 12; ++t) mf(1, 0, b0, t);
+      issue(5, slot ^ 1);
+#pragma unroll
+      for (int t = 12; t < 16; ++t) mf(1, 0, b0, t);
+      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
+      // ---- phase 3: quadrant (1,1); DMA P2 slots 6,7
+      pp_wait_vm<2>();
+      open_mfma();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) mf(1, 1, b1, t);
       issue(6, slot ^ 1);
+#pragma unroll
+      for (int t = 6; t < 12; ++t) mf(1, 1, b1, t);
       issue(7, slot ^ 1);
+#pragma unroll
+      for (int t = 12; t < 16; ++t) mf(1, 1, b1, t);
+      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
+      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+      __builtin_amdgcn_s_setprio(0);
+      bar();
       advance();
-      pp_wait_vm<4>();
-      open_mfma();
-      mfma_quadrant(1, 0, b0);
-      bar();
-      // ---- phase 3: quadrant (1,1); stage g+1's (0,0) W fragments; bias of stage g+1
-      {
-        const char* Wn = smem + (slot ^ 1) * PP_STAGE + PP_OP;  // past the end: a harmless re-read
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) b0[j][kk] = pp_frag(Wn, wn * 64 + j * 16 + frow, kk * 4 + fk);
-        int nn0 = cn0;  // origin column of the tile stage g+1 belongs to
-        if (kt + 1 == nk && ct + 1 < my_tiles) {
-          int m_;
-          pp_tile_coords(lo + xb + (ct + 1) * nbx, tiles_m, tiles_n, m_, nn0);
-        }
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds + (slot ^ 1) * 2048), 4,
-                                                 (unsigned)((nn0 + wn * 64 + lane) * 4), 0, 0, 0);
-      }
-      open_mfma();
-      mfma_quadrant(1, 1, b1);
-      bar();
       if (++kt == nk) {
-        pp_epilogue<EPI>(p, acc, reinterpret_cast<const float*>(bias_lds + slot * 2048), cm0, cn0, wm, wn, lane);
+        pp_epilogue<EPI>(p, acc, reinterpret_cast<const float*>(bias_lds), cm0, cn0, wm, wn, lane);
         pend = (cm0 + PP_BM <= p.M) && (cn0 + PP_BN <= p.N);
         kt = 0;
         ++ct;
-        if (ct < my_tiles) pp_tile_coords(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
+        if (ct < my_tiles) {
+          pp_tile_coords(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
+          bias_off = (unsigned)((cn0 + wn * 64 + lane) * 4);
+        }
       }
     }
     if (wm == 0) pp_barrier();  // balance the stagger
@@ -515,20 +562,20 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-template <int EPI, int ABL = 0, bool BAL = false>
+template <int EPI, int ABL = 0, bool DIM = false>
 void launch_pp1(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, ABL, BAL>,
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, ABL, DIM>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, BAL>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, DIM>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
 }
 
 template <int EPI, int ABL = 0>
 void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
-  if (ABL == 0 && g_gemm_pp_bal)
+  if (ABL == 0 && g_gemm_pp_dim)
     launch_pp1<EPI, 0, true>(grid, stream, p, tiles_m, tiles_n);
   else
     launch_pp1<EPI, ABL, false>(grid, stream, p, tiles_m, tiles_n);

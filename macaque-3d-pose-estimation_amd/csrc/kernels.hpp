@@ -38,7 +38,7 @@ extern bool g_gemm_force_small;
 // ping-pong 256x256 kernel (gemm_pp.hip): the two wave groups of a block alternate LDS traffic and MFMA
 extern int g_gemm_pingpong;
 extern int g_gemm_pp_ablate;
-extern int g_gemm_pp_bal;
+extern int g_gemm_pp_dim;
 bool gemm_pingpong_fits(const GemmArgs& p, int epi);
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 

@@ -137,7 +137,7 @@ def test_gemm_pingpong_bitwise_equals_interleaved(epi, M, N, K):
     outs = _run_pair(M, N, K, epi, aux_rows=192)
     bits = [o.view(torch.int16) if o.dtype == torch.bfloat16 else o.view(torch.int32) for o in outs]
     assert torch.equal(bits[0], bits[1])   # ping-pong, first schedule
-    assert torch.equal(bits[0], bits[2])   # ping-pong, balanced schedule
+    assert torch.equal(bits[0], bits[2])   # ping-pong, DMA issued inside the MFMA segments
 
 
 def test_gemm_small_path_nchw():

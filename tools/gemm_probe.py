@@ -58,7 +58,7 @@ def main():
         ctx.lib.mq_set_tuning(12, 0)
         ctx.lib.mq_set_tuning(13, 0)
         ctx.lib.mq_set_tuning(14, 0)
-        if var == "pb":  # ping-pong, balanced phase schedule
+        if var == "pd":  # ping-pong, DMA issued inside the MFMA segment
             ctx.lib.mq_set_tuning(12, 1)
             ctx.lib.mq_set_tuning(14, 1)
             var_st = "4"

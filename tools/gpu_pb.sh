@@ -5,7 +5,7 @@ OUT=${1:-pb}
 mkdir -p gpurun_out/$OUT
 timeout -k 10 400 python3 -u -m pytest tests/test_gpu_gemm.py -x -q --timeout 120 --timeout-method thread > gpurun_out/$OUT/pytest.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/$OUT/pytest.log; exit 1; }
 tail -1 gpurun_out/$OUT/pytest.log
-timeout -k 10 300 python3 tools/gemm_probe.py --iters 20 --shape qkv,fc1,fc1_bf16,fc2,dc1,dc2 --variants pp,pb > gpurun_out/$OUT/gemm_probe.log 2>&1 || { echo PROBE FAILED; tail -20 gpurun_out/$OUT/gemm_probe.log; exit 1; }
+timeout -k 10 300 python3 tools/gemm_probe.py --iters 20 --shape qkv,fc1,fc1_bf16,fc2,dc1,dc2 --variants pp,pd > gpurun_out/$OUT/gemm_probe.log 2>&1 || { echo PROBE FAILED; tail -20 gpurun_out/$OUT/gemm_probe.log; exit 1; }
 grep " r=1" gpurun_out/$OUT/gemm_probe.log
 for c in "14=0" "14=1" "14=0" "14=1"; do
   MQ_TUNING="$c" timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 20 > gpurun_out/$OUT/b.json 2> gpurun_out/$OUT/b.err || { echo BENCH FAILED "$c"; tail -20 gpurun_out/$OUT/b.err; exit 1; }
