@@ -170,6 +170,9 @@ int mq_set_tuning(int key, int value) {
         return fail("mq_set_tuning: ping-pong ablation must be 0, 1, 2, 3, 4, 8 or 15", -2);
       mq::g_gemm_pp_ablate = value;
       return 0;
+    case MQ_TUNE_ATTENTION_PERSIST:
+      mq::g_attention_persist = value != 0;
+      return 0;
     case MQ_TUNE_ATTENTION_ABLATE:
       if (value < 0 || value > 3) return fail("mq_set_tuning: attention ablation must be 0..3", -2);
       mq::g_attention_ablate = value;
@@ -199,6 +202,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_GEMM_PP_ABLATE: return mq::g_gemm_pp_ablate;
     case MQ_TUNE_GEMM_PP_DMA_IN_MFMA: return mq::g_gemm_pp_dim;
     case MQ_TUNE_ATTENTION_ABLATE: return mq::g_attention_ablate;
+    case MQ_TUNE_ATTENTION_PERSIST: return mq::g_attention_persist;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }

@@ -46,6 +46,7 @@ int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
                        float eps, hipStream_t s);
 extern int g_attention_ablate;
+extern int g_attention_persist;
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s);
 int patch_im2col(const float* crops, unsigned short* A, int n_crops, int flip_copies, int img_h, int img_w,

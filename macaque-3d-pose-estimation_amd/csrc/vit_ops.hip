@@ -16,18 +16,22 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const float* xr = x + (size_t)row * dim;
-  float4 v[MAXIT];
-  float s = 0.f;
+  float4 v[MAXIT], gg[MAXIT], bb[MAXIT];
+  // gamma / beta are loaded together with the row (one memory round trip per wave, not two)
 #pragma unroll
   for (int it = 0; it < MAXIT; ++it) {
     const int i = it * 256 + lane * 4;
     if (i < dim) {
       v[it] = *reinterpret_cast<const float4*>(xr + i);
-      s += (v[it].x + v[it].y) + (v[it].z + v[it].w);
+      gg[it] = *reinterpret_cast<const float4*>(g + i);
+      bb[it] = *reinterpret_cast<const float4*>(b + i);
     } else {
-      v[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      v[it] = gg[it] = bb[it] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  float s = 0.f;
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) s += (v[it].x + v[it].y) + (v[it].z + v[it].w);
   const float mean = wave_sum(s) / (float)dim;
   float q = 0.f;
 #pragma unroll
@@ -44,11 +48,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   for (int it = 0; it < MAXIT; ++it) {
     const int i = it * 256 + lane * 4;
     if (i < dim) {
-      const float4 gg = *reinterpret_cast<const float4*>(g + i);
-      const float4 bb = *reinterpret_cast<const float4*>(b + i);
       uint2 o;
-      o.x = pack_bf16x2((v[it].x - mean) * rstd * gg.x + bb.x, (v[it].y - mean) * rstd * gg.y + bb.y);
-      o.y = pack_bf16x2((v[it].z - mean) * rstd * gg.z + bb.z, (v[it].w - mean) * rstd * gg.w + bb.w);
+      o.x = pack_bf16x2((v[it].x - mean) * rstd * gg[it].x + bb[it].x, (v[it].y - mean) * rstd * gg[it].y + bb[it].y);
+      o.y = pack_bf16x2((v[it].z - mean) * rstd * gg[it].z + bb[it].z, (v[it].w - mean) * rstd * gg[it].w + bb[it].w);
       *reinterpret_cast<uint2*>(yr + i) = o;
     }
   }
@@ -260,12 +262,224 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t*
   }
 }
 
+// Persistent variant for the ViT grid (T = 192): 2 workgroups per CU walk (image, head) items with
+// stride gridDim.x and overlap the next item's staging with the current item's compute inside one
+// LDS footprint: K is refilled (LDS-DMA) right after every wave has finished S^T = K Q^T; V is
+// refilled and the next item's Q fragments loaded after P V.  The staging
+// of item i+1 therefore runs under item i's softmax, P V and output stores instead of in lockstep
+// with the co-resident workgroup's.  Same arithmetic as attention_kernel (bit-identical outputs).
+// Waits: all staging of an item is retired by a counted vmcnt at the loop head that leaves the 40
+// output stores of the previous item in flight.
+int g_attention_persist = 0;
+
+template <int DH>
+__global__ __launch_bounds__(ATT_THREADS, 3) void attention_persist_kernel(const bf16_t* __restrict__ qkv,
+                                                                            bf16_t* __restrict__ out, int D, int H,
+                                                                            float scale_log2, int n_items) {
+  using L = AttLayout<DH>;
+  constexpr int T = ATT_MAXT;
+  constexpr int NKS = DH / 16;
+  constexpr int DCH = DH / 8;
+  constexpr int NTB = T / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kimg = smem;
+  char* Vimg = smem + L::KBYTES;
+  int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int l16 = lane & 15, g = lane >> 4;
+  const int ld = 3 * D;
+  constexpr int nk_ins = (T * L::KCH + 63) / 64, nv_ins = (T * L::VCH + 63) / 64;
+
+  auto issue_k = [&](int it) {
+    const int img = it / H, h = it % H;
+    const bf16_t* kbase = qkv + (size_t)img * T * ld + D + h * DH;
+    for (int ins = wave; ins < nk_ins; ins += ATT_WAVES) {
+      const int q = ins * 64 + lane;
+      int t = q / L::KCH, ch = q - (q / L::KCH) * L::KCH;
+      if (t >= T || ch >= DCH) t = 0, ch = 0;
+      __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(kbase + (size_t)t * ld + ch * 8),
+                                       MQ_LDS_LOCAL(Kimg + ins * 1024), 16, 0, 0);
+    }
+  };
+  auto issue_v = [&](int it) {
+    const int img = it / H, h = it % H;
+    const bf16_t* vbase = qkv + (size_t)img * T * ld + 2 * D + h * DH;
+    for (int ins = wave; ins < nv_ins; ins += ATT_WAVES) {
+      const int q = ins * 64 + lane;
+      int t = q / L::VCH, ch = q - (q / L::VCH) * L::VCH;
+      if (t >= T || ch >= DCH) t = 0, ch = 0;
+      __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(vbase + (size_t)t * ld + ch * 8),
+                                       MQ_LDS_LOCAL(Vimg + ins * 1024), 16, 0, 0);
+    }
+  };
+  short4v qf[2][NKS];
+  auto load_q = [&](int it) {
+    const int img = it / H, h = it % H;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = (wave + u * ATT_WAVES) * 16 + l16;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks)
+        qf[u][ks] = *reinterpret_cast<const short4v*>(qkv + ((size_t)img * T + q) * ld + h * DH + ks * 16 + 4 * g);
+    }
+  };
+
+  int item = blockIdx.x;
+  if (item >= n_items) return;
+  issue_k(item);
+  issue_v(item);
+  load_q(item);
+  bool first = true;
+  for (; item < n_items; item += gridDim.x) {
+    const int next = item + gridDim.x;
+    const bool has_next = next < n_items;
+    // opaque per item: keeps the compiler from hoisting the many lane-derived LDS addresses out of
+    // the item loop (they would stay live through it and spill)
+    asm volatile("" : "+v"(lane));
+    l16 = lane & 15;
+    g = lane >> 4;
+    // this item's K, V and Q have landed (the previous item's 40 output stores may stay in flight)
+    if (first)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
+    first = false;
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    f32x4 S[2][NTB];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int tb = 0; tb < NTB; ++tb) S[u][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+#pragma unroll
+      for (int tb = 0; tb < NTB; ++tb) {
+        const short4v kf =
+            *reinterpret_cast<const short4v*>(Kimg + (tb * 16 + l16) * (L::KCH * 16) + (ks * 16 + 4 * g) * 2);
+        S[0][tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[0][ks], S[0][tb], 0, 0, 0);
+        S[1][tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[1][ks], S[1][tb], 0, 0, 0);
+      }
+    }
+    // every wave's K reads are consumed (the MFMAs above waited for them): refill K, reload Q
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (has_next) issue_k(next);
+
+    bf16x8 P[2][T / 32];
+    float lsum[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int tb = 0; tb < NTB; ++tb)
+        m = fmaxf(m, fmaxf(fmaxf(S[u][tb][0], S[u][tb][1]), fmaxf(S[u][tb][2], S[u][tb][3])));
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      m = fmaxf(m, __shfl_xor(m, 32, 64));
+      const float mb = m * scale_log2;
+      float ls = 0.f;
+#pragma unroll
+      for (int tb = 0; tb < NTB; ++tb) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pv = __builtin_amdgcn_exp2f(S[u][tb][e] * scale_log2 - mb);
+          S[u][tb][e] = pv;
+          ls += pv;
+        }
+      }
+      ls += __shfl_xor(ls, 16, 64);
+      ls += __shfl_xor(ls, 32, 64);
+      lsum[u] = ls;
+#pragma unroll
+      for (int kst = 0; kst < T / 32; ++kst) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          P[u][kst][e] = (__bf16)S[u][2 * kst][e];
+          P[u][kst][4 + e] = (__bf16)S[u][2 * kst + 1][e];
+        }
+      }
+    }
+
+    f32x4 O[2][NKS];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int dt = 0; dt < NKS; ++dt) O[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int trq = l16 >> 2, trp = l16 & 3;
+#pragma unroll
+    for (int kst = 0; kst < T / 32; ++kst) {
+#pragma unroll
+      for (int dt = 0; dt < NKS; ++dt) {
+        const int ra = 2 * kst * 16 + 4 * g + trq;
+        const char* pa = Vimg + ra * (L::VCH * 16) + (dt * 16 + 4 * trp) * 2;
+        const short4v v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa));
+        const short4v v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa + 16 * (L::VCH * 16)));
+        bf16x8 vb;
+        const short4v* pv0 = &v0;
+        const short4v* pv1 = &v1;
+        __builtin_memcpy(&vb, pv0, 8);
+        __builtin_memcpy(reinterpret_cast<char*>(&vb) + 8, pv1, 8);
+        O[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[0][kst], vb, O[0][dt], 0, 0, 0);
+        O[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[1][kst], vb, O[1][dt], 0, 0, 0);
+      }
+    }
+    // every wave's V reads are consumed: refill V; the Q registers are free again (loading the next
+    // Q right after S^T would keep 20 more VGPRs live through softmax and P V: scratch spills)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (has_next) {
+      issue_v(next);
+      load_q(next);
+    }
+
+    const int img = item / H, h = item % H;
+    const size_t row0 = (size_t)img * T;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qb = wave + u * ATT_WAVES;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float inv = 1.0f / __shfl(lsum[u], 4 * g + e, 64);
+        const int qq = qb * 16 + 4 * g + e;
+        bf16_t* orow = out + (row0 + qq) * D + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = __builtin_bit_cast(bf16_t, (__bf16)(O[u][dt][e] * inv));
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 int g_attention_ablate = 0;
 
 template <int DH>
 static void launch_attention(dim3 grid, dim3 block, hipStream_t s, const unsigned short* qkv, unsigned short* out,
                              int tokens, int dim, int heads, float scale_log2) {
   constexpr int lds = AttLayout<DH>::LDS;
+  if (tokens == ATT_MAXT && g_attention_persist && g_attention_ablate == 0) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)attention_persist_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                lds);
+      attr = true;
+    }
+    static int n_cus = 0;
+    if (!n_cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !n_cus) n_cus = 256;
+    }
+    const int n_items = (int)grid.x;
+    const int wgs = n_items < 2 * n_cus ? n_items : 2 * n_cus;  // two resident workgroups per CU
+    hipLaunchKernelGGL((attention_persist_kernel<DH>), dim3(wgs), block, lds, s, qkv, out, dim, heads, scale_log2,
+                       n_items);
+    return;
+  }
   if (tokens == ATT_MAXT) {
     switch (g_attention_ablate) {
       case 1: hipLaunchKernelGGL((attention_kernel<DH, 1, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;

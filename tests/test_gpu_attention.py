@@ -45,3 +45,30 @@ def test_attention_rejects_bad_shapes():
     out = torch.zeros((100, 1280), device="cuda", dtype=torch.bfloat16)
     assert ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), 1, 100, 1280, 16, None) != 0
     assert ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), 1, 96, 1280, 10, None) != 0
+
+
+@pytest.mark.parametrize("n", [1, 7, 64])
+def test_attention_persistent_bitwise_equals_per_item(n):
+    """The persistent T=192 kernel (MQ_TUNE_ATTENTION_PERSIST, K/V of the next (image, head) staged
+    under the current one's compute) runs the same arithmetic as the one-workgroup-per-item kernel:
+    outputs must match bit for bit, including grids with fewer items than workgroups."""
+    import torch
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    T, D, H = 192, 1280, 16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(100 + n)
+    qkv = (torch.randn((n * T, 3 * D), generator=g, device="cuda") * 2).to(torch.bfloat16)
+    outs = []
+    old = ctx.lib.mq_get_tuning(15)
+    try:
+        for persist in (0, 1):
+            assert ctx.lib.mq_set_tuning(15, persist) == 0
+            out = torch.full((n * T, D), float("nan"), device="cuda", dtype=torch.bfloat16)
+            _lib.check(ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), n, T, D, H,
+                                                 _lib.stream_ptr()), "mq_attention_bf16")
+            outs.append(out)
+    finally:
+        ctx.lib.mq_set_tuning(15, old)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))

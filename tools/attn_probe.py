@@ -16,8 +16,10 @@ def main():
     out = torch.empty((n * T, D), device="cuda", dtype=torch.bfloat16)
     s = _lib.stream_ptr()
     for rnd in range(2):
-        for mode in (0, 1, 2, 3):
-            assert ctx.lib.mq_set_tuning(8, mode) == 0
+        for mode in ("p", 0, 1, 2, 3):
+            # "p": the persistent kernel (MQ_TUNE_ATTENTION_PERSIST); the others run the per-item kernel
+            assert ctx.lib.mq_set_tuning(15, 1 if mode == "p" else 0) == 0
+            assert ctx.lib.mq_set_tuning(8, 0 if mode == "p" else mode) == 0
             for _ in range(3):
                 ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), n, T, D, H, s)
             torch.cuda.synchronize()
@@ -31,6 +33,7 @@ def main():
             print(f"attention mode={mode} r={rnd}: {us:.1f} us  ({2 * 2 * n * H * T * T * (D // H) / (us * 1e-6) / 1e12:.0f} TFLOP/s)",
                   flush=True)
     ctx.lib.mq_set_tuning(8, 0)
+    ctx.lib.mq_set_tuning(15, 1)
 
 
 if __name__ == "__main__":
