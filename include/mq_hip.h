@@ -53,6 +53,8 @@ const char* mq_last_error(void);
                                        waits, 2 no steady-state DMA, 3 both, 4 no fragment re-reads, 8 no barriers,
                                        15 all */
 #define MQ_TUNE_GEMM_PP_DMA_IN_MFMA 14 /* 1: ping-pong GEMM issuing each phase's LDS-DMA between the issuing wave's own MFMAs */
+#define MQ_TUNE_GEMM_PP_RESID_PREFETCH 16 /* 1: short-K residual GEMMs (proj) on the ping-pong kernel with the residual
+                                       tile prefetched during the K-loop (measured 13 % slower); 0 (default): interleaved kernel */
 #define MQ_TUNE_ATTENTION_PERSIST 15 /* 1: T = 192 attention as 2 persistent workgroups per CU that stage the
                                        next (image, head) while computing the current one (measured 3 % slower: the kernel is compute-bound); 0 (default): one workgroup per item */
 #define MQ_TUNE_OPTIM_PCG_ITERS 4  /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */

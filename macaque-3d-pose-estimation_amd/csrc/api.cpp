@@ -165,6 +165,9 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_GEMM_PP_DMA_IN_MFMA:
       mq::g_gemm_pp_dim = value != 0;
       return 0;
+    case MQ_TUNE_GEMM_PP_RESID_PREFETCH:
+      mq::g_gemm_pp_resid_pf = value != 0;
+      return 0;
     case MQ_TUNE_GEMM_PP_ABLATE:
       if (value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 8 && value != 15)
         return fail("mq_set_tuning: ping-pong ablation must be 0, 1, 2, 3, 4, 8 or 15", -2);
@@ -200,6 +203,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_GEMM_SYNC2: return mq::g_gemm_sync2;
     case MQ_TUNE_GEMM_PINGPONG: return mq::g_gemm_pingpong;
     case MQ_TUNE_GEMM_PP_ABLATE: return mq::g_gemm_pp_ablate;
+    case MQ_TUNE_GEMM_PP_RESID_PREFETCH: return mq::g_gemm_pp_resid_pf;
     case MQ_TUNE_GEMM_PP_DMA_IN_MFMA: return mq::g_gemm_pp_dim;
     case MQ_TUNE_ATTENTION_ABLATE: return mq::g_attention_ablate;
     case MQ_TUNE_ATTENTION_PERSIST: return mq::g_attention_persist;

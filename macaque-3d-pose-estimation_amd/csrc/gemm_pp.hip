@@ -49,7 +49,8 @@ constexpr int PP_BM = 256, PP_BN = 256, PP_BK = 64, PP_T = 512;
 constexpr int PP_OP = PP_BM * PP_BK * 2;  // 32 KiB: one operand slice of a stage
 constexpr int PP_STAGE = 2 * PP_OP;       // 64 KiB
 constexpr int PP_BIAS = 2 * PP_STAGE;     // bias area: 8 waves x 256 B
-constexpr int PP_LDS = PP_BIAS + 8 * 256;
+constexpr int PP_PF = PP_BIAS + 8 * 256;  // residual-prefetch sink: 8 waves x 1 KiB, never read
+constexpr int PP_LDS = PP_PF + 8 * 1024;
 
 __device__ __forceinline__ int pp_swz(int row) { return (row >> 1) & 7; }
 
@@ -226,7 +227,12 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
 // K-loop, bit1 no steady-state DMA, bit2 no fragment re-reads after the first K-step, bit3 no barriers
 // in the K-loop.
 // DIM: the DMA pieces of a phase are issued inside the issuing wave's MFMA segment (see below).
-template <int EPI, int ABL = 0, bool DIM = false>
+// PF (EPI_RESID_F32 at short K): the residual tile is prefetched during the K-loop -- two 1-KiB
+// LDS-DMA row reads per K-step and wave into a sink area that is never read -- so the epilogue's
+// read-modify-write hits the L2 / Infinity Cache instead of paying HBM latency and bandwidth at the
+// moment every CU reaches its epilogue.  The two prefetch DMAs sit in phase 2 (after P1), so the
+// phase-0 and phase-3 waits count two more younger operations.
+template <int EPI, int ABL = 0, bool DIM = false, bool PF = false>
 __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -472,11 +478,28 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     return;
   }
 
+  const __amdgpu_buffer_rsrc_t rsC =
+      __builtin_amdgcn_make_buffer_rsrc(p.C, 0, PF ? (int)((size_t)p.M * p.ldc * 4) : 0, 0x00020000);
+  char* pf_sink = smem + PP_PF + wave * 1024;
+  // prefetch rows 2*kt, 2*kt+1 (mod 32) of this wave's 32 rows of the compute tile's residual
+  auto prefetch = [&]() {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int row = cm0 + wave * 32 + ((2 * kt + r) & 31);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, MQ_LDS_LOCAL(pf_sink), 16,
+                                               (unsigned)(((size_t)row * p.ldc + cn0) * 4 + lane * 16), 0, 0, 0);
+    }
+  };
+  constexpr int NPF = PF ? 2 : 0;
+
   // prologue: stage 0 into buffer 0; P0 (the 4 oldest DMAs) must land before the first reads
 #pragma unroll
-  for (int i = 0; i < 8; ++i) issue(i, 0);
+  for (int i = 0; i < 6; ++i) issue(i, 0);
+  if constexpr (PF) prefetch();  // keeps the phase-0 wait count of the first K-step uniform
+  issue(6, 0);
+  issue(7, 0);
   advance();
-  pp_wait_vm<4>();
+  pp_wait_vm<4 + NPF>();
   if constexpr (ABL != 0) {
     pp_wait_vm<0>();
     g_abl_started = true;
@@ -506,9 +529,9 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     if constexpr ((ABL & 2) == 0)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
     if (stores_pending)
-      pp_wait_vm_loop<5 + EPI_OPS, ABL>();
+      pp_wait_vm_loop<5 + NPF + EPI_OPS, ABL>();
     else
-      pp_wait_vm_loop<5, ABL>();
+      pp_wait_vm_loop<5 + NPF, ABL>();
     open_mfma();
     mfma_quadrant(0, 0, b0);
     bar();
@@ -536,6 +559,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
         if (!(ABL & 4) || g == 0) a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
     issue(4, slot ^ 1);
     issue(5, slot ^ 1);
+    if constexpr (PF) prefetch();
     open_mfma();
     mfma_quadrant(1, 0, b0);
     bar();
@@ -543,7 +567,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     issue(6, slot ^ 1);
     issue(7, slot ^ 1);
     advance();
-    pp_wait_vm_loop<4, ABL>();
+    pp_wait_vm_loop<4 + NPF, ABL>();
     open_mfma();
     mfma_quadrant(1, 1, b1);
     bar();
@@ -562,15 +586,15 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-template <int EPI, int ABL = 0, bool DIM = false>
+template <int EPI, int ABL = 0, bool DIM = false, bool PF = false>
 void launch_pp1(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, ABL, DIM>,
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, ABL, DIM, PF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, DIM>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, DIM, PF>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
 }
 
 template <int EPI, int ABL = 0>
@@ -583,12 +607,16 @@ void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, in
 
 }  // namespace
 
-// Routing: every 256x256 GEMM with K % 64 == 0, except the f32 residual read-modify-write at
-// short K (proj, K = 1280: one tile per CU, 20 K-steps): there the residual loads stall both wave
-// groups of the ping-pong at the tile end, and the interleaved kernel measured 8 % faster
-// (755 vs 692 TFLOP/s); at K = 5120 (fc2) the ping-pong wins (1171 vs 1146).
+// Routing: every 256x256 GEMM with K % 64 == 0, except the f32 residual read-modify-write at short
+// K (proj, K = 1280: one tile per CU, 20 K-steps), which goes to the interleaved kernel: it measured
+// 8 % faster than the plain ping-pong there (755 vs 692 TFLOP/s; the residual loads stall both wave
+// groups at the tile end) and 13 % faster than the residual-prefetch variant (52.4 vs 59.1 us,
+// MQ_TUNE_GEMM_PP_RESID_PREFETCH 1 routes proj there).  At K = 5120 (fc2) the plain ping-pong wins.
+int g_gemm_pp_resid_pf = 0;
+
 bool gemm_pingpong_fits(const GemmArgs& p, int epi) {
-  return g_gemm_pingpong && epi != EPI_NCHW_F32 && !(epi == EPI_RESID_F32 && p.K < 2048) && p.K > 0 &&
+  return g_gemm_pingpong && epi != EPI_NCHW_F32 && !(epi == EPI_RESID_F32 && p.K < 2048 && !g_gemm_pp_resid_pf) &&
+         p.K > 0 &&
          p.K % PP_BK == 0 &&
          (size_t)p.M * p.lda * 2 < (1ull << 31) && (size_t)p.N * p.ldw * 2 < (1ull << 31);
 }
@@ -612,7 +640,12 @@ int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
   switch (epi) {
     case EPI_BF16: launch_pp<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RESID_F32: launch_pp<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RESID_F32:
+      if (p.K < 2048 && (size_t)p.M * p.ldc * 4 < (1ull << 31))
+        launch_pp1<EPI_RESID_F32, 0, false, true>(grid, stream, p, tiles_m, tiles_n);
+      else
+        launch_pp<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n);
+      break;
     case EPI_POS_F32: launch_pp<EPI_POS_F32>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_F32: launch_pp<EPI_F32>(grid, stream, p, tiles_m, tiles_n); break;
     default: return -3;

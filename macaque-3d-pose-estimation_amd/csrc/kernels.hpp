@@ -39,6 +39,7 @@ extern bool g_gemm_force_small;
 extern int g_gemm_pingpong;
 extern int g_gemm_pp_ablate;
 extern int g_gemm_pp_dim;
+extern int g_gemm_pp_resid_pf;
 bool gemm_pingpong_fits(const GemmArgs& p, int epi);
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 

@@ -58,6 +58,11 @@ def main():
         ctx.lib.mq_set_tuning(12, 0)
         ctx.lib.mq_set_tuning(13, 0)
         ctx.lib.mq_set_tuning(14, 0)
+        ctx.lib.mq_set_tuning(16, 1)
+        if var == "pf0":  # short-K residual GEMMs back on the interleaved kernel
+            ctx.lib.mq_set_tuning(12, 1)
+            ctx.lib.mq_set_tuning(16, 0)
+            var_st = "4"
         if var == "pd":  # ping-pong, DMA issued inside the MFMA segment
             ctx.lib.mq_set_tuning(12, 1)
             ctx.lib.mq_set_tuning(14, 1)
