@@ -158,6 +158,17 @@ int mq_triangulate_ransac(mq_ctx* ctx, const double* cams, int n_cams, const dou
 int mq_triangulate_pinv(mq_ctx* ctx, const double* cams, int n_cams, const double* und, const uint8_t* use, int n,
                         double* out, void* stream);
 
+/* step-2 cross-view geometry affinity (geometry_affinity2, step2_crossviewmatching.py:373-432),
+ * batched over B frames:
+ *   points     : float64 (B, M, J, 3) undistorted x, y and keypoint score per detection
+ *   cam_of_det : int32 (B, M) camera index of each detection (its dimGroup slot), -1 = padding
+ *   affinity   : float64 (B, M, M); padding rows / columns are 0
+ * Rays through each keypoint at depth 0 and 1000 (deproject :327-355), mean line distance over the
+ * keypoints both detections score above thr_kp (THR_KP = 0.1) when at least 3 qualify, z-score over
+ * the frame's entries below 300, logistic(-5 z), 0 beyond 150. */
+int mq_geometry_affinity(mq_ctx* ctx, const double* cams, int n_cams, const double* points, const int32_t* cam_of_det,
+                         int B, int M, int J, double thr_kp, double* affinity, void* stream);
+
 /* filter_pose_viterbi over every (animal, camera, joint) chain of kp (A,F,C,J,3)
  * [x, y, score] (step 4 layout of kp2d.pickle) -> out (A,F,C,J,3).  Scratch is
  * owned by the context.  score_threshold 0.3, n_back 3, offset_threshold 25 in step 4. */

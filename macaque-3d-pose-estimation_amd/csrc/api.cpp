@@ -69,6 +69,7 @@ struct mq_ctx {
   DevBuf scratch;  // geometry scratch (Viterbi back-pointers)
   DevBuf decode_work;
   DevBuf optim_ws;
+  DevBuf assoc_ws;  // step-2 affinity: rays + pairwise distances
 };
 
 struct ParamSlot {
@@ -230,6 +231,8 @@ int mq_destroy(mq_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   ctx->scratch.release();
   ctx->decode_work.release();
+  ctx->optim_ws.release();
+  ctx->assoc_ws.release();
   delete ctx;
   return 0;
 }
@@ -751,6 +754,23 @@ int mq_triangulate_pinv(mq_ctx* ctx, const double* cams, int C, const double* un
   int rc = check_geo(ctx, cams, C, n);
   if (rc) return rc;
   K_TRY(mq::triangulate_pinv(cams, C, und, use, n, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_geometry_affinity(mq_ctx* ctx, const double* cams, int C, const double* points, const int32_t* cam_of_det,
+                         int B, int M, int J, double thr_kp, double* affinity, void* stream) {
+  int rc = check_geo(ctx, cams, C, B);
+  if (rc) return rc;
+  if (!points || !cam_of_det || !affinity) return fail("mq_geometry_affinity: null argument");
+  if (M < 0 || J < 0) return fail("mq_geometry_affinity: negative size", -2);
+  if ((int64_t)B * M == 0) return 0;
+  if ((int64_t)B * M * M > (int64_t)1 << 31 || (int64_t)B * M * J > (int64_t)1 << 28)
+    return fail("mq_geometry_affinity: batch too large", -2);
+  const size_t rays_b = ((size_t)B * M * J * 6 * 8 + 255) & ~(size_t)255;
+  if (ctx->assoc_ws.ensure(rays_b + (size_t)B * M * M * 8 + 256)) return fail("affinity workspace alloc failed", -5);
+  double* rays = ctx->assoc_ws.as<double>();
+  double* dist = reinterpret_cast<double*>(ctx->assoc_ws.as<char>() + rays_b);
+  K_TRY(mq::geometry_affinity(cams, C, points, cam_of_det, B, M, J, thr_kp, rays, dist, affinity, (hipStream_t)stream));
   return 0;
 }
 

@@ -146,6 +146,159 @@ __device__ __forceinline__ void dlt_point(const double* cams, int C, const doubl
   out[2] = v[2] / v[3];
 }
 
+
+// ------------------------------------------------------------------ step-2 geometry affinity
+// geometry_affinity2 (step2_crossviewmatching.py:373-432) batched over B frames of up to M detections
+// (cam_of_det < 0 marks padding).  Three launches: rays, pairwise mean ray distance, per-frame z-score
+// + logistic.  Operation order follows the reference (numpy), compiled without FMA contraction.
+
+// 3x3 inverse (adjugate / determinant) of the camera rotation: deproject uses np.linalg.inv(R).
+__device__ __forceinline__ void inv3(const double* R, double* Ri) {
+  const double c00 = R[4] * R[8] - R[5] * R[7], c01 = R[5] * R[6] - R[3] * R[8], c02 = R[3] * R[7] - R[4] * R[6];
+  const double det = R[0] * c00 + R[1] * c01 + R[2] * c02;
+  const double id = 1.0 / det;
+  Ri[0] = c00 * id;
+  Ri[1] = (R[2] * R[7] - R[1] * R[8]) * id;
+  Ri[2] = (R[1] * R[5] - R[2] * R[4]) * id;
+  Ri[3] = c01 * id;
+  Ri[4] = (R[0] * R[8] - R[2] * R[6]) * id;
+  Ri[5] = (R[2] * R[3] - R[0] * R[5]) * id;
+  Ri[6] = c02 * id;
+  Ri[7] = (R[1] * R[6] - R[0] * R[7]) * id;
+  Ri[8] = (R[0] * R[4] - R[1] * R[3]) * id;
+}
+
+// deproject (step2:327-355) at depth 0 and 1000: rays[b][i][k] = (near xyz, far xyz)
+__global__ void affinity_rays_kernel(const double* __restrict__ cams, int C, const double* __restrict__ pts,
+                                     const int32_t* __restrict__ cam_of_det, int BM, int J,
+                                     double* __restrict__ rays) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= BM * J) return;
+  const int det = idx / J;
+  const int c = cam_of_det[det];
+  double* r = rays + (size_t)idx * 6;
+  if (c < 0 || c >= C) {  // padding (an out-of-range camera index is treated as padding too)
+    for (int e = 0; e < 6; ++e) r[e] = 0.0;
+    return;
+  }
+  const CamParams& cp = cam_at(cams, c);
+  double Ri[9];
+  inv3(cp.R, Ri);
+  const double x = pts[(size_t)idx * 3], y = pts[(size_t)idx * 3 + 1];
+  const double dn[3] = {0.0 * x - cp.t[0], 0.0 * y - cp.t[1], 0.0 * 1.0 - cp.t[2]};
+  const double df[3] = {x * 1000.0 - cp.t[0], y * 1000.0 - cp.t[1], 1.0 * 1000.0 - cp.t[2]};
+#pragma unroll
+  for (int row = 0; row < 3; ++row) {
+    r[row] = (Ri[3 * row] * dn[0] + Ri[3 * row + 1] * dn[1]) + Ri[3 * row + 2] * dn[2];
+    r[3 + row] = (Ri[3 * row] * df[0] + Ri[3 * row + 1] * df[1]) + Ri[3 * row + 2] * df[2];
+  }
+}
+
+// calc_dist_btw_lines (step2:359-369)
+__device__ __forceinline__ double line_dist(const double* v1, const double* v2) {
+  double d1[3], d2[3];
+  const double a0 = v1[3] - v1[0], a1 = v1[4] - v1[1], a2 = v1[5] - v1[2];
+  const double b0 = v2[3] - v2[0], b1 = v2[4] - v2[1], b2 = v2[5] - v2[2];
+  const double na = sqrt((a0 * a0 + a1 * a1) + a2 * a2), nb = sqrt((b0 * b0 + b1 * b1) + b2 * b2);
+  d1[0] = a0 / na; d1[1] = a1 / na; d1[2] = a2 / na;
+  d2[0] = b0 / nb; d2[1] = b1 / nb; d2[2] = b2 / nb;
+  const double c0 = d1[1] * d2[2] - d1[2] * d2[1];
+  const double c1 = d1[2] * d2[0] - d1[0] * d2[2];
+  const double c2 = d1[0] * d2[1] - d1[1] * d2[0];
+  const double num = ((v2[0] - v1[0]) * c0 + (v2[1] - v1[1]) * c1) + (v2[2] - v1[2]) * c2;
+  return fabs(num) / sqrt((c0 * c0 + c1 * c1) + c2 * c2);
+}
+
+// pairwise mean ray distance; dist = -1 marks a padding pair (excluded from the statistics)
+__global__ void affinity_dist_kernel(const double* __restrict__ rays, const double* __restrict__ pts,
+                                     const int32_t* __restrict__ cam_of_det, int C, int B, int M, int J,
+                                     double thr_kp, double* __restrict__ dist) {
+  const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)B * M * M) return;
+  const int b = (int)(idx / ((int64_t)M * M));
+  const int i = (int)((idx / M) % M), j = (int)(idx % M);
+  const int ci = cam_of_det[b * M + i], cj = cam_of_det[b * M + j];
+  double d;
+  if (ci < 0 || cj < 0 || ci >= C || cj >= C) {
+    d = -1.0;
+  } else if (i == j) {
+    d = 0.0;
+  } else if (ci == cj) {
+    d = 300.0;
+  } else {
+    const int lo = i < j ? i : j, hi = i < j ? j : i;  // the reference fills (i, j) and (j, i) from i < j
+    const double* ri = rays + ((size_t)(b * M + lo) * J) * 6;
+    const double* rj = rays + ((size_t)(b * M + hi) * J) * 6;
+    const double* si = pts + ((size_t)(b * M + lo) * J) * 3;
+    const double* sj = pts + ((size_t)(b * M + hi) * J) * 3;
+    double sum = 0.0;
+    int cnt = 0;
+    for (int k = 0; k < J; ++k) {
+      if (si[k * 3 + 2] > thr_kp && sj[k * 3 + 2] > thr_kp) {
+        sum = sum + line_dist(ri + k * 6, rj + k * 6);
+        ++cnt;
+      }
+    }
+    d = cnt >= 3 ? sum / (double)cnt : 300.0;
+  }
+  dist[idx] = d;
+}
+
+// per frame: mean / std (two-pass, ddof 0) over the entries < 2*Dth2, logistic(-5 z), 0 where > Dth2
+__global__ __launch_bounds__(256) void affinity_norm_kernel(const double* __restrict__ dist, int M,
+                                                            double* __restrict__ out) {
+  const int b = blockIdx.x;
+  const double* d = dist + (size_t)b * M * M;
+  double* o = out + (size_t)b * M * M;
+  __shared__ double red[256];
+  __shared__ int redc[256];
+  double s = 0.0;
+  int c = 0;
+  for (int e = threadIdx.x; e < M * M; e += blockDim.x) {
+    const double v = d[e];
+    if (v >= 0.0 && v < 300.0) {
+      s += v;
+      ++c;
+    }
+  }
+  red[threadIdx.x] = s;
+  redc[threadIdx.x] = c;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[threadIdx.x] += red[threadIdx.x + w];
+      redc[threadIdx.x] += redc[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  const double mean = red[0] / (double)redc[0];
+  const int cnt = redc[0];
+  __syncthreads();
+  double q = 0.0;
+  for (int e = threadIdx.x; e < M * M; e += blockDim.x) {
+    const double v = d[e];
+    if (v >= 0.0 && v < 300.0) q += (v - mean) * (v - mean);
+  }
+  red[threadIdx.x] = q;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const double sd = sqrt(red[0] / (double)cnt);
+  for (int e = threadIdx.x; e < M * M; e += blockDim.x) {
+    const double v = d[e];
+    double a;
+    if (v < 0.0 || v > 150.0) {
+      a = 0.0;
+    } else {
+      const double z = -(v - mean) / sd;
+      a = 1.0 / (1.0 + exp(-5.0 * z));
+    }
+    o[e] = a;
+  }
+}
+
 // ------------------------------------------------------------------ kernels
 __global__ void undistort_kernel(const double* __restrict__ cams, int C, const double* __restrict__ pts,
                                  double* __restrict__ out, int N) {
@@ -588,6 +741,21 @@ int triangulate_pinv(const double* cams, int C, const double* und, const uint8_t
     hipLaunchKernelGGL(pinv_dlt_kernel<16>, dim3((N + 63) / 64), dim3(64), 0, s, cams, C, und, use, N, out);
   else
     return -2;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+
+int geometry_affinity(const double* cams, int C, const double* pts, const int32_t* cam_of_det, int B, int M, int J,
+                      double thr_kp, double* rays, double* dist, double* out, hipStream_t s) {
+  if (B <= 0 || M <= 0) return 0;
+  const int bmj = B * M * J;
+  if (bmj > 0)
+    hipLaunchKernelGGL(affinity_rays_kernel, dim3((bmj + 255) / 256), dim3(256), 0, s, cams, C, pts, cam_of_det,
+                       B * M, J, rays);
+  const int64_t pairs = (int64_t)B * M * M;
+  hipLaunchKernelGGL(affinity_dist_kernel, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0, s, rays, pts,
+                     cam_of_det, C, B, M, J, thr_kp, dist);
+  hipLaunchKernelGGL(affinity_norm_kernel, dim3(B), dim3(256), 0, s, dist, M, out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

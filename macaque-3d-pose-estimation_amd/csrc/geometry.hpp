@@ -13,6 +13,8 @@ int triangulate_ransac(const double* cams, int C, const double* pts, int N, int 
                        double* p3d, uint8_t* picked, double* p2d, double* err, hipStream_t s);
 int triangulate_pinv(const double* cams, int C, const double* und, const uint8_t* use, int N, double* out,
                      hipStream_t s);
+int geometry_affinity(const double* cams, int C, const double* pts, const int32_t* cam_of_det, int B, int M, int J,
+                      double thr_kp, double* rays, double* dist, double* out, hipStream_t s);
 int viterbi_filter(const double* kp, int A, int F, int C, int J, double score_thr, int n_back, double thres_dist,
                    int8_t* back_scratch, double* out, hipStream_t s);
 }  // namespace mq
