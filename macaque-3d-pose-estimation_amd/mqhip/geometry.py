@@ -90,7 +90,24 @@ class CameraGroup:
     # ------------------------------------------------------------------ construction
     @staticmethod
     def from_dicts(arr, device: int = 0):
-        return CameraGroup([OmnidirCamera.from_dict(d) for d in arr], device=device)
+        """cameras.py:1972-1982: the camera model is chosen per dict -- ``fisheye`` ->
+        FisheyeCamera, ``omnidir`` -> OmnidirCamera, otherwise the pinhole Camera.  The
+        reference pipeline only ever writes omnidir calibrations (step4:101-138,
+        configs/calibration_tmpl.toml:9), so only OmnidirCamera has HIP kernels; a fisheye or
+        pinhole dict raises instead of being run through the omnidir model."""
+        cams = []
+        for i, d in enumerate(arr):
+            if d.get("fisheye", False):
+                kind = "fisheye (FisheyeCamera)"
+            elif d.get("omnidir", False):
+                cams.append(OmnidirCamera.from_dict(d))
+                continue
+            else:
+                kind = "pinhole (Camera)"
+            raise NotImplementedError(
+                f"camera {d.get('name', i)!r} is a {kind} calibration: only omnidir cameras "
+                f"(omnidir = true, the model step 4 writes) are implemented on MI355X")
+        return CameraGroup(cams, device=device)
 
     @staticmethod
     def load(path, device: int = 0):
@@ -244,14 +261,15 @@ class CameraGroup:
                                  scale_length=2, scale_length_weak=0.5, reproj_error_threshold=15,
                                  reproj_loss='soft_l1', n_deriv_smooth=1, scores=None, verbose=False):
         """cameras.py:1192-1415: lengths fixed to joint_len, p3d only; the reference caps scipy at
-        max_nfev=15, mirrored here as at most 15 Levenberg-Marquardt steps."""
+        max_nfev=15 (the initial evaluation + 14 trial steps), mirrored here as at most 14
+        Levenberg-Marquardt trial steps."""
         from .optim import optim_points_gpu
         joint_len = np.asarray(joint_len, dtype=np.float64).ravel()
         p3, _ = optim_points_gpu(self, points, p3ds, constraints=constraints, constraints_weak=constraints_weak,
                                  scale_smooth=scale_smooth, scale_length=scale_length,
                                  scale_length_weak=scale_length_weak, reproj_error_threshold=reproj_error_threshold,
                                  reproj_loss=reproj_loss, n_deriv_smooth=n_deriv_smooth, scores=scores,
-                                 verbose=verbose, joint_len=joint_len, max_iter=15)
+                                 verbose=verbose, joint_len=joint_len, max_iter=14)
         return p3, joint_len
 
 

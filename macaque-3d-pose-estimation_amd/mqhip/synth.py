@@ -124,7 +124,8 @@ def make_cameras(n_cams: int = 8, seed_dist: int = 0, seed_ext: int = 1):
         tvec = -R @ C
         mtx = np.array([[mfx, 0.0, cx], [0.0, mfx, cy], [0.0, 0.0, 1.0]])
         cams.append(dict(name=cid, size=[IMG_W, IMG_H], K=K, xi=np.array([xi]), D=D,
-                         rvec=rvec, tvec=tvec, matrix=mtx, distortions=np.zeros(5)))
+                         rvec=rvec, tvec=tvec, matrix=mtx, distortions=np.zeros(5), fisheye=False,
+                         omnidir=True))
     return cams
 
 

@@ -261,6 +261,70 @@ class CameraGroupOracle:
         return self.triangulate_possible(points.reshape(n_cams, n_points, 1, 2),
                                          undistort=undistort, min_cams=min_cams)
 
+    def triangulate_ransac_batched(self, points, min_cams=2, threshold=0.5):
+        """Same result as ``triangulate_ransac`` (cameras.py:639-743, n_possible = 1), batched
+        for clip-sized inputs (config 4: 20,400 points x <= 247 subsets).
+
+        Points are grouped by their set of cameras with a non-NaN observation; within a group
+        every subset of ``itertools.product`` order is triangulated for all of the group's
+        points in one stacked ``np.linalg.svd`` call on exactly the (2k x 4) matrices of
+        ``triangulate_simple`` (no padding, so each SVD is the one the loop version computes).
+        The loop's selection rule -- keep a subset iff err < best (best starts at 200), stop
+        at the first best < threshold -- reduces to: the first subset with err < threshold,
+        else the first occurrence of the minimum error below 200 (NaN errors never win).
+        tests/test_oracle_kat.py checks it against ``triangulate_ransac`` pick for pick."""
+        C, N, _ = points.shape
+        assert C == len(self.cameras)
+        und = self.undistort(points)
+        mats = np.array([c.extrinsics_mat()[:3] for c in self.cameras])
+        out = np.full((N, 3), np.nan)
+        picked = np.zeros((C, N, 1), dtype=bool)
+        errors = np.zeros(N)
+        p2 = np.full((C, N, 2), np.nan)
+        present = ~np.isnan(points[:, :, 0])                       # (C, N)
+        codes = (present.astype(np.int64) << np.arange(C)[:, None]).sum(0)
+        for code in np.unique(codes):
+            ips = np.flatnonzero(codes == code)
+            cams_p = [c for c in range(C) if (code >> c) & 1]
+            n = len(cams_p)
+            if n < 2:
+                continue    # 0 or 1 camera: p3d NaN, error stays 0 (cameras.py:675)
+            errs, p3s, subsets = [], [], []
+            for s in range(1 << n):
+                sub = [cams_p[i] for i in range(n) if not (s >> (n - 1 - i)) & 1]
+                k = len(sub)
+                if (k < min_cams and k != n) or k < 2:
+                    continue
+                x = und[sub][:, ips]                                 # (k, P, 2)
+                A = np.empty((len(ips), 2 * k, 4))
+                for i, c in enumerate(sub):
+                    A[:, 2 * i] = x[i, :, 0:1] * mats[c, 2] - mats[c, 0]
+                    A[:, 2 * i + 1] = x[i, :, 1:2] * mats[c, 2] - mats[c, 1]
+                vh = np.linalg.svd(A, full_matrices=True)[2]
+                p3 = vh[:, -1, :3] / vh[:, -1, 3:4]
+                en = np.stack([np.linalg.norm(points[c, ips] - self.cameras[c].project(p3), axis=1)
+                               for c in sub], axis=1)                # (P, k)
+                # per point: the loop version's np.sum over its (k, 1) error column
+                errs.append(np.sum(en, axis=1) / float(k))
+                p3s.append(p3)
+                subsets.append(sub)
+            E = np.array(errs)                                       # (S, P)
+            Ef = np.where(np.isnan(E), np.inf, E)
+            hit = Ef < threshold
+            first_hit = np.argmax(hit, axis=0)
+            best = np.argmin(Ef, axis=0)
+            sel = np.where(hit.any(axis=0), first_hit, best)
+            ok = Ef[sel, np.arange(len(ips))] < 200
+            for j, ip in enumerate(ips):
+                if not ok[j]:
+                    continue
+                s = sel[j]
+                out[ip] = p3s[s][j]
+                errors[ip] = E[s, j]
+                picked[subsets[s], ip, 0] = True
+                p2[subsets[s], ip] = points[subsets[s], ip]
+        return out, picked, p2, errors
+
     # ------------------------------------------------------------------ optim_points
     def _error_fun_triangulation(self, params, p2ds, constraints, constraints_weak,
                                  scale_smooth, scale_length, scale_length_weak,
@@ -295,6 +359,20 @@ class CameraGroupOracle:
             elw[cix] = 100 * (lengths - jlw[cix]) / jlw[cix]
         elw = elw.ravel() * scale_length_weak
         return np.hstack([errors_reproj, errors_smooth, el, elw])
+
+    def _error_fun_triangulation_jointlenfix(self, params, p2ds, joint_len, constraints, constraints_weak,
+                                             scale_smooth, scale_length, scale_length_weak,
+                                             reproj_error_threshold, reproj_loss, n_deriv_smooth):
+        """cameras.py:1355-1415: params = p3d only; the lengths are the fixed ``joint_len``
+        (strong first, then weak).  Otherwise the residual set of _error_fun_triangulation."""
+        n_cams, n_frames, n_joints, _ = p2ds.shape
+        n_3d = n_frames * n_joints * 3
+        n_c = len(constraints)
+        jl = np.asarray(joint_len, dtype=np.float64)
+        x = np.hstack([np.asarray(params, dtype=np.float64)[:n_3d], jl[:n_c], jl[n_c:]])
+        return self._error_fun_triangulation(x, p2ds, constraints, constraints_weak, scale_smooth,
+                                             scale_length, scale_length_weak, reproj_error_threshold,
+                                             reproj_loss, n_deriv_smooth)
 
 
 def medfilt_data(values, size=15):
@@ -409,6 +487,43 @@ def optim_points(cgroup, points, p3ds, constraints=(), constraints_weak=(), scal
               scale_length_weak, reproj_error_threshold, reproj_loss, n_deriv_smooth))
     p3ds_new = res.x[:p3ds.size].reshape(p3ds.shape)
     joint_len = res.x[p3ds.size:]
+    if return_result:
+        return p3ds_new, joint_len, res, scale_smooth_full, x0
+    return p3ds_new, joint_len
+
+
+def jac_sparsity_triangulation_jointlenfix(p2ds, constraints, constraints_weak, n_deriv_smooth=1):
+    """cameras.py:1272-1352: the pattern of jac_sparsity_triangulation without the length
+    columns (n_params = F*J*3; length residuals depend on the two joints' points only)."""
+    A = jac_sparsity_triangulation(p2ds, constraints, constraints_weak, n_deriv_smooth)
+    n_cams, n_frames, n_joints, _ = p2ds.shape
+    return A.tocsr()[:, :n_frames * n_joints * 3]
+
+
+def optim_points_jointlenfix(cgroup, points, p3ds, joint_len, constraints=(), constraints_weak=(),
+                             scale_smooth=4, scale_length=2, scale_length_weak=0.5,
+                             reproj_error_threshold=15, reproj_loss='soft_l1', n_deriv_smooth=1,
+                             ftol=1e-3, max_nfev=15, return_result=False):
+    """cameras.py:1192-1270 -- scipy TRF on p3d only (lengths fixed to ``joint_len``),
+    ftol 1e-3 and **max_nfev = 15** as in the reference."""
+    n_cams, n_frames, n_joints, _ = points.shape
+    assert n_cams == len(cgroup.cameras)
+    constraints = np.array(constraints)
+    constraints_weak = np.array(constraints_weak)
+    p3ds_intp = np.apply_along_axis(interpolate_data, 0, p3ds)
+    p3ds_med = np.apply_along_axis(medfilt_data, 0, p3ds_intp, size=7)
+    default_smooth = 1.0 / np.mean(np.abs(np.diff(p3ds_med, axis=0)))
+    scale_smooth_full = scale_smooth * default_smooth
+    x0 = initialize_params_triangulation(p3ds_intp, constraints, constraints_weak)
+    x0[~np.isfinite(x0)] = 0
+    x0 = x0[:p3ds.size]
+    jac = jac_sparsity_triangulation_jointlenfix(points, constraints, constraints_weak, n_deriv_smooth)
+    res = optimize.least_squares(
+        cgroup._error_fun_triangulation_jointlenfix, x0=x0, jac_sparsity=jac, loss='linear', ftol=ftol,
+        max_nfev=max_nfev,
+        args=(points, joint_len, constraints, constraints_weak, scale_smooth_full, scale_length,
+              scale_length_weak, reproj_error_threshold, reproj_loss, n_deriv_smooth))
+    p3ds_new = res.x[:p3ds.size].reshape(p3ds.shape)
     if return_result:
         return p3ds_new, joint_len, res, scale_smooth_full, x0
     return p3ds_new, joint_len

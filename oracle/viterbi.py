@@ -131,3 +131,80 @@ def step4_filter(kp2d):
             pf = wrap_points(pf, sf)
             kp2d_f[:, :, a, :, c] = np.squeeze(pf)
     return kp2d_f
+
+
+def viterbi_paths_batched(points, scores, n_back=3, thres_dist=30):
+    """``viterbi_path`` (filter_pose.py:48-120) for N independent single-candidate chains at once.
+
+    points (N, F, 2) with NaN for missing (already score-thresholded), scores (N, F).  With one
+    candidate per frame ``remove_dups`` never pairs two points (candidates of different frames sit
+    >= 100 apart in its time coordinate), so it is the identity here.  Every chain runs the loop
+    version's arithmetic on the same values: the same particles (frames i, i-1, ..., score * 2^-j,
+    or the (-1, -1, 0.001) placeholder), the same scipy ``norm.logcdf`` / ``logsumexp`` calls on the
+    same distances, the same clamps, and first-index max / argmax rules; padding slots of chains
+    with fewer particles are masked to -inf so they never win.  tests/test_oracle_kat.py checks it
+    against the loop version (``step4_filter``) value for value."""
+    N, F, _ = points.shape
+    K = n_back
+    good = ~np.isnan(points[:, :, 0])
+    part = np.zeros((N, F, K, 3))
+    valid = np.zeros((N, F), dtype=np.int64)
+    for i in range(F):
+        s = np.zeros(N, dtype=np.int64)
+        for j in range(n_back):
+            if i - j < 0:
+                break
+            g = good[:, i - j]
+            idx = np.flatnonzero(g)
+            part[idx, i, s[idx], :2] = points[idx, i - j]
+            part[idx, i, s[idx], 2] = scores[idx, i - j] * np.power(2.0, -j)
+            s += g
+        none = s == 0
+        part[none, i, 0] = [-1, -1, 0.001]
+        s[none] = 1
+        valid[:, i] = s
+    slot = np.arange(K)
+    T = np.full((N, F, K), -np.inf)
+    back = np.zeros((N, F, K), dtype=np.int64)
+    ok0 = slot[None, :] < valid[:, 0:1]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        T[:, 0] = np.where(ok0, np.log(np.where(ok0, part[:, 0, :, 2], 1.0)), -np.inf)
+    for i in range(1, F):
+        pa = part[:, i - 1, :, :2]                                   # (N, K, 2)
+        pb = part[:, i, :, :2]
+        diff = pb[:, :, None, :] - pa[:, None, :, :]                 # (N, Kb, Ka, 2): cdist(pa, pb).T
+        d = np.sqrt(diff[..., 0] * diff[..., 0] + diff[..., 1] * diff[..., 1])
+        cdf_high = stats.norm.logcdf(d + 2, scale=thres_dist)
+        cdf_low = stats.norm.logcdf(d - 2, scale=thres_dist)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            P = logsumexp(np.stack([cdf_high, cdf_low], axis=-1), b=[1, -1], axis=-1)
+        P[P < -100] = -100
+        P = np.where((pb[:, :, 0] == -1)[:, :, None], np.log(0.001), P)
+        P = np.where((pa[:, :, 0] == -1)[:, None, :], np.log(0.001), P)
+        va = slot[None, :] < valid[:, i - 1:i]                       # (N, Ka)
+        vb = slot[None, :] < valid[:, i:i + 1]                       # (N, Kb)
+        possible = np.where(va[:, None, :], T[:, i - 1][:, None, :] + P, -np.inf)
+        m = np.max(possible, axis=2)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            T[:, i] = np.where(vb, m + np.log(np.where(vb, part[:, i, :, 2], 1.0)), -np.inf)
+        back[:, i] = np.where(vb, np.argmax(possible, axis=2), 0)
+    out = np.zeros((N, F), dtype=np.int64)
+    out[:, -1] = np.argmax(T[:, -1], axis=1)
+    for i in range(F - 1, 0, -1):
+        out[:, i - 1] = back[np.arange(N), i, out[:, i]]
+    trace = part[np.arange(N)[:, None], np.arange(F)[None, :], out]  # (N, F, 3)
+    return trace[..., :2], trace[..., 2]
+
+
+def step4_filter_batched(kp2d, config=STEP4_FILTER_CONFIG):
+    """``step4_filter`` with every (animal, camera, joint) chain in one batched Viterbi: the
+    clip-sized (config 4: 544 chains x 300 frames) form used by the parity tests."""
+    kp = np.array(kp2d, dtype=np.float64, copy=True)                 # (A, F, C, J, 3)
+    A, F, C, J, _ = kp.shape
+    ch = kp.transpose(0, 2, 3, 1, 4).reshape(-1, F, 3)              # (A*C*J, F, 3)
+    pts = ch[..., :2].copy()
+    sc = ch[..., 2].copy()
+    pts[sc < config['filter']['score_threshold']] = np.nan
+    p, s = viterbi_paths_batched(pts, sc, config['filter']['n_back'], config['filter']['offset_threshold'])
+    out = np.concatenate([p, s[..., None]], axis=-1).reshape(A, C, J, F, 3)
+    return np.ascontiguousarray(out.transpose(3, 2, 0, 4, 1))       # (F, J, A, 3, C)

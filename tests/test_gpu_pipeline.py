@@ -191,3 +191,119 @@ def test_step1_multiview_batch_matches_per_view(tmp_path):
     assert os.path.exists(tmp_path / "cam0" / "alldata.json") and len(out) == 3
     assert np.load(tmp_path / "cam0" / "frame_num.npy").tolist() == [0, 1, 2]
     torch.cuda.synchronize()
+
+
+def _template(tmp_path, **tri):
+    """A copy of configs/config_tmpl.toml with [triangulation] keys overridden (how a reference
+    user switches step 4 to RANSAC: by editing the template, step4:102)."""
+    from mqhip import io as mqio
+    from src.pipeline import step4_aniposefiltering as step4
+    conf = mqio.load_toml(step4.CONFIG_TMPL)
+    conf["triangulation"].update(tri)
+    p = tmp_path / "config_tmpl.toml"
+    mqio.dump_toml(conf, str(p))
+    return str(p)
+
+
+def _oracle_scores_errors(o, kp_a, p3):
+    C, F, J, _ = kp_a.shape
+    p2 = kp_a[..., :2].copy()
+    sc = kp_a[..., 2].copy()
+    p2[sc < 0.5] = np.nan
+    good = ~np.isnan(p2[..., 0])
+    s = sc.copy()
+    s[~good] = 2
+    s3 = s.min(axis=0)
+    s3[good.sum(0) < 1] = np.nan
+    err = o.reprojection_error(p3.reshape(-1, 3), p2.reshape(C, -1, 2), mean=True).reshape(F, J)
+    err[good.sum(0) < 1] = np.nan
+    return p2, s3, err
+
+
+def test_step4_proc_config4_ransac_then_optim(tmp_path, monkeypatch):
+    """BASELINE config 4 end to end: a 300-frame clip, 8 views x 4 individuals x 17 joints through
+    step4.proc with ransac = true, optim = true (step4:228-291: Viterbi -> triangulate_ransac
+    (min_cams 2) -> optim_points -> reprojection error / scores).  Oracle composition: the batched
+    Viterbi and RANSAC restatements (pinned bit-for-bit to the loop restatements on CPU) and scipy
+    TRF with the reference's arguments per animal.  Tolerances: kp2d_f identical; RANSAC picks
+    identical, p3d/err 1e-6; kp3d within 1 mm median / 5 mm p99 of scipy (SURVEY 8(d) floor) and
+    no worse in cost than scipy + 0.1 %; scores exact; reprojection errors 1e-6 px."""
+    from mqhip import io as mqio
+    from mqhip import synth
+    from mqhip.geometry import CameraGroup
+    from oracle.geometry import CameraGroupOracle, optim_points
+    from oracle.viterbi import step4_filter_batched
+    from src.pipeline import step4_aniposefiltering as step4
+    cams, kp2d, root, cfg = _results_dir(tmp_path, A=4, F=300)
+    monkeypatch.setattr(step4, "CONFIG_TMPL", _template(tmp_path, ransac=True, optim=True))
+    step4.proc("demo", root, cfg, 17, redo=True)
+    rd = os.path.join(root, "demo")
+    got = mqio.load_array_pickle(os.path.join(rd, "kp3d.pickle"))
+    kp2d_f = mqio.load_array_pickle(os.path.join(rd, "kp2d_f.pickle"))
+    ref_f = step4_filter_batched(kp2d)
+    np.testing.assert_array_equal(kp2d_f, ref_f)
+    o = CameraGroupOracle(cams)
+    g = CameraGroup.from_dicts(cams)
+    cons = synth.constraint_indices(synth.CONSTRAINTS)
+    weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
+    kp = ref_f.transpose((2, 4, 0, 1, 3))                               # (A, C, F, J, 3)
+    A, C, F, J, _ = kp.shape
+    pts = kp[..., :2].copy()
+    pts[kp[..., 2] < 0.5] = np.nan
+    flat = np.ascontiguousarray(pts.transpose(1, 0, 2, 3, 4).reshape(C, -1, 2))
+    ro = o.triangulate_ransac_batched(flat, min_cams=2)
+    rg = g.triangulate_ransac(flat, min_cams=2)
+    np.testing.assert_array_equal(rg[1], ro[1])                          # picked subsets
+    np.testing.assert_allclose(rg[0], ro[0], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(rg[3], ro[3], rtol=0, atol=1e-6)
+    init = ro[0].reshape(A, F, J, 3)
+    for a in range(A):
+        p2, s3, _ = _oracle_scores_errors(o, kp[a], init[a])
+        sa = optim_points(o, p2, init[a], cons, weak, ftol=1e-3, return_result=True, **TRI)
+        dev = np.linalg.norm(got["kp3d"][a] - sa[0], axis=-1)
+        assert np.median(dev) <= 1.0 and np.percentile(dev, 99) <= 5.0, (a, np.median(dev),
+                                                                           np.percentile(dev, 99))
+        cg = 0.5 * np.sum(o._error_fun_triangulation(
+            np.hstack([got["kp3d"][a].ravel(), got["joint_len"][a]]), p2, np.array(cons), np.array(weak), sa[3],
+            TRI["scale_length"], TRI["scale_length_weak"], TRI["reproj_error_threshold"], "soft_l1",
+            TRI["n_deriv_smooth"]) ** 2)
+        assert cg <= sa[2].cost * (1 + 1e-3), (a, cg, sa[2].cost)
+        _, s3, err = _oracle_scores_errors(o, kp[a], got["kp3d"][a])
+        np.testing.assert_array_equal(got["kp3d_score"][a], s3)
+        np.testing.assert_allclose(got["kp3d_err"][a], err, rtol=0, atol=1e-6)
+    assert len(got["joint_len"]) == A
+
+
+def test_step4_proc_fixed_joint_lengths(tmp_path):
+    """calib/joint_len.npy present -> optim_points_jointlenfix with its median (step4:179-183,
+    259-270) and kp3d_fxdJointLen.pickle (:334-336), vs scipy TRF at max_nfev = 15."""
+    from mqhip import io as mqio
+    from mqhip import synth
+    from oracle.geometry import CameraGroupOracle, optim_points_jointlenfix
+    from oracle.viterbi import step4_filter_batched
+    from src.pipeline import step4_aniposefiltering as step4
+    cams, kp2d, root, cfg = _results_dir(tmp_path, A=2, F=40)
+    skel = synth.make_skeletons(2, 40)
+    cons = synth.constraint_indices(synth.CONSTRAINTS)
+    weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
+    jl_runs = np.array([[np.median(np.linalg.norm(skel[a][:, i] - skel[a][:, j], axis=1)) for i, j in cons + weak]
+                        for a in range(2)])
+    np.save(os.path.join(os.path.dirname(cfg), "joint_len.npy"), jl_runs)
+    step4.proc("demo", root, cfg, 17, redo=True)
+    rd = os.path.join(root, "demo")
+    assert not os.path.exists(os.path.join(rd, "kp3d.pickle"))
+    got = mqio.load_array_pickle(os.path.join(rd, "kp3d_fxdJointLen.pickle"))
+    jl = np.median(jl_runs, axis=0)
+    o = CameraGroupOracle(cams)
+    kp = step4_filter_batched(kp2d).transpose((2, 4, 0, 1, 3))
+    for a in range(2):
+        np.testing.assert_array_equal(got["joint_len"][a], jl)
+        p2, _, _ = _oracle_scores_errors(o, kp[a], np.zeros((40, 17, 3)))
+        init = o.triangulate(p2.reshape(8, -1, 2)).reshape(40, 17, 3)
+        sa = optim_points_jointlenfix(o, p2, init, jl, cons, weak, ftol=1e-3, max_nfev=15, return_result=True,
+                                      **TRI)
+        dev = np.linalg.norm(got["kp3d"][a] - sa[0], axis=-1)
+        assert np.median(dev) <= 1.0 and np.percentile(dev, 99) <= 5.0, (a, np.median(dev))
+        _, s3, err = _oracle_scores_errors(o, kp[a], got["kp3d"][a])
+        np.testing.assert_array_equal(got["kp3d_score"][a], s3)
+        np.testing.assert_allclose(got["kp3d_err"][a], err, rtol=0, atol=1e-6)

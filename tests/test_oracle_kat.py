@@ -172,3 +172,69 @@ def test_optim_points_oracle_reduces_cost():
     assert res.cost < 0.5 * np.sum(r0 ** 2)
     assert jl.shape == (31,) and np.isfinite(p3).all()
     assert np.nanmedian(np.linalg.norm(p3 - skel[0], axis=-1)) < 10.0
+
+
+@pytest.mark.parametrize("min_cams", [2, 3])
+def test_batched_ransac_oracle_equals_loop_oracle(min_cams):
+    """triangulate_ransac_batched (used for clip-sized parity, config 4) returns exactly what the
+    loop restatement of cameras.py:639-743 returns: same picks, same p3d / errors bit for bit,
+    including points seen by 0, 1 or 2 cameras."""
+    from mqhip import synth
+    from oracle.geometry import CameraGroupOracle
+    cams = synth.make_cameras(8)
+    kp2d = synth.make_kp2d(cams, synth.make_skeletons(2, 3), noise_px=2.0, drop=0.35, seed=7)
+    pts = kp2d[..., :2].copy()
+    pts[kp2d[..., 2] < 0.5] = np.nan
+    flat = np.ascontiguousarray(pts.transpose(2, 0, 1, 3, 4).reshape(8, -1, 2))
+    flat[:, 0] = np.nan
+    flat[1:, 1] = np.nan
+    flat[2:, 2] = np.nan
+    o = CameraGroupOracle(cams)
+    loop = o.triangulate_ransac(flat, min_cams=min_cams)
+    fast = o.triangulate_ransac_batched(flat, min_cams=min_cams)
+    for a, b in zip(loop, fast):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_jointlenfix_oracle_residual_and_nfev_cap():
+    """cameras.py:1192-1415: the fixed-length residual is the free one with the lengths pinned,
+    the sparsity drops the length columns, and scipy stops at max_nfev = 15."""
+    from mqhip import synth
+    from oracle.geometry import (CameraGroupOracle, jac_sparsity_triangulation_jointlenfix,
+                                 optim_points_jointlenfix)
+    cams = synth.make_cameras(8)
+    skel = synth.make_skeletons(1, 20)
+    kp2d = synth.make_kp2d(cams, skel, noise_px=2.0, drop=0.1)
+    o = CameraGroupOracle(cams)
+    pts = kp2d[0].transpose(1, 0, 2, 3)
+    p2 = pts[..., :2].copy()
+    p2[pts[..., 2] < 0.5] = np.nan
+    init = o.triangulate(p2.reshape(8, -1, 2)).reshape(20, 17, 3)
+    cons = synth.constraint_indices(synth.CONSTRAINTS)
+    weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
+    jl = np.linspace(50, 300, len(cons) + len(weak))
+    x = init.ravel().copy()
+    x[~np.isfinite(x)] = 0
+    r_fix = o._error_fun_triangulation_jointlenfix(x, p2, jl, np.array(cons), np.array(weak), 2.0, 5, 2, 3,
+                                                   'soft_l1', 2)
+    r_free = o._error_fun_triangulation(np.hstack([x, jl]), p2, np.array(cons), np.array(weak), 2.0, 5, 2, 3,
+                                        'soft_l1', 2)
+    np.testing.assert_array_equal(r_fix, r_free)
+    A = jac_sparsity_triangulation_jointlenfix(p2, np.array(cons), np.array(weak), 2)
+    assert A.shape == (len(r_fix), x.size)
+    p3, jl_out, res, ssf, x0 = optim_points_jointlenfix(o, p2, init, jl, cons, weak, scale_smooth=3,
+                                                        scale_length=5, scale_length_weak=2, n_deriv_smooth=2,
+                                                        reproj_error_threshold=3, max_nfev=3, ftol=1e-12,
+                                                        return_result=True)
+    assert res.nfev <= 3 and jl_out is jl and p3.shape == init.shape
+
+
+def test_batched_viterbi_oracle_equals_loop_oracle():
+    """step4_filter_batched (clip-sized parity, config 4) == the loop restatement of
+    filter_pose.py:48-186 as driven by step4:142-167, value for value (gaps, placeholders)."""
+    from mqhip import synth
+    from oracle.viterbi import step4_filter, step4_filter_batched
+    cams = synth.make_cameras(8)
+    kp2d = synth.make_kp2d(cams, synth.make_skeletons(2, 30), noise_px=6.0, drop=0.45, seed=11)
+    kp2d[0, 5:12, 3] = 0          # a camera loses animal 0 for 7 frames
+    np.testing.assert_array_equal(step4_filter(kp2d), step4_filter_batched(kp2d))
