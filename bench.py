@@ -46,51 +46,187 @@ def parse():
     ap.add_argument("--model", default="huge", choices=["huge", "base", "tiny"])
     ap.add_argument("--resident-frames", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-lift", action="store_true", help="skip the config-4 lift timing (extra keys)")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a hipGraph (disables live timing)")
     return ap.parse_args()
 
 
-def cpu_baseline(cfg, cams_np, n_crops_sample=2):
-    """Oracle (CPU restatement) timed on this host: ViT fp32 flip + decode for a sample of
-    the frame's crops, extrapolated to the frame's 32 crops, + the frame's DLT."""
+def cpu_info():
+    """Host cores this process may use (what `nproc` reports) and the CPU model (`lscpu`)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": len(os.sched_getaffinity(0)), "os_cpu_count": os.cpu_count(), "model": model}
+
+
+def _median_time(fn, reps):
+    import numpy as np
+    fn()  # warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
+    """The build's CPU restatement of the reference path (oracle/, "port"), timed on this host per
+    BASELINE.md's plan: torch fp32 with one thread per available core, median of `reps` runs after
+    a warm-up.  Config 2 (the headline): ViT-H flip-test forward + UDP decode of `n_crops_sample` of
+    the frame's 32 crops (scaled by 32 / sample) + the frame's omnidir DLT.  Config 1: ViT-B on its
+    4 crops + decode + DLT, whole.  Config 4: the step-4 lift of the 300-frame clip (batched
+    Viterbi and RANSAC restatements, scipy optim_points on one animal scaled x4, reprojection)."""
     import numpy as np
     import torch
     from mqhip import synth
-    from mqhip.weights import make_random_weights
+    from mqhip.weights import CONFIGS, make_random_weights
     from oracle.decode import decode_batch
     from oracle.geometry import CameraGroupOracle
     from oracle.vitpose import forward_flip_test
-    threads = min(16, os.cpu_count() or 1)
+    info = cpu_info()
+    threads = info["nproc"]
     torch.set_num_threads(threads)
-    w = make_random_weights(cfg, seed=0, device="cpu")
-    x = torch.randn((n_crops_sample, 3, 256, 192))
-    with torch.no_grad():
-        forward_flip_test(x[:1], w, cfg)  # warm-up
-        t0 = time.perf_counter()
-        hm, _, _ = forward_flip_test(x, w, cfg)
-        t_vit = time.perf_counter() - t0
-    hm = hm.numpy()
-    c = np.tile(np.array([[800, 600]], np.float32), (n_crops_sample, 1))
-    s = np.tile(np.array([[300, 400]], np.float32), (n_crops_sample, 1))
-    t0 = time.perf_counter()
-    decode_batch(hm, c, s)
-    t_dec = time.perf_counter() - t0
-    skel = synth.make_skeletons(N_ANIMALS, 1)
-    kp2d = synth.make_kp2d(cams_np, skel)
-    pts = kp2d[:, 0].transpose(1, 0, 2, 3).reshape(N_VIEWS, -1, 3)
-    p = pts[..., :2].copy()
-    p[pts[..., 2] < TRI_THR] = np.nan
     g = CameraGroupOracle(cams_np)
+
+    def frame_pass(cfg, n_crops, n_views):
+        w = make_random_weights(cfg, seed=0, device="cpu")
+        x = torch.randn((n_crops, 3, 256, 192), generator=torch.Generator().manual_seed(0))
+        c = np.tile(np.array([[800, 600]], np.float32), (n_crops, 1))
+        s = np.tile(np.array([[300, 400]], np.float32), (n_crops, 1))
+        skel = synth.make_skeletons(N_ANIMALS, 1)
+        kp2d = synth.make_kp2d(cams_np, skel)
+        pts = kp2d[:, 0].transpose(1, 0, 2, 3)[:n_views].reshape(n_views, -1, 3)
+        p = pts[..., :2].copy()
+        p[pts[..., 2] < TRI_THR] = np.nan
+        gv = g.subset(range(n_views))
+
+        def run():
+            with torch.no_grad():
+                hm, _, _ = forward_flip_test(x, w, cfg)
+            decode_batch(hm.numpy(), c, s)
+            return hm
+
+        t_vit, _ = _median_time(run, reps)
+        t_tri, _ = _median_time(lambda: gv.triangulate(p), reps)
+        return t_vit, t_tri
+
+    crops = N_VIEWS * N_ANIMALS
+    t2, tri2 = frame_pass(CONFIGS["huge"], n_crops_sample, N_VIEWS)
+    t_frame2 = t2 * crops / n_crops_sample + tri2
+    t1, tri1 = frame_pass(CONFIGS["base"], 4, 4)
+    lift = lift_cpu(cams_np)
+    return {"value": round(N_ANIMALS / t_frame2, 5), "unit": "individuals×frames/s", "cores": threads,
+            "kind": "port", "nproc": info["nproc"], "os_cpu_count": info["os_cpu_count"], "cpu_model": info["model"],
+            "statistic": f"median of {reps} after 1 warm-up",
+            "sample": f"config 2: oracle ViT-H fp32 flip-test forward + UDP decode of {n_crops_sample} of the frame's "
+                      f"{crops} crops (x{crops / n_crops_sample:g}) + omnidir DLT of the frame's "
+                      f"{N_ANIMALS}x{N_JOINTS} joints; torch CPU {threads} threads",
+            "seconds_per_frame": round(t_frame2, 4),
+            "config1": {"seconds_per_frame": round(t1 + tri1, 4), "individuals_frames_per_s": round(1.0 / (t1 + tri1), 4),
+                        "sample": "ViT-B fp32 flip-test forward + decode of 4 crops (4 views x 1 individual) + DLT"},
+            "config4_lift": lift}
+
+
+def lift_inputs(A=4, F=300, C=8, seed=2):
+    import numpy as np
+    from mqhip import synth
+    cams = synth.make_cameras(C)
+    kp2d = synth.make_kp2d(cams, synth.make_skeletons(A, F, seed=seed), noise_px=2.0, drop=0.1)
+    return cams, kp2d
+
+
+LIFT_ARGS = dict(scale_smooth=3, scale_length=5, scale_length_weak=2, n_deriv_smooth=2, reproj_error_threshold=3)
+
+
+def lift_cpu(cams_np):
+    """Config-4 step-4 lift on the CPU restatement (oracle/): wall seconds per stage."""
+    import numpy as np
+    from mqhip import synth
+    from oracle.geometry import CameraGroupOracle, optim_points
+    from oracle.viterbi import step4_filter_batched
+    cams, kp2d = lift_inputs()
+    A, F, C, J, _ = kp2d.shape
+    o = CameraGroupOracle(cams)
+    cons = synth.constraint_indices(synth.CONSTRAINTS)
+    weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
+    t = {}
     t0 = time.perf_counter()
-    g.triangulate(p)
-    t_tri = time.perf_counter() - t0
-    crops_per_frame = N_VIEWS * N_ANIMALS
-    t_frame = (t_vit + t_dec) * crops_per_frame / n_crops_sample + t_tri
-    return {"value": N_ANIMALS / t_frame, "unit": "individuals×frames/s", "cores": threads, "kind": "port",
-            "sample": f"ViT-{cfg.name} fp32 flip-test forward + UDP decode of {n_crops_sample} of the frame's "
-                      f"{crops_per_frame} crops (x{crops_per_frame // n_crops_sample} extrapolated) + omnidir DLT "
-                      f"of the frame's {N_ANIMALS}x{N_JOINTS} joints; torch CPU {threads} threads",
-            "seconds_per_frame": t_frame}
+    kf = step4_filter_batched(kp2d).transpose((2, 4, 0, 1, 3))           # (A, C, F, J, 3)
+    t["viterbi_a15"] = time.perf_counter() - t0
+    pts = kf[..., :2].copy()
+    pts[kf[..., 2] < 0.5] = np.nan
+    flat = np.ascontiguousarray(pts.transpose(1, 0, 2, 3, 4).reshape(C, -1, 2))
+    t0 = time.perf_counter()
+    p3, _, _, _ = o.triangulate_ransac_batched(flat, min_cams=2)
+    t["ransac_a13"] = time.perf_counter() - t0
+    init = p3.reshape(A, F, J, 3)
+    t0 = time.perf_counter()
+    r0 = optim_points(o, pts[0], init[0], cons, weak, **LIFT_ARGS)
+    t["optim_points_a16"] = (time.perf_counter() - t0) * A
+    t0 = time.perf_counter()
+    o.reprojection_error(np.ascontiguousarray(np.tile(r0[0], (A, 1, 1, 1)).reshape(-1, 3)), flat, mean=True)
+    t["reproj_a14"] = time.perf_counter() - t0
+    tot = sum(t.values())
+    return {"seconds": {k: round(v, 4) for k, v in t.items()}, "total_s": round(tot, 4),
+            "individuals_frames_per_s": round(A * F / tot, 3), "cores": 1, "kind": "port",
+            "sample": f"{F} frames x {C} views x {A} individuals x {J} joints; batched numpy Viterbi / RANSAC "
+                      f"restatements (pinned equal to the loop restatements), scipy least_squares optim_points on "
+                      f"animal 0 scaled x{A}"}
+
+
+def lift_gpu(device, reps=3):
+    """Config-4 step-4 lift on the GPU (HIP kernels through the drop-in API, numpy in / out):
+    Viterbi over the 544 chains, RANSAC (min_cams 2) over 20,400 points, batched optim_points over
+    the 4 animals, mean reprojection error.  Median wall ms per stage over `reps` runs."""
+    import numpy as np
+    import torch
+    from mqhip import synth
+    from mqhip.geometry import CameraGroup, viterbi_filter
+    from mqhip.optim import optim_points_batch
+    cams, kp2d = lift_inputs()
+    A, F, C, J, _ = kp2d.shape
+    g = CameraGroup.from_dicts(cams, device=device)
+    cons = synth.constraint_indices(synth.CONSTRAINTS)
+    weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
+    times = {k: [] for k in ("viterbi_a15", "ransac_a13", "optim_points_a16", "reproj_a14")}
+    stats = None
+    for _ in range(reps + 1):
+        def tick():
+            torch.cuda.synchronize(device)
+            return time.perf_counter()
+        t0 = tick()
+        kf = viterbi_filter(kp2d, device=device)
+        t1 = tick()
+        pts = kf[..., :2].copy()
+        pts[kf[..., 2] < 0.5] = np.nan
+        flat = np.ascontiguousarray(pts.transpose(2, 0, 1, 3, 4).reshape(C, -1, 2))
+        t2 = tick()
+        p3 = g.triangulate_ransac(flat, min_cams=2)[0]
+        t3 = tick()
+        P2 = np.ascontiguousarray(pts.transpose(0, 2, 1, 3, 4))
+        t4 = tick()
+        res, jl, stats, _ = optim_points_batch(g, P2, p3.reshape(A, F, J, 3), cons, weak, return_stats=True,
+                                               **LIFT_ARGS)
+        t5 = tick()
+        g.reprojection_error(np.ascontiguousarray(res.reshape(-1, 3)), flat, mean=True)
+        t6 = tick()
+        for k, v in (("viterbi_a15", t1 - t0), ("ransac_a13", t3 - t2), ("optim_points_a16", t5 - t4),
+                     ("reproj_a14", t6 - t5)):
+            times[k].append(v)
+    med = {k: float(np.median(v[1:])) * 1e3 for k, v in times.items()}
+    tot = sum(med.values())
+    return {"gpu_ms": {k: round(v, 3) for k, v in med.items()}, "total_ms": round(tot, 3),
+            "individuals_frames_per_s": round(A * F / (tot * 1e-3), 2),
+            "optim_lm_iterations": stats[:, 2].tolist(), "statistic": f"median of {reps} after 1 warm-up",
+            "workload": f"BASELINE config 4: {F} frames x {C} views x {A} individuals x {J} joints, ransac + optim",
+            "note": "wall time per stage through the drop-in numpy API (host<->device copies included)"}
 
 
 def main():
@@ -244,8 +380,13 @@ def main():
         "end_to_end_mfma_frac": round(model_tflops / (world * PEAK_BF16_TFLOPS), 4),
         "roofline": roof,
     }
+    if rank == 0 and world == 1 and not args.no_lift:
+        result["lift_config4"] = lift_gpu(local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, cams_np)
+        result["cpu_baseline"] = cpu_baseline(cams_np)
+        if "lift_config4" in result:
+            result["lift_config4"]["speedup_vs_cpu_port"] = round(
+                result["cpu_baseline"]["config4_lift"]["total_s"] * 1e3 / result["lift_config4"]["total_ms"], 1)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:

@@ -8,6 +8,10 @@
  *     contexts / models own their weights and workspaces;
  *   - work is stream ordered on the hipStream_t passed as `void* stream`
  *     (NULL = the null stream); nothing synchronises unless stated;
+ *   - a context owns per-device scratch (decode, Viterbi, optim_points and affinity
+ *     workspaces) and a model owns its activations and mq_topdown staging: calls that
+ *     share one mq_ctx (or one mq_vitpose) must be issued on ONE stream (or be ordered
+ *     by the caller); use one context per stream for concurrent work;
  *   - missing 2D / 3D data is NaN on the way in and out (Viterbi emits (-1,-1,0.001)
  *     for missing frames exactly like anipose).
  *
@@ -33,31 +37,14 @@ typedef struct mq_vitpose mq_vitpose;
 int mq_abi_version(void);
 const char* mq_last_error(void);
 
-/* Process-wide tuning knobs (for A/B measurement; defaults are the tuned values). */
-#define MQ_TUNE_GEMM_STAGES 1       /* LDS ring depth of the 256x256 GEMM: 4 (128 KiB) or 5 (160 KiB) */
-#define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 kernel */
-#define MQ_TUNE_GEMM_ABLATE 3       /* timing ablations of the f32-epilogue 256 GEMM (WRONG results):
-                                       1 no steady-state DMA, 2 no barrier, 3 both, 7 + no LDS reads,
-                                       8 DMA issued but never waited for, 9 = 8 with buffer_load staging */
-#define MQ_TUNE_GEMM_BUFLOAD 5      /* 1 (default): stage GEMM tiles with buffer_load_dwordx4 ... lds; 0: global_load_lds */
-#define MQ_TUNE_GEMM_MFMA32 6       /* 1: 256x256 GEMM on v_mfma_f32_32x32x16_bf16 (else 16x16x32) */
-#define MQ_TUNE_ATTENTION_ABLATE 8  /* attention timing ablations (WRONG results): 1 staging only, 2 no K/V loads,
-                                       3 no output stores */
-#define MQ_TUNE_GEMM_SCHED 7        /* 1 (default): K-step with DMA issue / fragment reads interleaved between MFMAs */
-#define MQ_TUNE_GEMM_BM128 9        /* 1: 128x256 tiles when the 256x256 grid has at most one tile per CU (default 0) */
-#define MQ_TUNE_GEMM_PRIO 10        /* MFMA priority: 0 (default) s_setprio flips per MFMA cluster, 1 static priority for waves 4-7, 2 none */
-#define MQ_TUNE_GEMM_SYNC2 11       /* 1: with MQ_TUNE_GEMM_STAGES 5, one vmcnt wait + barrier per two K-steps (default 0) */
-#define MQ_TUNE_GEMM_PINGPONG 12    /* 1 (default): 256x256 GEMMs with K % 64 == 0 on the ping-pong kernel (wave groups alternate
-                                       LDS traffic and MFMA, gemm_pp.hip); 0: the interleaved-K-step kernel */
-#define MQ_TUNE_GEMM_PP_ABLATE 13   /* ping-pong GEMM timing ablations, bf16 epilogue only (WRONG results): 1 no vmcnt
-                                       waits, 2 no steady-state DMA, 3 both, 4 no fragment re-reads, 8 no barriers,
-                                       15 all */
-#define MQ_TUNE_GEMM_PP_DMA_IN_MFMA 14 /* 1: ping-pong GEMM issuing each phase's LDS-DMA between the issuing wave's own MFMAs */
-#define MQ_TUNE_GEMM_PP_RESID_PREFETCH 16 /* 1: short-K residual GEMMs (proj) on the ping-pong kernel with the residual
-                                       tile prefetched during the K-loop (measured 13 % slower); 0 (default): interleaved kernel */
-#define MQ_TUNE_ATTENTION_PERSIST 15 /* 1: T = 192 attention as 2 persistent workgroups per CU that stage the
-                                       next (image, head) while computing the current one (measured 3 % slower: the kernel is compute-bound); 0 (default): one workgroup per item */
-#define MQ_TUNE_OPTIM_PCG_ITERS 4  /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
+/* Process-wide routing knobs.  Every setting computes the same results (tested equal); they exist
+ * for A/B measurement.  Changing one makes the next mq_vitpose_forward re-capture its graph. */
+#define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 kernel (default 0) */
+#define MQ_TUNE_OPTIM_PCG_ITERS 4   /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
+#define MQ_TUNE_GEMM_PINGPONG 12    /* 1 (default): 256x256 GEMMs with K % 64 == 0 on the ping-pong kernel (wave groups
+                                       alternate LDS traffic and MFMA, gemm_pp.hip); 0: the interleaved-K-step kernel */
+#define MQ_TUNE_ATTENTION_V2 17     /* 1 (default): attention on 16x16x32 QK^T + transposed-output PV (vit_ops.hip
+                                       attention2_kernel); 0: the first-generation kernel */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

@@ -21,6 +21,7 @@
 namespace {
 
 thread_local std::string g_err;
+int g_tuning_gen = 0;  // bumped by mq_set_tuning
 
 int fail(const std::string& msg, int code = -1) {
   g_err = msg;
@@ -112,7 +113,7 @@ struct mq_vitpose {
   hipEvent_t ev_in = nullptr, ev_out = nullptr;
   bool use_graph = false;
   hipGraphExec_t gexec = nullptr;
-  int g_n = -1, g_flip = -1;
+  int g_n = -1, g_flip = -1, g_gen = -1;
   const void* g_in = nullptr;
   void* g_out = nullptr;
   // live kernel timing (eager forwards only): hipEvent pairs around every FFN fc1
@@ -121,93 +122,44 @@ struct mq_vitpose {
   int64_t g_rows_timed = 0;
   std::vector<hipEvent_t> t_events;
   size_t t_used = 0;
+  DevBuf stage;  // mq_topdown: crops, center / scale, heatmaps (allocated on the model's device)
 };
 
 extern "C" {
 
 int mq_abi_version(void) { return MQ_ABI_VERSION; }
 
+// Every knob selects between variants that compute the same results (they are tested equal):
+// kernel routing for A/B measurement and the inner-solver iteration count.  A change bumps the
+// generation so that ViTPose graphs captured under the old routing are re-captured.
 int mq_set_tuning(int key, int value) {
   switch (key) {
-    case MQ_TUNE_GEMM_STAGES:
-      if (value != 4 && value != 5) return fail("mq_set_tuning: GEMM stages must be 4 or 5", -2);
-      mq::g_gemm_stages = value;
-      return 0;
-    case MQ_TUNE_GEMM_ABLATE:
-      if (value != 0 && value != 1 && value != 2 && value != 3 && value != 7 && value != 8 && value != 9)
-        return fail("mq_set_tuning: ablation must be 0, 1, 2, 3, 7, 8 or 9", -2);
-      mq::g_gemm_ablate = value;
-      return 0;
     case MQ_TUNE_GEMM_FORCE_SMALL:
       mq::g_gemm_force_small = value != 0;
-      return 0;
-    case MQ_TUNE_GEMM_BUFLOAD:
-      mq::g_gemm_bufload = value != 0;
-      return 0;
-    case MQ_TUNE_GEMM_MFMA32:
-      mq::g_gemm_mfma32 = value != 0;
-      return 0;
-    case MQ_TUNE_GEMM_BM128:
-      mq::g_gemm_bm128 = value != 0;
-      return 0;
-    case MQ_TUNE_GEMM_SYNC2:
-      mq::g_gemm_sync2 = value != 0;
-      return 0;
-    case MQ_TUNE_GEMM_PRIO:
-      if (value < 0 || value > 2) return fail("mq_set_tuning: GEMM priority mode must be 0, 1 or 2", -2);
-      mq::g_gemm_prio = value;
-      return 0;
-    case MQ_TUNE_GEMM_SCHED:
-      mq::g_gemm_sched = value != 0;
-      return 0;
+      break;
     case MQ_TUNE_GEMM_PINGPONG:
       mq::g_gemm_pingpong = value != 0;
-      return 0;
-    case MQ_TUNE_GEMM_PP_DMA_IN_MFMA:
-      mq::g_gemm_pp_dim = value != 0;
-      return 0;
-    case MQ_TUNE_GEMM_PP_RESID_PREFETCH:
-      mq::g_gemm_pp_resid_pf = value != 0;
-      return 0;
-    case MQ_TUNE_GEMM_PP_ABLATE:
-      if (value != 0 && value != 1 && value != 2 && value != 3 && value != 4 && value != 8 && value != 15)
-        return fail("mq_set_tuning: ping-pong ablation must be 0, 1, 2, 3, 4, 8 or 15", -2);
-      mq::g_gemm_pp_ablate = value;
-      return 0;
-    case MQ_TUNE_ATTENTION_PERSIST:
-      mq::g_attention_persist = value != 0;
-      return 0;
-    case MQ_TUNE_ATTENTION_ABLATE:
-      if (value < 0 || value > 3) return fail("mq_set_tuning: attention ablation must be 0..3", -2);
-      mq::g_attention_ablate = value;
-      return 0;
+      break;
     case MQ_TUNE_OPTIM_PCG_ITERS:
       if (value < 1 || value > 128) return fail("mq_set_tuning: PCG iterations must be in [1, 128]", -2);
       mq::g_optim_pcg_iters = value;
-      return 0;
+      break;
+    case MQ_TUNE_ATTENTION_V2:
+      mq::g_attention_v2 = value != 0;
+      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
+  ++g_tuning_gen;
+  return 0;
 }
 
 int mq_get_tuning(int key) {
   switch (key) {
-    case MQ_TUNE_GEMM_STAGES: return mq::g_gemm_stages;
     case MQ_TUNE_GEMM_FORCE_SMALL: return mq::g_gemm_force_small ? 1 : 0;
-    case MQ_TUNE_GEMM_ABLATE: return mq::g_gemm_ablate;
-    case MQ_TUNE_OPTIM_PCG_ITERS: return mq::g_optim_pcg_iters;
-    case MQ_TUNE_GEMM_BUFLOAD: return mq::g_gemm_bufload;
-    case MQ_TUNE_GEMM_MFMA32: return mq::g_gemm_mfma32;
-    case MQ_TUNE_GEMM_SCHED: return mq::g_gemm_sched;
-    case MQ_TUNE_GEMM_BM128: return mq::g_gemm_bm128;
-    case MQ_TUNE_GEMM_PRIO: return mq::g_gemm_prio;
-    case MQ_TUNE_GEMM_SYNC2: return mq::g_gemm_sync2;
     case MQ_TUNE_GEMM_PINGPONG: return mq::g_gemm_pingpong;
-    case MQ_TUNE_GEMM_PP_ABLATE: return mq::g_gemm_pp_ablate;
-    case MQ_TUNE_GEMM_PP_RESID_PREFETCH: return mq::g_gemm_pp_resid_pf;
-    case MQ_TUNE_GEMM_PP_DMA_IN_MFMA: return mq::g_gemm_pp_dim;
-    case MQ_TUNE_ATTENTION_ABLATE: return mq::g_attention_ablate;
-    case MQ_TUNE_ATTENTION_PERSIST: return mq::g_attention_persist;
+    case MQ_TUNE_OPTIM_PCG_ITERS: return mq::g_optim_pcg_iters;
+    case MQ_TUNE_ATTENTION_V2: return mq::g_attention_v2;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }
@@ -385,6 +337,7 @@ int mq_vitpose_destroy(mq_vitpose* m) {
   if (m->ev_out) (void)hipEventDestroy(m->ev_out);
   m->weights.release();
   m->ws.release();
+  m->stage.release();
   delete m;
   return 0;
 }
@@ -580,7 +533,8 @@ int mq_vitpose_forward(mq_vitpose* m, const float* crops, int n, int flip_test, 
     HIP_TRY(hipEventCreateWithFlags(&m->ev_out, hipEventDisableTiming));
   }
   hipStream_t cs = m->cap_stream;
-  if (!m->gexec || m->g_n != n || m->g_flip != flip_test || m->g_in != crops || m->g_out != heatmaps) {
+  if (!m->gexec || m->g_n != n || m->g_flip != flip_test || m->g_in != crops || m->g_out != heatmaps ||
+      m->g_gen != g_tuning_gen) {
     if (m->gexec) {
       (void)hipGraphExecDestroy(m->gexec);
       m->gexec = nullptr;
@@ -599,6 +553,7 @@ int mq_vitpose_forward(mq_vitpose* m, const float* crops, int n, int flip_test, 
     if (e != hipSuccess) return fail(std::string("hipGraphInstantiate: ") + hipGetErrorString(e), -5);
     m->g_n = n;
     m->g_flip = flip_test;
+    m->g_gen = g_tuning_gen;
     m->g_in = crops;
     m->g_out = heatmaps;
   }
@@ -666,13 +621,13 @@ int mq_topdown(mq_vitpose* m, const uint8_t* frames, int64_t frame_stride, int h
   if (!m) return fail("mq_topdown: null model");
   if (n <= 0) return 0;
   HIP_TRY(hipSetDevice(m->ctx->device));
-  // scratch: crops, center/scale, heatmaps (if caller passes none)
-  static thread_local DevBuf tmp;  // per-thread staging, grown on demand
+  // staging owned by the model (its device): crops, center/scale, heatmaps (if caller passes none).
+  // Calls on one model are stream-ordered: the staging is reused by the next call on the model.
   const size_t crop_b = (size_t)n * 3 * m->img_h * m->img_w * 4;
   const size_t cs_b = (size_t)n * 4 * 4;
   const size_t hm_b = (size_t)n * m->J * 16 * m->T * 4;
-  if (tmp.ensure(crop_b + cs_b + hm_b + 1024)) return fail("mq_topdown: scratch alloc failed", -5);
-  char* b = tmp.as<char>();
+  if (m->stage.ensure(crop_b + cs_b + hm_b + 1024)) return fail("mq_topdown: scratch alloc failed", -5);
+  char* b = m->stage.as<char>();
   float* crops = (float*)b;
   float* center = (float*)(b + crop_b);
   float* scale = center + 2 * n;

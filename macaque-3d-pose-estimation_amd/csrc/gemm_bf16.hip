@@ -156,26 +156,16 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
 // 16 B (f32) per lane instead of scalar 2-byte stores.
 // LDS image: 64-byte rows, 16-byte chunk c of row r at slot c ^ ((r >> 1) & 3)
 // (ds_read_b128 conflict-free for the 16x16x32 fragment pattern).
-constexpr int B2M = 256, B2N = 256, B2K = 32, B2T = 512;
+// Staging: buffer_load_dwordx4 ... lds with a 32-bit per-lane offset fixed per tile and the
+// K advance in soffset.  Each K-step is one basic block with the DMAs and the next stage's
+// fragment reads spread between the MFMAs (sched_group_barrier).
+// This kernel serves the f32-residual GEMM at short K (proj, K = 1280); gemm_pp.hip serves the rest.
+constexpr int B2M = 256, B2N = 256, B2K = 32, B2T = 512, B2NS = 4;
 constexpr int B2_OP_BYTES = B2M * B2K * 2;       // 16 KiB per operand per stage
 constexpr int B2_STAGE_BYTES = 2 * B2_OP_BYTES;  // 32 KiB
+constexpr int B2_LDS = B2NS * B2_STAGE_BYTES;    // 128 KiB
 
 __device__ __forceinline__ int swz2(int row) { return (row >> 1) & 3; }
-
-// one 256x32 bf16 operand tile = 16 wave-instructions of 1 KiB; wave w issues 2 of them
-__device__ __forceinline__ void stage256(const bf16_t* __restrict__ g, int ld, int r0, int rmax, int k0,
-                                         char* lds_op, int wave, int lane) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int rbase = (wave * 2 + i) * 16;
-    const int row = rbase + (lane >> 2);
-    const int chunk = (lane & 3) ^ swz2(row);
-    int grow = r0 + row;
-    grow = grow < rmax ? grow : rmax - 1;
-    const bf16_t* src = g + (size_t)grow * ld + k0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(src), MQ_LDS_LOCAL(lds_op + rbase * 64), 16, 0, 0);
-  }
-}
 
 __device__ __forceinline__ bf16x8 frag256(const char* lds_op, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds_op + row * 64 + ((chunk ^ swz2(row)) << 4));
@@ -189,8 +179,7 @@ __device__ __forceinline__ void wait_vm() {
 }
 
 // Tile -> (m0, n0): grouped ordering (8 M-tiles per group) so the tiles an XCD works
-// on concurrently share A and W panels in its L2.  BM = tile rows (256 or 128).
-template <int BM_ = B2M>
+// on concurrently share A and W panels in its L2.
 __device__ __forceinline__ void tile_coords(int wid, int tiles_m, int tiles_n, int& m0, int& n0) {
   constexpr int GROUP_M = 8;
   const int per_group = GROUP_M * tiles_n;
@@ -198,31 +187,19 @@ __device__ __forceinline__ void tile_coords(int wid, int tiles_m, int tiles_n, i
   const int first_m = grp * GROUP_M;
   const int gsize = min(tiles_m - first_m, GROUP_M);
   const int in_g = wid - grp * per_group;
-  m0 = (first_m + in_g % gsize) * BM_;
+  m0 = (first_m + in_g % gsize) * B2M;
   n0 = (in_g / gsize) * B2N;
 }
 
 // Persistent: one 512-thread block per CU walks its tiles; the DMA stream and the
 // fragment pipeline run straight across tile boundaries (the first stages of the
 // next tile are in flight while the current tile's epilogue stores drain).
-// MI = 16-row A fragments per wave: 8 -> 256x256 tile (wave 128x64), 4 -> 128x256 tile
-// (wave 64x64).  The 128-row tile is for narrow-N GEMMs (N = 1280: proj, fc2) where the
-// 256x256 grid is one tile per CU and the f32 residual epilogue (a 256 KiB read-modify-write
-// per tile) would run exposed after the K-loop; with two 128-row tiles per CU the first
-// tile's epilogue drains behind the second tile's K-loop.
-// ABL (timing ablations only, outputs are wrong when non-zero): bit0 no steady-state
-// DMA, bit1 no per-step barrier, bit2 no fragment re-reads.
-// BUF: stage with buffer_load_dwordx4 ... lds (32-bit per-lane offset fixed per tile, K advance in
-// soffset) instead of global_load_lds_dwordx4 (64-bit per-lane address rebuilt every stage).
-template <int EPI, int NS, int ABL = 0, bool BUF = false, bool SCHED = false, int MI = 8, int PRIO = 0, bool SYNC2 = false>
+template <int EPI>
 __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m, int tiles_n) {
-  static_assert(MI == 8 || MI == 4, "tile rows 256 or 128");
-  constexpr int BMT = 32 * MI;              // tile rows
-  constexpr int NA = BMT / 128;             // A-operand DMA instructions per wave per stage
-  constexpr int A_BYTES = BMT * B2K * 2;    // A operand bytes per stage
-  constexpr int STAGE = A_BYTES + B2_OP_BYTES;
-  constexpr int DMA_PER_STAGE = NA + 2;     // per wave
-  constexpr int WROWS = BMT / 2;            // A rows per wave (2 waves along M)
+  constexpr int MI = 8;                     // 16-row A fragments per wave
+  constexpr int NS = B2NS;
+  constexpr int DMA_PER_STAGE = 4;          // per wave: 2 A + 2 W wave-instructions
+  constexpr int WROWS = B2M / 2;            // A rows per wave (2 waves along M)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
@@ -250,8 +227,6 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
   // end the cursor stays on the last stage: extra DMAs re-load it into a dead buffer,
   // which keeps every wait count uniform.
   int iss_t = 0, iss_k = 0, iss_slot = 0;
-  const bf16_t* pa[2];
-  const bf16_t* pw[2];
   unsigned va[2], vw[2];
   const __amdgpu_buffer_rsrc_t rsA =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)((size_t)p.M * p.lda * 2), 0x00020000);
@@ -259,52 +234,31 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
   auto set_tile_ptrs = [&](int ti) {
     int m0, n0;
-    tile_coords<BMT>(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int row = (wave * NA + i) * 16 + (lane >> 2);
-      const int chunk = (lane & 3) ^ swz2(row);
-      const int ga = min(m0 + row, p.M - 1);
-      if constexpr (BUF)
-        va[i] = (unsigned)(((size_t)ga * p.lda + chunk * 8) * 2);
-      else
-        pa[i] = p.A + (size_t)ga * p.lda + chunk * 8;
-    }
+    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = (wave * 2 + i) * 16 + (lane >> 2);
       const int chunk = (lane & 3) ^ swz2(row);
+      const int ga = min(m0 + row, p.M - 1);
       const int gw = min(n0 + row, p.N - 1);
-      if constexpr (BUF)
-        vw[i] = (unsigned)(((size_t)gw * p.ldw + chunk * 8) * 2);
-      else
-        pw[i] = p.W + (size_t)gw * p.ldw + chunk * 8;
+      va[i] = (unsigned)(((size_t)ga * p.lda + chunk * 8) * 2);
+      vw[i] = (unsigned)(((size_t)gw * p.ldw + chunk * 8) * 2);
     }
   };
   set_tile_ptrs(0);
   auto issue_a = [&]() {
-    char* sb = smem + iss_slot * STAGE;
+    char* sb = smem + iss_slot * B2_STAGE_BYTES;
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      if constexpr (BUF)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(sb + (wave * NA + i) * 16 * 64), 16, va[i],
-                                                 iss_k * B2K * 2, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pa[i] + iss_k * B2K),
-                                         MQ_LDS_LOCAL(sb + (wave * NA + i) * 16 * 64), 16, 0, 0);
-    }
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, va[i],
+                                               iss_k * B2K * 2, 0, 0);
   };
   auto issue_w = [&]() {
-    char* sb = smem + iss_slot * STAGE + A_BYTES;
+    char* sb = smem + iss_slot * B2_STAGE_BYTES + B2_OP_BYTES;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if constexpr (BUF)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, vw[i],
-                                                 iss_k * B2K * 2, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pw[i] + iss_k * B2K),
-                                         MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
-    }
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, vw[i],
+                                               iss_k * B2K * 2, 0, 0);
   };
   auto advance = [&]() {
     iss_slot = iss_slot + 1 == NS ? 0 : iss_slot + 1;
@@ -316,11 +270,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       set_tile_ptrs(iss_t);
     }
   };
-  auto issue_w_and_advance = [&]() {
-    issue_w();
-    advance();
-  };
-  auto stage_ptr = [&](int g) { return smem + (g % NS) * STAGE; };
+  auto stage_ptr = [&](int g) { return smem + (g % NS) * B2_STAGE_BYTES; };
 
   f32x4 acc[MI][4];
 #pragma unroll
@@ -332,7 +282,8 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st) {
     issue_a();
-    issue_w_and_advance();
+    issue_w();
+    advance();
   }
   wait_vm<DMA_PER_STAGE * (NS - 3)>();  // stages 0 and 1 landed (this wave)
   __builtin_amdgcn_s_barrier();
@@ -341,14 +292,14 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
   {
     const char* As = stage_ptr(0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b0[j] = frag256(As + A_BYTES, wn * 64 + j * 16 + frow, fk);
+    for (int j = 0; j < 4; ++j) b0[j] = frag256(As + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
 #pragma unroll
     for (int i = 0; i < MI; ++i) a[i] = frag256(As, wm * WROWS + i * 16 + frow, fk);
   }
 
   auto epilogue = [&](int ti) {
     int m0, n0;
-    tile_coords<BMT>(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
     // lane holds D[n][m] with m = l & 15 (col of D) and n = 4 * (l >> 4) + e
     const int mm = lane & 15;
     const int nn = 4 * (lane >> 4);
@@ -408,7 +359,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
         const int n = n0 + wn * 64 + j * 16 + nn;
         bias[j] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      const bool full = (m0 + BMT <= p.M) && (n0 + B2N <= p.N);
+      const bool full = (m0 + B2M <= p.M) && (n0 + B2N <= p.N);
       if (full) {
         // CH fragment rows of loads in flight at a time (register budget: the accumulators
         // stay live for the next tile)
@@ -488,56 +439,36 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
     }
   };
 
+
   // >= this many VMEM ops of a full tile's epilogue are younger than the DMA of the stage a
   // K-step waits for (bf16: 2 stores per fragment row; f32: 4 stores (+ loads) per row)
   constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 2 * MI : 4 * MI;
   bool stores_pending = false;
   int kt = 0, ct = 0, cm0 = 0, cn0 = 0;  // K-step within the current tile, tile index, its origin
-  auto tile_start = [&]() { tile_coords<BMT>(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0); };
+  auto tile_start = [&]() { tile_coords(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0); };
   tile_start();
   auto end_step = [&]() {
-    if constexpr (SYNC2) {
-      // one wait + barrier per TWO K-steps (an effective BK = 64 step; needs NS = 5 and even
-      // nk): after odd step h, stages up to h+3 landed (the reads of steps h+1, h+2), stage h+4
-      // (issued in step h) in flight; slots refilled in steps h+1, h+2 were last read in h-1, h.
-      static_assert(!SYNC2 || NS == 5, "SYNC2 needs a 5-stage ring");
-      if (kt & 1) {
-        wait_vm<DMA_PER_STAGE * (NS - 4)>();
-        __builtin_amdgcn_s_barrier();
-      }
-      stores_pending = false;
-      if (++kt == nk) {
-        epilogue(ct);
-        kt = 0;
-        ++ct;
-        tile_start();
-      }
-      return;
-    }
-    if constexpr (!(ABL & 1) && !(ABL & 8)) {
-      // stage g+2 landed; g+3 .. g+NS-1 in flight.  Right after a full tile's epilogue its
-      // stores sit between those DMAs in the in-order vmcnt queue: let them drain behind
-      // this step instead of stalling the MFMAs on them.
-      if (stores_pending)
-        wait_vm<DMA_PER_STAGE * (NS - 3) + EPI_OPS>();
-      else
-        wait_vm<DMA_PER_STAGE * (NS - 3)>();
-    }
+    // stage g+2 landed; g+3 .. g+NS-1 in flight.  Right after a full tile's epilogue its
+    // stores sit between those DMAs in the in-order vmcnt queue: let them drain behind
+    // this step instead of stalling the MFMAs on them.
+    if (stores_pending)
+      wait_vm<DMA_PER_STAGE * (NS - 3) + EPI_OPS>();
+    else
+      wait_vm<DMA_PER_STAGE * (NS - 3)>();
     stores_pending = false;
-    if constexpr (!(ABL & 2)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     if (++kt == nk) {
       epilogue(ct);
-      stores_pending = (cm0 + BMT <= p.M) && (cn0 + B2N <= p.N);
+      stores_pending = (cm0 + B2M <= p.M) && (cn0 + B2N <= p.N);
       kt = 0;
       ++ct;
       tile_start();
     }
   };
-  // SCHED: one basic block per K-step body with the DMAs and fragment reads spread between the
-  // MFMAs (sched_group_barrier), instead of DMA issue right after the barrier.
-  auto kstep_sched = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
-    const char* An = stage_ptr(g + 1);
-    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(1);
+  // one basic block per K-step body with the DMAs and fragment reads spread between the MFMAs
+  auto kstep = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
+    const char* An = stage_ptr(g + 1);  // past the end: harmless reads of a dead buffer
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < MI / 2; ++i)
 #pragma unroll
@@ -545,12 +476,12 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
     issue_a();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bn[j] = frag256(An + A_BYTES, wn * 64 + j * 16 + frow, fk);
+    for (int j = 0; j < 4; ++j) bn[j] = frag256(An + B2_OP_BYTES, wn * 64 + j * 16 + frow, fk);
 #pragma unroll
     for (int i = 0; i < MI / 2; ++i) a[i] = frag256(An, wm * WROWS + i * 16 + frow, fk);
-    // first half: 4 MI MFMAs, NA DMAs, 4 + MI/2 fragment reads
+    // first half: 4 MI MFMAs, 2 DMAs, 4 + MI/2 fragment reads
 #pragma unroll
-    for (int t = 0; t < NA; ++t) {
+    for (int t = 0; t < 2; ++t) {
       __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
     }
@@ -559,8 +490,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    if constexpr (2 * MI - 2 * NA - 4 - MI / 2 > 0)
-      __builtin_amdgcn_sched_group_barrier(0x8, 2 * MI - 2 * NA - 4 - MI / 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x8, 2 * MI - 4 - 4 - MI / 2, 0);
 #pragma unroll
     for (int i = MI / 2; i < MI; ++i)
 #pragma unroll
@@ -579,53 +509,11 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
       __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
-    if constexpr (MI - 4 > 0) __builtin_amdgcn_sched_group_barrier(0x8, MI - 4, 0);
-    if constexpr (PRIO == 0) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_group_barrier(0x8, MI - 4, 0);
+    __builtin_amdgcn_s_setprio(0);
     advance();
     end_step();
   };
-  auto kstep = [&](int g, bf16x8 (&bc)[4], bf16x8 (&bn)[4]) {
-    if constexpr (SCHED) {
-      kstep_sched(g, bc, bn);
-      return;
-    }
-    const char* An = stage_ptr(g + 1);  // past the end: harmless reads of a dead buffer
-    if constexpr (!(ABL & 1)) issue_a();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < MI / 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if constexpr (!(ABL & 4)) {
-#pragma unroll
-      for (int i = 0; i < MI / 2; ++i) a[i] = frag256(An, wm * WROWS + i * 16 + frow, fk);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bn[j] = frag256(An + A_BYTES, wn * 64 + j * 16 + frow, fk);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bn[j] = bc[j];
-    }
-    if constexpr (!(ABL & 1)) issue_w_and_advance();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = MI / 2; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bc[j], a[i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if constexpr (!(ABL & 4)) {
-#pragma unroll
-      for (int i = MI / 2; i < MI; ++i) a[i] = frag256(An, wm * WROWS + i * 16 + frow, fk);
-    }
-    end_step();
-  };
-  // PRIO 1: static priority for the second-dispatched half (waves 4-7 lose VALU/issue
-  // arbitration to the older half on every segment); PRIO 0: flips around each MFMA cluster
-  if constexpr (PRIO == 1) {
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-  }
   int g = 0;
   for (; g + 1 < total; g += 2) {
     kstep(g, b0, b1);
@@ -635,377 +523,16 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the block
 }
 
-// ============================================================================
-// Same persistent 256x256 tile and DMA pipeline, on v_mfma_f32_32x32x16_bf16.  A 32x32x16
-// MFMA holds the SIMD's vector issue for 8 of its 32 cycles (16x16x32: 8 of 16), so the
-// fragment reads, LDS-DMA issues and waits of a K-step fit in the MFMA shadow.
-// Each wave: 128 x 64 = 4 (M) x 2 (N) blocks of 32x32, acc = 8 x f32x16.
-// Operand fragment (both operands): lane l holds row (l & 31), k = 8 * (l >> 5) .. +7 of a
-// 16-deep K slice; a BK = 32 stage has two slices (kk), i.e. 16-B chunk c = 2 kk + (l >> 5).
-// Swapped product D = W * A^T: lane l, register r holds C[m = l & 31][n = 8 (r >> 2) + 4 (l >> 5) + (r & 3)].
-// LDS image: 64-B rows, chunk c of row r at slot c ^ ((r >> 2) & 3) -- conflict-free for the
-// ds_read_b128 lane groups of this pattern (rows {0-3,12-15,20-27}, {4-11,16-19,28-31}).
-__device__ __forceinline__ int swz32(int row) { return (row >> 2) & 3; }
-
-__device__ __forceinline__ bf16x8 frag32(const char* lds_op, int row, int chunk) {
-  return *reinterpret_cast<const bf16x8*>(lds_op + row * 64 + ((chunk ^ swz32(row)) << 4));
-}
-
-template <int EPI, int NS, bool BUF>
-__global__ __launch_bounds__(B2T, 2) void gemm256m32_kernel(GemmArgs p, int tiles_m, int tiles_n) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int frow = lane & 31;
-  const int fh = lane >> 5;
-
-  const int nt = tiles_m * tiles_n;
-  const int G = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int nbx = (G - xcd + 7) >> 3;
-  const int xb = bid >> 3;
-  const int q = nt >> 3, r = nt & 7;
-  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int len = q + (xcd < r ? 1 : 0);
-  const int my_tiles = xb < len ? (len - xb + nbx - 1) / nbx : 0;
-  const int nk = p.K / B2K;
-  const int total = my_tiles * nk;
-  if (total == 0) return;
-
-  int iss_t = 0, iss_k = 0, iss_slot = 0;
-  const bf16_t* pa[2];
-  const bf16_t* pw[2];
-  unsigned va[2], vw[2];
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)((size_t)p.M * p.lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsW =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
-  auto set_tile_ptrs = [&](int ti) {
-    int m0, n0;
-    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (wave * 2 + i) * 16 + (lane >> 2);
-      const int chunk = (lane & 3) ^ swz32(row);
-      const int ga = min(m0 + row, p.M - 1), gw = min(n0 + row, p.N - 1);
-      if constexpr (BUF) {
-        va[i] = (unsigned)(((size_t)ga * p.lda + chunk * 8) * 2);
-        vw[i] = (unsigned)(((size_t)gw * p.ldw + chunk * 8) * 2);
-      } else {
-        pa[i] = p.A + (size_t)ga * p.lda + chunk * 8;
-        pw[i] = p.W + (size_t)gw * p.ldw + chunk * 8;
-      }
-    }
-  };
-  set_tile_ptrs(0);
-  auto issue_a = [&]() {
-    char* sb = smem + iss_slot * B2_STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if constexpr (BUF)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, va[i],
-                                                 iss_k * B2K * 2, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pa[i] + iss_k * B2K),
-                                         MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
-    }
-  };
-  auto issue_w_and_advance = [&]() {
-    char* sb = smem + iss_slot * B2_STAGE_BYTES + B2_OP_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if constexpr (BUF)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsW, MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, vw[i],
-                                                 iss_k * B2K * 2, 0, 0);
-      else
-        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(pw[i] + iss_k * B2K),
-                                         MQ_LDS_LOCAL(sb + (wave * 2 + i) * 16 * 64), 16, 0, 0);
-    }
-    iss_slot = iss_slot + 1 == NS ? 0 : iss_slot + 1;
-    if (iss_k + 1 < nk) {
-      ++iss_k;
-    } else if (iss_t + 1 < my_tiles) {
-      ++iss_t;
-      iss_k = 0;
-      set_tile_ptrs(iss_t);
-    }
-  };
-  auto stage_ptr = [&](int g) { return smem + (g % NS) * B2_STAGE_BYTES; };
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-#pragma unroll
-  for (int st = 0; st < NS - 1; ++st) {
-    issue_a();
-    issue_w_and_advance();
-  }
-  wait_vm<4 * (NS - 3)>();
-  __builtin_amdgcn_s_barrier();
-
-  bf16x8 a[4][2], b0[2][2], b1[2][2];
-  {
-    const char* S = stage_ptr(0);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) b0[j][kk] = frag32(S + B2_OP_BYTES, wn * 64 + j * 32 + frow, 2 * kk + fh);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) a[i][kk] = frag32(S, wm * 128 + i * 32 + frow, 2 * kk + fh);
-  }
-
-  auto epilogue = [&](int ti) {
-    int m0, n0;
-    tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
-    if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
-      // lanes l and l+32 hold columns 8g+0..3 and 8g+4..7 of row l & 31; pairing groups
-      // (g, g+1) with v_permlane32_swap gives each lane 8 consecutive columns -> 16-B stores.
-      float4 bias[2][4];
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int n = n0 + wn * 64 + j * 32 + g4 * 8 + fh * 4;
-          bias[j][g4] = (p.bias && n < p.N) ? *reinterpret_cast<const float4*>(p.bias + n)
-                                            : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wm * 128 + i * 32 + frow;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-#pragma unroll
-          for (int gp = 0; gp < 4; gp += 2) {
-            unsigned pk[2][2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int g4 = gp + h;
-              const float4 bb = bias[j][g4];
-              float v[4] = {acc[i][j][4 * g4 + 0] + bb.x, acc[i][j][4 * g4 + 1] + bb.y,
-                            acc[i][j][4 * g4 + 2] + bb.z, acc[i][j][4 * g4 + 3] + bb.w};
-              if constexpr (EPI == EPI_GELU_BF16) {
-                const f32x2 g0 = gelu_erf2((f32x2){v[0], v[1]}), g1 = gelu_erf2((f32x2){v[2], v[3]});
-                v[0] = g0.x;
-                v[1] = g0.y;
-                v[2] = g1.x;
-                v[3] = g1.y;
-              }
-              pk[h][0] = pack_bf16x2(v[0], v[1]);
-              pk[h][1] = pack_bf16x2(v[2], v[3]);
-            }
-            const auto s0 = __builtin_amdgcn_permlane32_swap(pk[0][0], pk[1][0], false, false);
-            const auto s1 = __builtin_amdgcn_permlane32_swap(pk[0][1], pk[1][1], false, false);
-            // lanes < 32: group gp of row m; lanes >= 32: group gp+1 of row m
-            const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-            const int n = n0 + wn * 64 + j * 32 + (gp + fh) * 8;
-            if (m < p.M && n < p.N) *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
-          }
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-        }
-      }
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = m0 + wm * 128 + i * 32 + frow;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int n = n0 + wn * 64 + j * 32 + g4 * 8 + fh * 4;
-          float v[4] = {acc[i][j][4 * g4 + 0], acc[i][j][4 * g4 + 1], acc[i][j][4 * g4 + 2], acc[i][j][4 * g4 + 3]};
-          if (m >= p.M || n >= p.N) continue;
-          if (p.bias) {
-            const float4 bias = *reinterpret_cast<const float4*>(p.bias + n);
-            v[0] += bias.x;
-            v[1] += bias.y;
-            v[2] += bias.z;
-            v[3] += bias.w;
-          }
-          if constexpr (EPI == EPI_RESID_F32) {
-            float4* c = reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n);
-            float4 x = *c;
-            x.x += v[0];
-            x.y += v[1];
-            x.z += v[2];
-            x.w += v[3];
-            *c = x;
-          } else if constexpr (EPI == EPI_POS_F32) {
-            const float4 ps = *reinterpret_cast<const float4*>(p.aux + (size_t)(m % p.aux_rows) * p.N + n);
-            *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) =
-                make_float4(v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w);
-          } else if constexpr (EPI == EPI_F32) {
-            *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n) = make_float4(v[0], v[1], v[2], v[3]);
-          }
-        }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-      }
-    }
-  };
-
-  bool stores_pending = false;
-  auto kstep = [&](int g, bf16x8 (&bc)[2][2], bf16x8 (&bn)[2][2]) {
-    const char* Sn = stage_ptr(g + 1);  // past the end: harmless reads of a dead buffer
-    issue_a();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[j][kk], a[i][kk], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) a[i][kk] = frag32(Sn, wm * 128 + i * 32 + frow, 2 * kk + fh);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bn[j][kk] = frag32(Sn + B2_OP_BYTES, wn * 64 + j * 32 + frow, 2 * kk + fh);
-    issue_w_and_advance();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 2; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bc[j][kk], a[i][kk], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int i = 2; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) a[i][kk] = frag32(Sn, wm * 128 + i * 32 + frow, 2 * kk + fh);
-    constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
-    if (stores_pending)
-      wait_vm<4 * (NS - 3) + EPI_OPS>();
-    else
-      wait_vm<4 * (NS - 3)>();
-    stores_pending = false;
-    __builtin_amdgcn_s_barrier();
-    const int ti = g / nk;
-    if (g - ti * nk == nk - 1) {
-      epilogue(ti);
-      int m0, n0;
-      tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
-      stores_pending = (m0 + B2M <= p.M) && (n0 + B2N <= p.N);
-    }
-  };
-  int g = 0;
-  for (; g + 1 < total; g += 2) {
-    kstep(g, b0, b1);
-    kstep(g + 1, b1, b0);
-  }
-  if (g < total) kstep(g, b0, b1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 static int g_num_cus = 0;
 
-int g_gemm_stages = 4;  // tuning knob (mq_set_tuning(MQ_TUNE_GEMM_STAGES, 4|5))
-int g_gemm_ablate = 0;  // timing ablation knob (MQ_TUNE_GEMM_ABLATE)
-int g_gemm_bufload = 1; // MQ_TUNE_GEMM_BUFLOAD: stage with buffer_load ... lds (default: +3-11 % over glds)
-int g_gemm_sched = 1;   // MQ_TUNE_GEMM_SCHED: K-step with DMAs/reads interleaved between MFMAs (default: +1-3 %)
-int g_gemm_mfma32 = 0;  // MQ_TUNE_GEMM_MFMA32: 32x32x16 MFMA variant of the 256x256 kernel
-int g_gemm_sync2 = 0;   // MQ_TUNE_GEMM_SYNC2: with 5 stages, one wait + barrier per two K-steps
-int g_gemm_prio = 0;    // MQ_TUNE_GEMM_PRIO: 0 setprio flips per MFMA cluster, 1 static priority for waves 4-7, 2 none
-int g_gemm_bm128 = 0;   // MQ_TUNE_GEMM_BM128: 128x256 tiles for grids of at most one 256x256 tile per CU (measured slower: 16 MFMAs per wave per K-step do not cover the step overheads)
-
-template <int EPI, int NS, int ABL, bool BUF = false, bool SCHED = false, int MI = 8, int PRIO = 0, bool SYNC2 = false>
+template <int EPI>
 static void launch256(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
-  const int lds = NS * (32 * MI * B2K * 2 + B2_OP_BYTES);
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI, NS, ABL, BUF, SCHED, MI, PRIO, SYNC2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, B2_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm256_kernel<EPI, NS, ABL, BUF, SCHED, MI, PRIO, SYNC2>), grid, dim3(B2T), lds, stream, p,
-                     tiles_m, tiles_n);
-}
-
-template <int EPI, int NS, bool BUF>
-static void launch256m32(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
-  static bool attr = false;
-  const int lds = NS * B2_STAGE_BYTES;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256m32_kernel<EPI, NS, BUF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    attr = true;
-  }
-  hipLaunchKernelGGL((gemm256m32_kernel<EPI, NS, BUF>), grid, dim3(B2T), lds, stream, p, tiles_m, tiles_n);
-}
-
-template <int EPI>
-static void launch256s(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
-  if (g_gemm_mfma32) {
-    if (g_gemm_bufload)
-      launch256m32<EPI, 4, true>(grid, stream, p, tiles_m, tiles_n);
-    else
-      launch256m32<EPI, 4, false>(grid, stream, p, tiles_m, tiles_n);
-    return;
-  }
-  if constexpr (EPI == EPI_F32) {  // ablations are compiled for the plain-f32 epilogue only
-    switch (g_gemm_ablate) {
-      case 1: launch256<EPI, 4, 1>(grid, stream, p, tiles_m, tiles_n); return;
-      case 2: launch256<EPI, 4, 2>(grid, stream, p, tiles_m, tiles_n); return;
-      case 3: launch256<EPI, 4, 3>(grid, stream, p, tiles_m, tiles_n); return;
-      case 7: launch256<EPI, 4, 7>(grid, stream, p, tiles_m, tiles_n); return;
-      case 8: launch256<EPI, 4, 8>(grid, stream, p, tiles_m, tiles_n); return;
-      case 9: launch256<EPI, 4, 8, true>(grid, stream, p, tiles_m, tiles_n); return;
-      default: break;
-    }
-  }
-  if (g_gemm_sched) {
-    if (g_gemm_stages == 5 && g_gemm_sync2 && (p.K / B2K) % 2 == 0)
-      launch256<EPI, 5, 0, true, true, 8, 0, true>(grid, stream, p, tiles_m, tiles_n);
-    else if (g_gemm_stages == 5)
-      launch256<EPI, 5, 0, true, true>(grid, stream, p, tiles_m, tiles_n);
-    else if (g_gemm_prio == 1)
-      launch256<EPI, 4, 0, true, true, 8, 1>(grid, stream, p, tiles_m, tiles_n);
-    else if (g_gemm_prio == 2)
-      launch256<EPI, 4, 0, true, true, 8, 2>(grid, stream, p, tiles_m, tiles_n);
-    else
-      launch256<EPI, 4, 0, true, true>(grid, stream, p, tiles_m, tiles_n);
-    return;
-  }
-  if (g_gemm_bufload) {
-    if (g_gemm_stages == 5)
-      launch256<EPI, 5, 0, true>(grid, stream, p, tiles_m, tiles_n);
-    else
-      launch256<EPI, 4, 0, true>(grid, stream, p, tiles_m, tiles_n);
-    return;
-  }
-  if (g_gemm_stages == 5)
-    launch256<EPI, 5, 0>(grid, stream, p, tiles_m, tiles_n);
-  else
-    launch256<EPI, 4, 0>(grid, stream, p, tiles_m, tiles_n);
-}
-
-// 128x256 tiles: grid = tiles / rounds so every block walks the same number of tiles
-template <int EPI>
-static void launch128(hipStream_t stream, const GemmArgs& p) {
-  const int tiles_m = (p.M + 127) / 128, tiles_n = (p.N + B2N - 1) / B2N;
-  const int tiles = tiles_m * tiles_n;
-  const int rounds = (tiles + g_num_cus - 1) / g_num_cus;
-  dim3 grid((tiles + rounds - 1) / rounds);
-  if (g_gemm_sched)
-    launch256<EPI, 4, 0, true, true, 4>(grid, stream, p, tiles_m, tiles_n);
-  else
-    launch256<EPI, 4, 0, true, false, 4>(grid, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm256_kernel<EPI>), grid, dim3(B2T), B2_LDS, stream, p, tiles_m, tiles_n);
 }
 
 static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
@@ -1015,29 +542,16 @@ static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
     if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
       g_num_cus = 256;
   }
-  if (gemm_pingpong_fits(p, epi) && !g_gemm_ablate && !g_gemm_mfma32) return gemm_pingpong(p, epi, g_num_cus, stream);
+  if (gemm_pingpong_fits(p, epi)) return gemm_pingpong(p, epi, g_num_cus, stream);
   const int tiles_m = (p.M + B2M - 1) / B2M, tiles_n = (p.N + B2N - 1) / B2N;
   const int tiles = tiles_m * tiles_n;
-  // narrow grids (at most one 256x256 tile per CU, e.g. N = 1280): 128-row tiles, two or more
-  // per CU, so epilogues overlap the next tile's K-loop
-  if (g_gemm_bm128 && tiles <= g_num_cus && !g_gemm_mfma32 && !g_gemm_ablate) {
-    switch (epi) {
-      case EPI_BF16: launch128<EPI_BF16>(stream, p); break;
-      case EPI_GELU_BF16: launch128<EPI_GELU_BF16>(stream, p); break;
-      case EPI_RESID_F32: launch128<EPI_RESID_F32>(stream, p); break;
-      case EPI_POS_F32: launch128<EPI_POS_F32>(stream, p); break;
-      case EPI_F32: launch128<EPI_F32>(stream, p); break;
-      default: return -3;
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -4;
-  }
   dim3 grid(tiles < g_num_cus ? tiles : g_num_cus);
   switch (epi) {
-    case EPI_BF16: launch256s<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_GELU_BF16: launch256s<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RESID_F32: launch256s<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_POS_F32: launch256s<EPI_POS_F32>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_F32: launch256s<EPI_F32>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_BF16: launch256<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_GELU_BF16: launch256<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RESID_F32: launch256<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_POS_F32: launch256<EPI_POS_F32>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_F32: launch256<EPI_F32>(grid, stream, p, tiles_m, tiles_n); break;
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;

@@ -40,8 +40,6 @@
 namespace mq {
 
 int g_gemm_pingpong = 1;
-int g_gemm_pp_ablate = 0;
-int g_gemm_pp_dim = 0;
 
 namespace {
 
@@ -49,19 +47,12 @@ constexpr int PP_BM = 256, PP_BN = 256, PP_BK = 64, PP_T = 512;
 constexpr int PP_OP = PP_BM * PP_BK * 2;  // 32 KiB: one operand slice of a stage
 constexpr int PP_STAGE = 2 * PP_OP;       // 64 KiB
 constexpr int PP_BIAS = 2 * PP_STAGE;     // bias area: 8 waves x 256 B
-constexpr int PP_PF = PP_BIAS + 8 * 256;  // residual-prefetch sink: 8 waves x 1 KiB, never read
-constexpr int PP_LDS = PP_PF + 8 * 1024;
+constexpr int PP_LDS = PP_BIAS + 8 * 256;
 
 __device__ __forceinline__ int pp_swz(int row) { return (row >> 1) & 7; }
 
 __device__ __forceinline__ bf16x8 pp_frag(const char* op, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(op + row * 128 + ((chunk ^ pp_swz(row)) << 4));
-}
-
-template <int N_IN_FLIGHT, int ABL = 0>
-__device__ __forceinline__ void pp_wait_vm_loop() {
-  if constexpr ((ABL & 1) == 0)
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N_IN_FLIGHT) : "memory");
 }
 
 template <int N_IN_FLIGHT>
@@ -223,16 +214,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
   }
 }
 
-// ABL (timing ablations, WRONG results when non-zero; EPI_BF16 only): bit0 no vmcnt waits in the
-// K-loop, bit1 no steady-state DMA, bit2 no fragment re-reads after the first K-step, bit3 no barriers
-// in the K-loop.
-// DIM: the DMA pieces of a phase are issued inside the issuing wave's MFMA segment (see below).
-// PF (EPI_RESID_F32 at short K): the residual tile is prefetched during the K-loop -- two 1-KiB
-// LDS-DMA row reads per K-step and wave into a sink area that is never read -- so the epilogue's
-// read-modify-write hits the L2 / Infinity Cache instead of paying HBM latency and bandwidth at the
-// moment every CU reaches its epilogue.  The two prefetch DMAs sit in phase 2 (after P1), so the
-// phase-0 and phase-3 waits count two more younger operations.
-template <int EPI, int ABL = 0, bool DIM = false, bool PF = false>
+template <int EPI>
 __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -264,7 +246,6 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, p.bias ? p.N * 4 : 0, 0x00020000);
 
-  bool g_abl_started = false;  // ablation builds: the prologue DMA has landed
   // DMA issue cursor: (tile, k) of the next stage to load and this lane's source offsets for
   // that tile.  Past the end it stays on the last stage (re-loaded into the idle buffer), which
   // keeps every wait count uniform.
@@ -285,9 +266,6 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   };
   set_tile_ptrs(0);
   auto issue = [&](int i, int slot) {
-    if constexpr ((ABL & 2) != 0) {
-      if (g_abl_started) return;
-    }
     char* dst = smem + slot * PP_STAGE + (pp_slot_is_w(i) ? PP_OP : 0) + pp_group_row(wave, i) * 128;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(pp_slot_is_w(i) ? rsW : rsA, MQ_LDS_LOCAL(dst), 16, voff[i],
                                              iss_k * PP_BK * 2, 0, 0);
@@ -328,182 +306,17 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     __builtin_amdgcn_s_setprio(0);
   };
   // barrier that opens an MFMA segment: the segment's fragment reads are complete
-  auto bar = [&]() {
-    if constexpr ((ABL & 8) == 0) pp_barrier();
-  };
+  auto bar = [&]() { pp_barrier(); };
   auto open_mfma = [&]() {
     bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
-  if constexpr (DIM) {
-    // DMA-in-MFMA schedule: each phase's DMA pieces are issued between the issuing wave's own MFMAs
-    // (after MFMA 4/8/12 or 6/12 of the quadrant) instead of in its load segment, so the TA issue cost
-    // of a piece overlaps the wave's MFMA stream and the partner's load segment holds only fragment
-    // reads.  Every piece lands one segment later than in the base schedule; waits: phase 0
-    // vmcnt(2) retires P1(g), phase 1 vmcnt(3) P2(g), phase 3 vmcnt(2) P0(g+1).
-    auto mf = [&](int qm, int qn, bf16x8 (&bb)[2][2], int t) {
-      const int kk = t >> 3, i = (t >> 1) & 3, j = t & 1;
-      acc[qm * 4 + i][qn * 2 + j] =
-          __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][kk], a[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
-    };
-#pragma unroll
-    for (int i = 0; i < 8; ++i) issue(i, 0);
-    advance();
-    pp_wait_vm<4>();
-    pp_barrier();
-    if (wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
-    constexpr int EPI_OPS_D = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
-    bool pend = false;
-    for (int g = 0; g < total; ++g) {
-      const int slot = g & 1;
-      const char* As = smem + slot * PP_STAGE;
-      const char* Ws = As + PP_OP;
-      // ---- phase 0: quadrant (0,0); DMA P0 slots 0,1 + bias inside the MFMA segment
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) b0[j][kk] = pp_frag(Ws, wn * 64 + j * 16 + frow, kk * 4 + fk);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, wm * 128 + i * 16 + frow, kk * 4 + fk);
-      }
-      if (pend)
-        pp_wait_vm<2 + EPI_OPS_D>();
-      else
-        pp_wait_vm<2>();
-      open_mfma();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) mf(0, 0, b0, t);
-      issue(0, slot ^ 1);
-#pragma unroll
-      for (int t = 4; t < 8; ++t) mf(0, 0, b0, t);
-      issue(1, slot ^ 1);
-#pragma unroll
-      for (int t = 8; t < 12; ++t) mf(0, 0, b0, t);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
-#pragma unroll
-      for (int t = 12; t < 16; ++t) mf(0, 0, b0, t);
-      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-      __builtin_amdgcn_s_setprio(0);
-      bar();
-      // ---- phase 1: quadrant (0,1); DMA P0 slots 2,3
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) b1[j][kk] = pp_frag(Ws, wn * 64 + 32 + j * 16 + frow, kk * 4 + fk);
-      if (pend)
-        pp_wait_vm<3 + EPI_OPS_D>();
-      else
-        pp_wait_vm<3>();
-      pend = false;
-      open_mfma();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int t = 0; t < 6; ++t) mf(0, 1, b1, t);
-      issue(2, slot ^ 1);
-#pragma unroll
-      for (int t = 6; t < 12; ++t) mf(0, 1, b1, t);
-      issue(3, slot ^ 1);
-#pragma unroll
-      for (int t = 12; t < 16; ++t) mf(0, 1, b1, t);
-      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-      __builtin_amdgcn_s_setprio(0);
-      bar();
-      // ---- phase 2: quadrant (1,0); DMA P1 slots 4,5
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
-      open_mfma();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int t = 0; t < 6; ++t) mf(1, 0, b0, t);
-      issue(4, slot ^ 1);
-#pragma unroll
-      for (int t = 6; t < 12; ++t) mf(1, 0, b0, t);
-      issue(5, slot ^ 1);
-#pragma unroll
-      for (int t = 12; t < 16; ++t) mf(1, 0, b0, t);
-      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-      __builtin_amdgcn_s_setprio(0);
-      bar();
-      // ---- phase 3: quadrant (1,1); DMA P2 slots 6,7
-      pp_wait_vm<2>();
-      open_mfma();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int t = 0; t < 6; ++t) mf(1, 1, b1, t);
-      issue(6, slot ^ 1);
-#pragma unroll
-      for (int t = 6; t < 12; ++t) mf(1, 1, b1, t);
-      issue(7, slot ^ 1);
-#pragma unroll
-      for (int t = 12; t < 16; ++t) mf(1, 1, b1, t);
-      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 6, 0);
-      __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-      __builtin_amdgcn_s_setprio(0);
-      bar();
-      advance();
-      if (++kt == nk) {
-        pp_epilogue<EPI>(p, acc, reinterpret_cast<const float*>(bias_lds), cm0, cn0, wm, wn, lane);
-        pend = (cm0 + PP_BM <= p.M) && (cn0 + PP_BN <= p.N);
-        kt = 0;
-        ++ct;
-        if (ct < my_tiles) {
-          pp_tile_coords(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
-          bias_off = (unsigned)((cn0 + wn * 64 + lane) * 4);
-        }
-      }
-    }
-    if (wm == 0) pp_barrier();  // balance the stagger
-    pp_wait_vm<0>();            // no DMA may outlive the block
-    return;
-  }
-
-  const __amdgpu_buffer_rsrc_t rsC =
-      __builtin_amdgcn_make_buffer_rsrc(p.C, 0, PF ? (int)((size_t)p.M * p.ldc * 4) : 0, 0x00020000);
-  char* pf_sink = smem + PP_PF + wave * 1024;
-  // prefetch rows 2*kt, 2*kt+1 (mod 32) of this wave's 32 rows of the compute tile's residual
-  auto prefetch = [&]() {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int row = cm0 + wave * 32 + ((2 * kt + r) & 31);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsC, MQ_LDS_LOCAL(pf_sink), 16,
-                                               (unsigned)(((size_t)row * p.ldc + cn0) * 4 + lane * 16), 0, 0, 0);
-    }
-  };
-  constexpr int NPF = PF ? 2 : 0;
-
   // prologue: stage 0 into buffer 0; P0 (the 4 oldest DMAs) must land before the first reads
 #pragma unroll
-  for (int i = 0; i < 6; ++i) issue(i, 0);
-  if constexpr (PF) prefetch();  // keeps the phase-0 wait count of the first K-step uniform
-  issue(6, 0);
-  issue(7, 0);
+  for (int i = 0; i < 8; ++i) issue(i, 0);
   advance();
-  pp_wait_vm<4 + NPF>();
-  if constexpr (ABL != 0) {
-    pp_wait_vm<0>();
-    g_abl_started = true;
-  }
+  pp_wait_vm<4>();
   pp_barrier();
   if (wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
 
@@ -519,19 +332,18 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        if (!(ABL & 4) || g == 0) b0[j][kk] = pp_frag(Ws, wn * 64 + j * 16 + frow, kk * 4 + fk);
+        b0[j][kk] = pp_frag(Ws, wn * 64 + j * 16 + frow, kk * 4 + fk);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (!(ABL & 4) || g == 0) a[i][kk] = pp_frag(As, wm * 128 + i * 16 + frow, kk * 4 + fk);
+        a[i][kk] = pp_frag(As, wm * 128 + i * 16 + frow, kk * 4 + fk);
     }
     issue(0, slot ^ 1);
     issue(1, slot ^ 1);
-    if constexpr ((ABL & 2) == 0)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
     if (stores_pending)
-      pp_wait_vm_loop<5 + NPF + EPI_OPS, ABL>();
+      pp_wait_vm<5 + EPI_OPS>();
     else
-      pp_wait_vm_loop<5 + NPF, ABL>();
+      pp_wait_vm<5>();
     open_mfma();
     mfma_quadrant(0, 0, b0);
     bar();
@@ -540,13 +352,13 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        if (!(ABL & 4) || g == 0) b1[j][kk] = pp_frag(Ws, wn * 64 + 32 + j * 16 + frow, kk * 4 + fk);
+        b1[j][kk] = pp_frag(Ws, wn * 64 + 32 + j * 16 + frow, kk * 4 + fk);
     issue(2, slot ^ 1);
     issue(3, slot ^ 1);
     if (stores_pending)
-      pp_wait_vm_loop<5 + EPI_OPS, ABL>();
+      pp_wait_vm<5 + EPI_OPS>();
     else
-      pp_wait_vm_loop<5, ABL>();
+      pp_wait_vm<5>();
     stores_pending = false;
     open_mfma();
     mfma_quadrant(0, 1, b1);
@@ -556,10 +368,9 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (!(ABL & 4) || g == 0) a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
+        a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
     issue(4, slot ^ 1);
     issue(5, slot ^ 1);
-    if constexpr (PF) prefetch();
     open_mfma();
     mfma_quadrant(1, 0, b0);
     bar();
@@ -567,7 +378,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     issue(6, slot ^ 1);
     issue(7, slot ^ 1);
     advance();
-    pp_wait_vm_loop<4 + NPF, ABL>();
+    pp_wait_vm<4>();
     open_mfma();
     mfma_quadrant(1, 1, b1);
     bar();
@@ -586,66 +397,35 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-template <int EPI, int ABL = 0, bool DIM = false, bool PF = false>
-void launch_pp1(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
+template <int EPI>
+void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, ABL, DIM, PF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, ABL, DIM, PF>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
-}
-
-template <int EPI, int ABL = 0>
-void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
-  if (ABL == 0 && g_gemm_pp_dim)
-    launch_pp1<EPI, 0, true>(grid, stream, p, tiles_m, tiles_n);
-  else
-    launch_pp1<EPI, ABL, false>(grid, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
 }
 
 }  // namespace
 
 // Routing: every 256x256 GEMM with K % 64 == 0, except the f32 residual read-modify-write at short
 // K (proj, K = 1280: one tile per CU, 20 K-steps), which goes to the interleaved kernel: it measured
-// 8 % faster than the plain ping-pong there (755 vs 692 TFLOP/s; the residual loads stall both wave
-// groups at the tile end) and 13 % faster than the residual-prefetch variant (52.4 vs 59.1 us,
-// MQ_TUNE_GEMM_PP_RESID_PREFETCH 1 routes proj there).  At K = 5120 (fc2) the plain ping-pong wins.
-int g_gemm_pp_resid_pf = 0;
-
+// 8 % faster than the ping-pong there (755 vs 692 TFLOP/s; the residual loads stall both wave
+// groups at the tile end).  At K = 5120 (fc2) the ping-pong wins.
 bool gemm_pingpong_fits(const GemmArgs& p, int epi) {
-  return g_gemm_pingpong && epi != EPI_NCHW_F32 && !(epi == EPI_RESID_F32 && p.K < 2048 && !g_gemm_pp_resid_pf) &&
-         p.K > 0 &&
-         p.K % PP_BK == 0 &&
-         (size_t)p.M * p.lda * 2 < (1ull << 31) && (size_t)p.N * p.ldw * 2 < (1ull << 31);
+  return g_gemm_pingpong && epi != EPI_NCHW_F32 && !(epi == EPI_RESID_F32 && p.K < 2048) && p.K > 0 &&
+         p.K % PP_BK == 0 && (size_t)p.M * p.lda * 2 < (1ull << 31) && (size_t)p.N * p.ldw * 2 < (1ull << 31);
 }
 
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
   const int tiles_m = (p.M + PP_BM - 1) / PP_BM, tiles_n = (p.N + PP_BN - 1) / PP_BN;
   const int tiles = tiles_m * tiles_n;
   dim3 grid(tiles < num_cus ? tiles : num_cus);
-  if (g_gemm_pp_ablate && epi == EPI_BF16) {
-    switch (g_gemm_pp_ablate) {
-      case 1: launch_pp<EPI_BF16, 1>(grid, stream, p, tiles_m, tiles_n); break;
-      case 2: launch_pp<EPI_BF16, 2>(grid, stream, p, tiles_m, tiles_n); break;
-      case 3: launch_pp<EPI_BF16, 3>(grid, stream, p, tiles_m, tiles_n); break;
-      case 4: launch_pp<EPI_BF16, 4>(grid, stream, p, tiles_m, tiles_n); break;
-      case 8: launch_pp<EPI_BF16, 8>(grid, stream, p, tiles_m, tiles_n); break;
-      case 15: launch_pp<EPI_BF16, 15>(grid, stream, p, tiles_m, tiles_n); break;
-      default: return -3;
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -4;
-  }
   switch (epi) {
     case EPI_BF16: launch_pp<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RESID_F32:
-      if (p.K < 2048 && (size_t)p.M * p.ldc * 4 < (1ull << 31))
-        launch_pp1<EPI_RESID_F32, 0, false, true>(grid, stream, p, tiles_m, tiles_n);
-      else
-        launch_pp<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n);
-      break;
+    case EPI_RESID_F32: launch_pp<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_POS_F32: launch_pp<EPI_POS_F32>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_F32: launch_pp<EPI_F32>(grid, stream, p, tiles_m, tiles_n); break;
     default: return -3;

@@ -26,28 +26,17 @@ struct GemmArgs {
 };
 
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
-extern int g_gemm_stages;
-extern int g_gemm_ablate;
-extern int g_gemm_bufload;
-extern int g_gemm_mfma32;
-extern int g_gemm_sched;
-extern int g_gemm_bm128;
-extern int g_gemm_prio;
-extern int g_gemm_sync2;
-extern bool g_gemm_force_small;
+// routing knobs (mq_set_tuning): both settings give correct results
+extern bool g_gemm_force_small;  // every GEMM on the 128x128 kernel
 // ping-pong 256x256 kernel (gemm_pp.hip): the two wave groups of a block alternate LDS traffic and MFMA
 extern int g_gemm_pingpong;
-extern int g_gemm_pp_ablate;
-extern int g_gemm_pp_dim;
-extern int g_gemm_pp_resid_pf;
 bool gemm_pingpong_fits(const GemmArgs& p, int epi);
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
                        float eps, hipStream_t s);
-extern int g_attention_ablate;
-extern int g_attention_persist;
+extern int g_attention_v2;  // 1 (default): attention2_kernel; 0: the first-generation kernel
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s);
 int patch_im2col(const float* crops, unsigned short* A, int n_crops, int flip_copies, int img_h, int img_w,

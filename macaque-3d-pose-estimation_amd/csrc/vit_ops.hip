@@ -91,10 +91,9 @@ struct AttLayout {
   static constexpr int LDS = KBYTES + VBYTES;
 };
 
-// MODE (timing ablations only, results are wrong when non-zero): 1 = staging only, 3 = no output
-// stores.  TT: compile-time token count (192 = the ViT-H 256x192 grid) so every per-block guard
+// TT: compile-time token count (192 = the ViT-H 256x192 grid) so every per-block guard
 // folds away; 0 = runtime T (other grids / tests).
-template <int DH, int MODE = 0, int TT = 0>
+template <int DH, int TT = 0>
 __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t* __restrict__ qkv,
                                                                     bf16_t* __restrict__ out, int T_rt, int D,
                                                                     int H, float scale_log2) {
@@ -148,10 +147,6 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t*
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (MODE == 1) {
-    if (threadIdx.x == 0) out[row0 * D + h * DH] = *reinterpret_cast<const bf16_t*>(Kimg + 16 * wave) + qf[0][0][0];
-    return;
-  }
   if (wave >= ntb) return;
   const bool has1 = (TT == MAXT) ? true : (wave + ATT_WAVES < ntb);
 
@@ -249,139 +244,126 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t*
       const float inv = 1.0f / __shfl(lsum[u], 4 * g + e, 64);
       const int qq = qb * 16 + 4 * g + e;
       bf16_t* orow = out + (row0 + qq) * D + h * DH;
-      if constexpr (MODE == 3) {
-        float acc3 = 0.f;
 #pragma unroll
-        for (int dt = 0; dt < NKS; ++dt) acc3 += O[u][dt][e] * inv;
-        if (acc3 == 12345.678f) orow[l16] = 1;
-      } else {
-#pragma unroll
-        for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = __builtin_bit_cast(bf16_t, (__bf16)(O[u][dt][e] * inv));
-      }
+      for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = __builtin_bit_cast(bf16_t, (__bf16)(O[u][dt][e] * inv));
     }
   }
 }
 
-// Persistent variant for the ViT grid (T = 192): 2 workgroups per CU walk (image, head) items with
-// stride gridDim.x and overlap the next item's staging with the current item's compute inside one
-// LDS footprint: K is refilled (LDS-DMA) right after every wave has finished S^T = K Q^T; V is
-// refilled and the next item's Q fragments loaded after P V.  The staging
-// of item i+1 therefore runs under item i's softmax, P V and output stores instead of in lockstep
-// with the co-resident workgroup's.  Same arithmetic as attention_kernel (bit-identical outputs).
-// Waits: all staging of an item is retired by a counted vmcnt at the loop head that leaves the 40
-// output stores of the previous item in flight.
-int g_attention_persist = 0;
+// ---------------------------------------------------------------- attention, version 2
+// Same work split (one 6-wave workgroup per (image, head), two 16-query blocks per wave, K/V
+// staged whole in LDS by LDS-DMA, Q fragments straight to registers), rebuilt around the gfx950
+// MFMA forms and the output path:
+//   S^T = K Q^T   v_mfma_f32_16x16x32_bf16: ceil(DH/32) k-steps of 32 (the last one half
+//                 zero-padded on the Q side when DH % 32 == 16) instead of DH/16 steps of the
+//                 half-rate 16x16x16 form.  K image rows of 10 x 16-B chunks (80 d = 160 B, no
+//                 pad): the ds_read_b128 lane groups of the A-operand pattern hit 16 distinct
+//                 slots, conflict-free.
+//   softmax       in registers; row max by 3-input max, sum by plain adds, 2 cross-lane steps.
+//   O^T = V^T P^T v_mfma_f32_16x16x32_bf16 with V^T as the A operand (the same ds_read_b64_tr_b16
+//                 gather as before) and P as the B operand: the output lands with the query on the
+//                 lane and 4 consecutive d per lane, so the 1/l normalisation needs no cross-lane
+//                 step and a v_permlane16_swap pairs neighbouring d runs into 16-B row stores.
+constexpr int ATT2_KCH = 10;  // K image row stride in 16-B chunks (DH <= 80)
 
-template <int DH>
-__global__ __launch_bounds__(ATT_THREADS, 3) void attention_persist_kernel(const bf16_t* __restrict__ qkv,
-                                                                            bf16_t* __restrict__ out, int D, int H,
-                                                                            float scale_log2, int n_items) {
+template <int DH, int TT = 0>
+__global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t* __restrict__ qkv,
+                                                                     bf16_t* __restrict__ out, int T_rt, int D,
+                                                                     int H, float scale_log2) {
   using L = AttLayout<DH>;
-  constexpr int T = ATT_MAXT;
-  constexpr int NKS = DH / 16;
-  constexpr int DCH = DH / 8;
-  constexpr int NTB = T / 16;
+  const int T = TT ? TT : T_rt;
+  constexpr int NKS = (DH + 31) / 32;   // 16x16x32 k-steps of QK^T
+  constexpr bool HALF = (DH % 32) == 16;  // last k-step carries 16 real d
+  constexpr int NDT = DH / 16;          // 16-wide d blocks of O
+  constexpr int DCH = DH / 8;           // data chunks per row
+  constexpr int KCH = ATT2_KCH;
+  constexpr int MAXT = ATT_MAXT;
+  constexpr int KBYTES = (MAXT * KCH + 63) / 64 * 1024;
+  static_assert(DCH <= KCH, "K image row too short");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
-  char* Vimg = smem + L::KBYTES;
-  int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int l16 = lane & 15, g = lane >> 4;
+  char* Vimg = smem + KBYTES;
+
+  const int img = blockIdx.x / H, h = blockIdx.x % H;
+  const size_t row0 = (size_t)img * T;
   const int ld = 3 * D;
-  constexpr int nk_ins = (T * L::KCH + 63) / 64, nv_ins = (T * L::VCH + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g = lane >> 4;
+  const int ntb = T / 16;
 
-  auto issue_k = [&](int it) {
-    const int img = it / H, h = it % H;
-    const bf16_t* kbase = qkv + (size_t)img * T * ld + D + h * DH;
-    for (int ins = wave; ins < nk_ins; ins += ATT_WAVES) {
-      const int q = ins * 64 + lane;
-      int t = q / L::KCH, ch = q - (q / L::KCH) * L::KCH;
-      if (t >= T || ch >= DCH) t = 0, ch = 0;
-      __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(kbase + (size_t)t * ld + ch * 8),
-                                       MQ_LDS_LOCAL(Kimg + ins * 1024), 16, 0, 0);
-    }
-  };
-  auto issue_v = [&](int it) {
-    const int img = it / H, h = it % H;
-    const bf16_t* vbase = qkv + (size_t)img * T * ld + 2 * D + h * DH;
-    for (int ins = wave; ins < nv_ins; ins += ATT_WAVES) {
-      const int q = ins * 64 + lane;
-      int t = q / L::VCH, ch = q - (q / L::VCH) * L::VCH;
-      if (t >= T || ch >= DCH) t = 0, ch = 0;
-      __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(vbase + (size_t)t * ld + ch * 8),
-                                       MQ_LDS_LOCAL(Vimg + ins * 1024), 16, 0, 0);
-    }
-  };
-  short4v qf[2][NKS];
-  auto load_q = [&](int it) {
-    const int img = it / H, h = it % H;
+  const bf16_t* kbase = qkv + row0 * ld + D + h * DH;
+  const bf16_t* vbase = kbase + D;
+  const int nk_ins = (T * KCH + 63) / 64, nv_ins = (T * L::VCH + 63) / 64;
+  for (int ins = wave; ins < nk_ins; ins += ATT_WAVES) {
+    const int q = ins * 64 + lane;
+    int t = q / KCH, ch = q - (q / KCH) * KCH;
+    if (t >= T || ch >= DCH) t = 0, ch = 0;
+    __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(kbase + (size_t)t * ld + ch * 8), MQ_LDS_LOCAL(Kimg + ins * 1024),
+                                     16, 0, 0);
+  }
+  for (int ins = wave; ins < nv_ins; ins += ATT_WAVES) {
+    const int q = ins * 64 + lane;
+    int t = q / L::VCH, ch = q - (q / L::VCH) * L::VCH;
+    if (t >= T || ch >= DCH) t = 0, ch = 0;
+    __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(vbase + (size_t)t * ld + ch * 8), MQ_LDS_LOCAL(Vimg + ins * 1024),
+                                     16, 0, 0);
+  }
+  // Q^T fragments (B operand: k = d 32 ks + 8 g + j, column = query l16); d >= DH is zero
+  bf16x8 qf[2][NKS];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int q = (wave + u * ATT_WAVES) * 16 + l16;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks)
-        qf[u][ks] = *reinterpret_cast<const short4v*>(qkv + ((size_t)img * T + q) * ld + h * DH + ks * 16 + 4 * g);
-    }
-  };
-
-  int item = blockIdx.x;
-  if (item >= n_items) return;
-  issue_k(item);
-  issue_v(item);
-  load_q(item);
-  bool first = true;
-  for (; item < n_items; item += gridDim.x) {
-    const int next = item + gridDim.x;
-    const bool has_next = next < n_items;
-    // opaque per item: keeps the compiler from hoisting the many lane-derived LDS addresses out of
-    // the item loop (they would stay live through it and spill)
-    asm volatile("" : "+v"(lane));
-    l16 = lane & 15;
-    g = lane >> 4;
-    // this item's K, V and Q have landed (the previous item's 40 output stores may stay in flight)
-    if (first)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(40)" ::: "memory");
-    first = false;
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-
-    f32x4 S[2][NTB];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int tb = 0; tb < NTB; ++tb) S[u][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = 0; u < 2; ++u) {
+    const int qb = min(wave + u * ATT_WAVES, ntb - 1);
+    const bf16_t* qrow = qkv + (row0 + qb * 16 + l16) * ld + h * DH;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
+      if (HALF && ks == NKS - 1 && g >= 2)
+        qf[u][ks] = bf16x8{};
+      else
+        qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (wave >= ntb) return;
+  const bool has1 = (TT == MAXT) ? true : (wave + ATT_WAVES < ntb);
+
+  f32x4 S[2][MAXT / 16];
 #pragma unroll
-      for (int tb = 0; tb < NTB; ++tb) {
-        const short4v kf =
-            *reinterpret_cast<const short4v*>(Kimg + (tb * 16 + l16) * (L::KCH * 16) + (ks * 16 + 4 * g) * 2);
-        S[0][tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[0][ks], S[0][tb], 0, 0, 0);
-        S[1][tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[1][ks], S[1][tb], 0, 0, 0);
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int tb = 0; tb < MAXT / 16; ++tb) S[u][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int chunk = (HALF && ks == NKS - 1) ? 4 * ks + (g & 1) : 4 * ks + g;
+#pragma unroll
+    for (int tb = 0; tb < MAXT / 16; ++tb) {
+      if (tb < ntb) {
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kimg + (tb * 16 + l16) * (KCH * 16) + chunk * 16);
+        S[0][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ks], S[0][tb], 0, 0, 0);
+        if (has1) S[1][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ks], S[1][tb], 0, 0, 0);
       }
     }
-    // every wave's K reads are consumed (the MFMAs above waited for them): refill K, reload Q
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (has_next) issue_k(next);
-
-    bf16x8 P[2][T / 32];
-    float lsum[2];
+  }
+  // softmax over the tokens of query l16: registers hold tokens tb*16 + 4 g + e
+  bf16x8 P[2][MAXT / 32];
+  float linv[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      float m = -INFINITY;
+  for (int u = 0; u < 2; ++u) {
+    float m = -INFINITY;
 #pragma unroll
-      for (int tb = 0; tb < NTB; ++tb)
-        m = fmaxf(m, fmaxf(fmaxf(S[u][tb][0], S[u][tb][1]), fmaxf(S[u][tb][2], S[u][tb][3])));
-      m = fmaxf(m, __shfl_xor(m, 16, 64));
-      m = fmaxf(m, __shfl_xor(m, 32, 64));
-      const float mb = m * scale_log2;
-      float ls = 0.f;
+    for (int tb = 0; tb < MAXT / 16; ++tb)
+      if (tb < ntb) {
+        m = fmaxf(m, fmaxf(S[u][tb][0], S[u][tb][1]));
+        m = fmaxf(m, fmaxf(S[u][tb][2], S[u][tb][3]));
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float mb = m * scale_log2;
+    float ls = 0.f;
 #pragma unroll
-      for (int tb = 0; tb < NTB; ++tb) {
+    for (int tb = 0; tb < MAXT / 16; ++tb) {
+      if (tb < ntb) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float pv = __builtin_amdgcn_exp2f(S[u][tb][e] * scale_log2 - mb);
@@ -389,29 +371,34 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_persist_kernel(const
           ls += pv;
         }
       }
-      ls += __shfl_xor(ls, 16, 64);
-      ls += __shfl_xor(ls, 32, 64);
-      lsum[u] = ls;
+    }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    linv[u] = 1.0f / ls;
+    // B operand of P^T: element j of lane group g = token 32 kst + 16 (j >> 2) + 4 g + (j & 3)
 #pragma unroll
-      for (int kst = 0; kst < T / 32; ++kst) {
+    for (int kst = 0; kst < MAXT / 32; ++kst) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          P[u][kst][e] = (__bf16)S[u][2 * kst][e];
-          P[u][kst][4 + e] = (__bf16)S[u][2 * kst + 1][e];
-        }
+      for (int e = 0; e < 4; ++e) {
+        P[u][kst][e] = (__bf16)S[u][2 * kst][e];
+        P[u][kst][4 + e] = (__bf16)S[u][2 * kst + 1][e];
       }
     }
+  }
 
-    f32x4 O[2][NKS];
+  f32x4 O[2][NDT];
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+  for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int dt = 0; dt < NKS; ++dt) O[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int trq = l16 >> 2, trp = l16 & 3;
+    for (int dt = 0; dt < NDT; ++dt) O[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // V^T (A operand, row = d, k = the token order of P): transposed read, lane 4q+p of each 16-lane
+  // group addresses token row r0+q, columns c0+4p..+3 and receives column c0 + (lane & 15)
+  const int trq = l16 >> 2, trp = l16 & 3;
 #pragma unroll
-    for (int kst = 0; kst < T / 32; ++kst) {
+  for (int kst = 0; kst < MAXT / 32; ++kst) {
+    if (kst < T / 32) {
 #pragma unroll
-      for (int dt = 0; dt < NKS; ++dt) {
+      for (int dt = 0; dt < NDT; ++dt) {
         const int ra = 2 * kst * 16 + 4 * g + trq;
         const char* pa = Vimg + ra * (L::VCH * 16) + (dt * 16 + 4 * trp) * 2;
         const short4v v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -423,72 +410,61 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_persist_kernel(const
         const short4v* pv1 = &v1;
         __builtin_memcpy(&vb, pv0, 8);
         __builtin_memcpy(reinterpret_cast<char*>(&vb) + 8, pv1, 8);
-        O[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[0][kst], vb, O[0][dt], 0, 0, 0);
-        O[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[1][kst], vb, O[1][dt], 0, 0, 0);
-      }
-    }
-    // every wave's V reads are consumed: refill V; the Q registers are free again (loading the next
-    // Q right after S^T would keep 20 more VGPRs live through softmax and P V: scratch spills)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (has_next) {
-      issue_v(next);
-      load_q(next);
-    }
-
-    const int img = item / H, h = item % H;
-    const size_t row0 = (size_t)img * T;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int qb = wave + u * ATT_WAVES;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float inv = 1.0f / __shfl(lsum[u], 4 * g + e, 64);
-        const int qq = qb * 16 + 4 * g + e;
-        bf16_t* orow = out + (row0 + qq) * D + h * DH;
-#pragma unroll
-        for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = __builtin_bit_cast(bf16_t, (__bf16)(O[u][dt][e] * inv));
+        O[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb, P[0][kst], O[0][dt], 0, 0, 0);
+        if (has1) O[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb, P[1][kst], O[1][dt], 0, 0, 0);
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // O^T C-layout: column = query l16, rows 4 g + e = d within the 16-block dt.  Pairs (dt, dt+1):
+  // after v_permlane16_swap even groups hold d 16 dt + 4 g + 0..7, odd groups 16 (dt+1) + 4 (g-1) + 0..7.
+  const bool odd = g & 1;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (u == 1 && !has1) break;
+    const int q = (wave + u * ATT_WAVES) * 16 + l16;
+    bf16_t* orow = out + (row0 + q) * D + h * DH;
+    const float inv = linv[u];
+#pragma unroll
+    for (int dp = 0; dp + 1 < NDT; dp += 2) {
+      unsigned pk[2][2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        pk[hh][0] = pack_bf16x2(O[u][dp + hh][0] * inv, O[u][dp + hh][1] * inv);
+        pk[hh][1] = pack_bf16x2(O[u][dp + hh][2] * inv, O[u][dp + hh][3] * inv);
+      }
+      const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+      const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      *reinterpret_cast<uint4*>(orow + (dp + (odd ? 1 : 0)) * 16 + 4 * (g - (odd ? 1 : 0))) = o;
+    }
+    if constexpr (NDT & 1) {
+      constexpr int dt = NDT - 1;
+      const uint2 o = make_uint2(pack_bf16x2(O[u][dt][0] * inv, O[u][dt][1] * inv),
+                                 pack_bf16x2(O[u][dt][2] * inv, O[u][dt][3] * inv));
+      *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * g) = o;
+    }
+  }
 }
 
-int g_attention_ablate = 0;
+int g_attention_v2 = 1;
 
 template <int DH>
 static void launch_attention(dim3 grid, dim3 block, hipStream_t s, const unsigned short* qkv, unsigned short* out,
                              int tokens, int dim, int heads, float scale_log2) {
   constexpr int lds = AttLayout<DH>::LDS;
-  if (tokens == ATT_MAXT && g_attention_persist && g_attention_ablate == 0) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)attention_persist_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                lds);
-      attr = true;
-    }
-    static int n_cus = 0;
-    if (!n_cus) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !n_cus) n_cus = 256;
-    }
-    const int n_items = (int)grid.x;
-    const int wgs = n_items < 2 * n_cus ? n_items : 2 * n_cus;  // two resident workgroups per CU
-    hipLaunchKernelGGL((attention_persist_kernel<DH>), dim3(wgs), block, lds, s, qkv, out, dim, heads, scale_log2,
-                       n_items);
+  if (g_attention_v2) {
+    constexpr int lds2 = (ATT_MAXT * ATT2_KCH + 63) / 64 * 1024 + AttLayout<DH>::VBYTES;
+    if (tokens == ATT_MAXT)
+      hipLaunchKernelGGL((attention2_kernel<DH, ATT_MAXT>), grid, block, lds2, s, qkv, out, tokens, dim, heads,
+                         scale_log2);
+    else
+      hipLaunchKernelGGL((attention2_kernel<DH, 0>), grid, block, lds2, s, qkv, out, tokens, dim, heads, scale_log2);
     return;
   }
-  if (tokens == ATT_MAXT) {
-    switch (g_attention_ablate) {
-      case 1: hipLaunchKernelGGL((attention_kernel<DH, 1, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
-      case 3: hipLaunchKernelGGL((attention_kernel<DH, 3, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2); break;
-      default: hipLaunchKernelGGL((attention_kernel<DH, 0, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
-    }
-  } else {
-    hipLaunchKernelGGL((attention_kernel<DH, 0, 0>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
-  }
+  if (tokens == ATT_MAXT)
+    hipLaunchKernelGGL((attention_kernel<DH, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+  else
+    hipLaunchKernelGGL((attention_kernel<DH, 0>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
 }
 
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,

@@ -107,8 +107,9 @@ def stream_ptr(device=None):
 
 
 def apply_tuning_env(lib) -> None:
-    """MQ_TUNING="key=value,key=value" (include/mq_hip.h MQ_TUNE_* keys): kernel-variant knobs for
-    A/B runs of the unchanged bench / tests; unset means the library defaults."""
+    """MQ_TUNING="key=value,key=value" (include/mq_hip.h MQ_TUNE_* keys): kernel-routing knobs for
+    A/B runs in the measurement tools (tools/).  Product code never reads the environment: every
+    knob the library accepts gives the same results, but nothing is switched behind a caller."""
     spec = os.environ.get("MQ_TUNING", "").strip()
     if not spec:
         return
@@ -131,7 +132,6 @@ class Context:
         h = C.c_void_p()
         check(self.lib.mq_create(device, C.byref(h)), "mq_create")
         self.handle = h
-        apply_tuning_env(self.lib)
 
     @classmethod
     def get(cls, device: int = 0) -> "Context":

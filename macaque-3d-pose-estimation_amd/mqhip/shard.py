@@ -3,7 +3,9 @@ one collective -- the all-gather of per-view 2D keypoints before the temporally 
 step-4 stages.
 
 Everything per frame (crop -> ViT -> decode -> per-frame triangulation) is rank-local;
-weights are replicated.  ``gather_keypoints`` moves fixed-size per-rank buffers
+weights are replicated.  ``pose_clip_sharded`` is the clip driver of BASELINE config 3: step 1
+over a clip's time steps sharded across ranks, one all-gather, then the sequential per-track
+post-process and (by the caller) step 4 on the gathered keypoints.  ``gather_keypoints`` moves fixed-size per-rank buffers
 ([F_block, C, A, J, 3] f32, zero-padded to the largest block) so the collective is a single
 RCCL all-gather over xGMI (backend "nccl") -- or gloo in the CPU tests.
 """
@@ -33,3 +35,47 @@ def gather_keypoints(kp_local: torch.Tensor, n_frames: int, world: int, group=No
         s, e = frame_block(n_frames, world, r)
         out.append(parts[r][:e - s])
     return torch.cat(out, dim=0)
+
+
+def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, steps_per_batch=8,
+                      kp_params=None, device=None):
+    """BASELINE config 3: the step-1 pose slice of a clip, time steps sharded across ranks.
+
+    Every rank walks the same per-camera time grid (``step1_proc2d.plan_jobs``); rank r runs the
+    ViTPose jobs of its contiguous block of time steps (``frame_block``); one all-gather moves
+    every rank's raw keypoints and scores ([steps, C, boxes, J, 3] float64, padded to the largest
+    block and box count) to every rank, which then runs the sequential KP_THR / EMA / alldata
+    post-process over the whole clip -- the EMA is recursive in time per track, so it runs after
+    the gather and the result equals the single-GPU ``process_stores`` exactly.  Returns what
+    ``process_stores`` returns (per camera: rows per kept frame, frame numbers)."""
+    import numpy as np
+    import torch.distributed as dist
+    from src.pipeline import step1_proc2d as s1
+    kp_params = s1.KP_PARAMS if kp_params is None else kp_params
+    plans, jobs = s1.plan_jobs(stores, T, kp_params)
+    n_steps, C = len(T), len(stores)
+    s0, e0 = frame_block(n_steps, world, rank)
+    raw = s1.run_pose(pose_model, stores, jobs, range(s0, e0), steps_per_batch)
+    J = 17
+    for kp, _ in raw.values():
+        J = kp.shape[1]
+        break
+    nb = max([len(j[2]) for js in jobs.values() for j in js] or [1])
+    block = frame_block(n_steps, world, 0)[1]
+    buf = torch.full((block, C, nb, J, 3), float("nan"), dtype=torch.float64)
+    for (k, c), (kp, sc) in raw.items():
+        buf[k - s0, c, :len(kp), :, :2] = torch.from_numpy(kp)
+        buf[k - s0, c, :len(kp), :, 2] = torch.from_numpy(sc.astype(np.float64))
+    if device is not None:
+        buf = buf.to(device)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    allraw = {}
+    for r in range(world):
+        s, e = frame_block(n_steps, world, r)
+        part = parts[r].cpu().numpy()
+        for k in range(s, e):
+            for (c, _, boxes, _, _) in jobs.get(k, []):
+                v = part[k - s, c, :len(boxes)]
+                allraw[(k, c)] = (v[..., :2].copy(), v[..., 2].astype(np.float32))
+    return s1.assemble_rows(stores, T, plans, jobs, allraw, kp_params)

@@ -14,9 +14,10 @@ per camera.
 
 Out of scope: the Swin Mask R-CNN detector, BoT-SORT tracker and
 ResNet ID classifier, and imgstore video decoding.  Their outputs enter here as
-arguments: per-frame tracker rows ``(N, >=5)`` [x1, y1, x2, y2, track_id, ...]
-and, optionally, ID predictions; without ID predictions every box gets
-``assigned_id = -1`` (the reference's "not confident" value).
+data: per-frame tracker rows ``(N, >=5)`` [x1, y1, x2, y2, track_id, ...] and,
+optionally, ID predictions -- carried by the per-camera ``mqhip.io.FrameStore``
+that ``proc`` reads; without ID predictions every box gets ``assigned_id = -1``
+(the reference's "not confident" value).
 """
 from __future__ import annotations
 
@@ -178,12 +179,145 @@ def process_single_cam(frames, tracks, out_dir, pose_model, frame_numbers=None, 
     return results
 
 
-def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0):
-    """step1.proc (step1:450): needs the detector, tracker and imgstore reader, which are outside
-    this build's scope.  Use process_single_cam / process_frame_multiview
-    with externally produced tracks."""
+def _frame_plan(store, T):
+    """The reference's per-camera walk over the time grid (step1_proc2d.py:210-223): for each t the
+    stored frame nearest in time; a t whose nearest frame is not newer than the last one processed
+    repeats the previous result.  Returns [(frame_number, is_repeat)] per t."""
+    md = store.get_frame_metadata()
+    t_cam, fnums = md["frame_time"], md["frame_number"]
+    plan, frame_number = [], -1
+    for t in T:
+        idx = int(np.abs(t_cam - t).argmin())
+        if frame_number >= fnums[idx]:
+            plan.append((frame_number, True))
+            continue
+        frame_number = int(fnums[idx])
+        plan.append((frame_number, False))
+    return plan
+
+
+def plan_jobs(stores, T, kp_params=KP_PARAMS):
+    """Per camera the time-grid walk (_frame_plan) and, per time step, the pose jobs of the frames
+    it newly reaches: {step: [(cam, frame_number, boxes int32, track ids, expanded boxes f32)]}
+    (degenerate-box filter and margin expansion of step1:254-292)."""
+    plans = [_frame_plan(st, T) for st in stores]
+    jobs = {}
+    for k in range(len(T)):
+        for c, st in enumerate(stores):
+            fn, rep = plans[c][k]
+            if rep:
+                continue
+            boxes, tids = filter_tracks(st.tracks_of(fn))
+            if len(boxes):
+                jobs.setdefault(k, []).append((c, fn, boxes, tids, expand_boxes(boxes, kp_params)))
+    return plans, jobs
+
+
+def run_pose(pose_model, stores, jobs, steps, steps_per_batch=8):
+    """The ViTPose work of the given time steps: every job of ``steps_per_batch`` consecutive steps
+    (all cameras) in ONE batched crop -> ViT -> decode launch sequence per image size.
+    Returns {(step, cam): (keypoints float64 (n, J, 2), scores float32 (n, J))}."""
+    steps = [k for k in steps if k in jobs]
+    raw = {}
+    for b0 in range(0, len(steps), steps_per_batch):
+        by_shape = {}
+        for k in steps[b0:b0 + steps_per_batch]:
+            for (c, fn, _, _, bb) in jobs[k]:
+                img = stores[c].image(fn)
+                by_shape.setdefault(img.shape, []).append(((k, c), img, bb))
+        for items in by_shape.values():
+            out = inference_topdown_batch(pose_model, [im for _, im, _ in items], [bb for _, _, bb in items])
+            for (key, _, _), r in zip(items, out):
+                kp = np.stack([np.asarray(x.pred_instances.keypoints[0], dtype=np.float64) for x in r])
+                sc = np.stack([np.asarray(x.pred_instances.keypoint_scores[0], dtype=np.float32) for x in r])
+                raw[key] = (kp, sc)
+    return raw
+
+
+def _as_results(kp, sc):
+    from types import SimpleNamespace
+    return [SimpleNamespace(pred_instances=SimpleNamespace(keypoints=kp[i][None], keypoint_scores=sc[i][None]))
+            for i in range(len(kp))]
+
+
+def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS):
+    """KP_THR, the recursive per-track EMA and the alldata rows (step1:300-370), per camera in time
+    order, from the pose results of ``run_pose``.  Returns per camera (rows per kept frame, frame
+    numbers) after the reference's "valid frames only" filter."""
+    smoothers = [KeypointSmoother(kp_params) for _ in stores]
+    results = [[] for _ in stores]
+    fnums = [[] for _ in stores]
+    for k in range(len(T)):
+        job_of = {c: j for j in jobs.get(k, []) for c in (j[0],)}
+        for c, st in enumerate(stores):
+            fn, rep = plans[c][k]
+            if rep:
+                results[c].append(results[c][-1] if results[c] else [])
+            elif c not in job_of:  # no tracks / only degenerate boxes in this frame (step1:229-265)
+                results[c].append([])
+            else:
+                _, _, boxes, tids, _ = job_of[c]
+                kp, sc = raw[(k, c)]
+                results[c].append(_rows(_as_results(kp, sc), boxes, tids, smoothers[c], fn, st.id_preds_of(fn),
+                                        kp_params))
+            fnums[c].append(fn)
+    out = []
+    for c, st in enumerate(stores):  # "Save valid frames only" (step1:364-370)
+        valid = set(int(x) for x in st.get_frame_metadata()["frame_number"])
+        keep = [(r, f) for r, f in zip(results[c], fnums[c]) if f in valid]
+        out.append(([r for r, _ in keep], [f for _, f in keep]))
+    return out
+
+
+def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8):
+    """Pose half of step1_proc2d_custom / process_single_cam (step1_proc2d.py:166-447) for every
+    camera at once.  Per camera the reference's time-grid walk, degenerate-box filter, margin
+    expansion, KP_THR and recursive EMA are kept exactly (the EMA state is per camera and runs in
+    time order); the ViTPose work of ``steps_per_batch`` time steps x all cameras goes through ONE
+    batched crop -> ViT -> decode launch sequence (the reference: one inference_topdown per camera
+    frame).  Returns per camera (alldata rows per kept frame, frame numbers)."""
+    plans, jobs = plan_jobs(stores, T, kp_params)
+    raw = run_pose(pose_model, stores, jobs, range(len(T)), steps_per_batch)
+    return assemble_rows(stores, T, plans, jobs, raw, kp_params)
+
+
+def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None, redo=False, pose_model=None,
+                        device_str="cuda:0", steps_per_batch=8):
+    """step1_proc2d.py:389-447 with the frame stores of ``mqhip.io.FrameStore`` and the tracker
+    rows they carry (detector / tracker / ID classifier run upstream).  Writes
+    <results_root>/<data_name>/<cam>/alldata.json and frame_num.npy."""
     import glob
-    if not glob.glob(os.path.join(raw_root, f"{data_name}.*", "metadata.yaml")):
+    from mqhip.io import FrameStore
+    meta_paths = sorted(glob.glob(os.path.join(raw_root, f"{data_name}.*", "metadata.yaml")))
+    if not meta_paths:
         raise FileNotFoundError(f'No imgstore metadata for "{data_name}" in {raw_root}')
-    raise NotImplementedError("detection/tracking/ID (Swin Mask R-CNN, BoT-SORT, ResNet-152) are not part of "
-                              "this build; feed tracker rows to process_single_cam")
+    stores = [FrameStore(os.path.dirname(p)) for p in meta_paths]
+    md0 = stores[0].get_frame_metadata()
+    t0 = md0["frame_time"][0]
+    if t_intv is None:
+        t_start, t_end = t0, md0["frame_time"][-1]
+    else:
+        t_start, t_end = t0 + t_intv[0], t0 + t_intv[1]
+    T = np.arange(t_start, t_end, 1.0 / fps)
+    suffix = "" if t_intv is None else f".{int(t_intv[0]):04d}-{int(t_intv[1]):04d}"
+    out_dirs = [os.path.join(results_root, data_name + suffix, os.path.basename(st.filename).split(".")[-1])
+                for st in stores]
+    todo = [i for i, d in enumerate(out_dirs)
+            if redo or not (os.path.exists(os.path.join(d, "alldata.json"))
+                            and os.path.exists(os.path.join(d, "frame_num.npy")))]
+    if not todo:
+        return
+    if pose_model is None:
+        pose_model = init_pose_model(device=device_str)
+    res = process_stores(pose_model, [stores[i] for i in todo], T, steps_per_batch=steps_per_batch)
+    for i, (rows, fn) in zip(todo, res):
+        os.makedirs(out_dirs[i], exist_ok=True)
+        np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))
+        with open(Path(out_dirs[i]) / "alldata.json", "w") as fp:
+            json.dump(rows, fp)
+
+
+def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0, pose_model=None):
+    """step1.proc (step1_proc2d.py:450): the pose slice over every camera's frame store.  Unlike the
+    reference (which hard-codes cuda:1, step1:50,421) the device argument is honoured."""
+    step1_proc2d_custom(data_name, results_root, raw_root, fps=fps, pose_model=pose_model, device_str=device_str)

@@ -126,3 +126,25 @@ def test_library_is_gfx950_code_object(lib):
 def test_last_error_is_safe_without_gpu(lib):
     # no HIP device here: only touch entry points that do not initialise the runtime
     assert isinstance(lib.mq_last_error(), bytes)
+
+
+def test_tuning_knobs_only_select_equivalent_variants(lib):
+    """mq_set_tuning accepts only routing knobs whose settings are tested equal (GEMM routing,
+    attention version, PCG iterations); the timing-ablation keys of earlier builds (which produced
+    wrong results on purpose) are rejected.  No HIP call is made, so this runs without a GPU."""
+    for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 99):
+        assert lib.mq_set_tuning(key, 1) == -2, key
+        assert lib.mq_get_tuning(key) == -2, key
+    for key, default, other in ((2, 0, 1), (12, 1, 0), (17, 1, 0), (4, 40, 10)):
+        assert lib.mq_get_tuning(key) == default
+        assert lib.mq_set_tuning(key, other) == 0
+        assert lib.mq_get_tuning(key) == other
+        assert lib.mq_set_tuning(key, default) == 0
+    assert lib.mq_set_tuning(4, 0) == -2
+
+
+def test_context_ignores_tuning_environment():
+    """Product code never applies MQ_TUNING (only tools/ call apply_tuning_env)."""
+    import inspect
+    from mqhip import _lib
+    assert "apply_tuning_env" not in inspect.getsource(_lib.Context)

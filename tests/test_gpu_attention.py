@@ -19,8 +19,20 @@ def _ref(qkv, n, T, D, H):
     return (a @ v).permute(0, 2, 1, 3).reshape(n * T, D)
 
 
-@pytest.mark.parametrize("n,T,D,H", [(3, 192, 1280, 16), (2, 192, 768, 12), (2, 64, 320, 4), (1, 96, 1280, 16)])
-def test_attention_matches_fp32(n, T, D, H):
+@pytest.fixture(params=[1, 0], ids=["v2", "v1"])
+def version(request):
+    """MQ_TUNE_ATTENTION_V2 (key 17): the shipped kernel (v2) and the first-generation one (v1)."""
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    old = ctx.lib.mq_get_tuning(17)
+    assert ctx.lib.mq_set_tuning(17, request.param) == 0
+    yield request.param
+    ctx.lib.mq_set_tuning(17, old)
+
+
+@pytest.mark.parametrize("n,T,D,H", [(3, 192, 1280, 16), (2, 192, 768, 12), (2, 64, 320, 4), (1, 96, 1280, 16),
+                                     (64, 192, 1280, 16)])
+def test_attention_matches_fp32(n, T, D, H, version):
     import torch
     from mqhip import _lib
     ctx = _lib.Context.get(0)
@@ -47,28 +59,23 @@ def test_attention_rejects_bad_shapes():
     assert ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), 1, 96, 1280, 10, None) != 0
 
 
-@pytest.mark.parametrize("n", [1, 7, 64])
-def test_attention_persistent_bitwise_equals_per_item(n):
-    """The persistent T=192 kernel (MQ_TUNE_ATTENTION_PERSIST, K/V of the next (image, head) staged
-    under the current one's compute) runs the same arithmetic as the one-workgroup-per-item kernel:
-    outputs must match bit for bit, including grids with fewer items than workgroups."""
+def test_attention_spiky_scores_match_fp32(version):
+    """A few very large keys per query: the row max dominates and most P underflow -- the softmax
+    must still be normalised per query (checks the lane-local 1/l of the transposed output)."""
     import torch
     from mqhip import _lib
     ctx = _lib.Context.get(0)
-    T, D, H = 192, 1280, 16
+    n, T, D, H = 2, 192, 1280, 16
     g = torch.Generator(device="cuda")
-    g.manual_seed(100 + n)
-    qkv = (torch.randn((n * T, 3 * D), generator=g, device="cuda") * 2).to(torch.bfloat16)
-    outs = []
-    old = ctx.lib.mq_get_tuning(15)
-    try:
-        for persist in (0, 1):
-            assert ctx.lib.mq_set_tuning(15, persist) == 0
-            out = torch.full((n * T, D), float("nan"), device="cuda", dtype=torch.bfloat16)
-            _lib.check(ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), n, T, D, H,
-                                                 _lib.stream_ptr()), "mq_attention_bf16")
-            outs.append(out)
-    finally:
-        ctx.lib.mq_set_tuning(15, old)
+    g.manual_seed(5)
+    qkv = torch.randn((n * T, 3 * D), generator=g, device="cuda")
+    qkv[7, D:2 * D] *= 12.0                     # one key row much larger
+    qkv[200, D:2 * D] *= -9.0
+    qkv = qkv.to(torch.bfloat16)
+    out = torch.empty((n * T, D), device="cuda", dtype=torch.bfloat16)
+    _lib.check(ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), n, T, D, H, _lib.stream_ptr()),
+               "mq_attention_bf16")
     torch.cuda.synchronize()
-    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    ref = _ref(qkv, n, T, D, H)
+    vmax = qkv[:, 2 * D:].float().abs().max().item()
+    assert (out.float() - ref).abs().max().item() <= 1.5e-2 * vmax

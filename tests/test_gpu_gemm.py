@@ -50,21 +50,15 @@ def _run(M, N, K, epi, aux_rows=0, seed=0):
     return err, scale
 
 
-@pytest.fixture(params=[(0, 0, 0, 0, 4, 0, 0), (1, 0, 0, 0, 4, 0, 0), (0, 1, 0, 0, 4, 0, 0), (1, 1, 0, 0, 4, 0, 0),
-                        (1, 0, 1, 0, 4, 0, 0), (1, 0, 0, 1, 4, 0, 0), (1, 0, 1, 1, 4, 0, 0), (1, 0, 1, 0, 5, 0, 0),
-                        (1, 0, 1, 0, 5, 1, 0), (1, 0, 1, 0, 4, 0, 1)],
-                ids=["glds", "bufload", "mfma32", "bufload-mfma32", "sched", "bufload-bm128", "sched-bm128",
-                     "sched-5stage", "sched-5stage-sync2", "pingpong"])
+@pytest.fixture(params=[(0, 0), (1, 0)], ids=["interleaved", "pingpong"])
 def staging(request):
-    """Every variant of the persistent kernel: LDS-DMA staging form (MQ_TUNE_GEMM_BUFLOAD) x
-    MFMA shape (MQ_TUNE_GEMM_MFMA32: 32x32x16 vs 16x16x32) x interleaved K-step (MQ_TUNE_GEMM_SCHED)
-    x 128-row tiles for narrow grids (MQ_TUNE_GEMM_BM128) x ring depth (MQ_TUNE_GEMM_STAGES) x one
-    barrier per two K-steps (MQ_TUNE_GEMM_SYNC2) x the ping-pong kernel (MQ_TUNE_GEMM_PINGPONG)."""
+    """Both 256x256 kernels: the interleaved-K-step kernel (gemm_bf16.hip gemm256_kernel) and the
+    ping-pong kernel (gemm_pp.hip), selected by MQ_TUNE_GEMM_PINGPONG (key 12)."""
     from mqhip import _lib
     ctx = _lib.Context.get(0)
-    keys = (5, 6, 7, 9, 1, 11, 12)
+    keys = (12, 2)
     old = [ctx.lib.mq_get_tuning(k) for k in keys]
-    for k, v in zip(keys, request.param):
+    for k, v in zip(keys, (request.param[0], 0)):
         assert ctx.lib.mq_set_tuning(k, v) == 0
     yield request.param
     for k, v in zip(keys, old):
@@ -109,19 +103,17 @@ def _run_pair(M, N, K, epi, aux_rows, seed=0):
     if epi in (0, 1):
         C0 = C0.to(torch.bfloat16)
     outs = []
-    old = ctx.lib.mq_get_tuning(12), ctx.lib.mq_get_tuning(14)
+    old = ctx.lib.mq_get_tuning(12)
     try:
-        for pp, bal in ((0, 0), (1, 0), (1, 1)):
+        for pp in (0, 1):
             assert ctx.lib.mq_set_tuning(12, pp) == 0
-            assert ctx.lib.mq_set_tuning(14, bal) == 0
             Cm = C0.clone()
             _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), _lib.ptr(bias),
                                             _lib.ptr(aux), M, N, K, K, K, N, aux_rows, epi, _lib.stream_ptr()),
                        "mq_gemm_bf16")
             outs.append(Cm)
     finally:
-        ctx.lib.mq_set_tuning(12, old[0])
-        ctx.lib.mq_set_tuning(14, old[1])
+        ctx.lib.mq_set_tuning(12, old)
     torch.cuda.synchronize()
     return outs
 
@@ -136,8 +128,21 @@ def test_gemm_pingpong_bitwise_equals_interleaved(epi, M, N, K):
     import torch
     outs = _run_pair(M, N, K, epi, aux_rows=192)
     bits = [o.view(torch.int16) if o.dtype == torch.bfloat16 else o.view(torch.int32) for o in outs]
-    assert torch.equal(bits[0], bits[1])   # ping-pong, first schedule
-    assert torch.equal(bits[0], bits[2])   # ping-pong, DMA issued inside the MFMA segments
+    assert torch.equal(bits[0], bits[1])
+
+
+def test_gemm_force_small_matches_fp32():
+    """MQ_TUNE_GEMM_FORCE_SMALL routes every GEMM to the 128x128 kernel: still correct."""
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    old = ctx.lib.mq_get_tuning(2)
+    try:
+        assert ctx.lib.mq_set_tuning(2, 1) == 0
+        for epi in (0, 1, 2, 4):
+            err, scale = _run(700, 512, 320, epi)
+            assert err <= 2e-3 * scale + (0.01 * scale if epi in (0, 1) else 0.0)
+    finally:
+        ctx.lib.mq_set_tuning(2, old)
 
 
 def test_gemm_small_path_nchw():

@@ -1,0 +1,120 @@
+"""GPU: BASELINE config 1 through run_demo.proc -- 1 frame, 4 views, 1 individual, ViTPose-B.
+
+Chain (run_demo.py:21-30 of the reference, association bypassed): per-camera frame stores with
+tracker rows -> step 1 pose slice (batched crop -> ViT-B flip -> UDP decode -> KP_THR) ->
+alldata.json -> step 3's kp2d writer with the known track -> individual map -> step 4 (Viterbi,
+triangulation; optim_points is skipped below 20 points, step4:242-245) -> kp3d.pickle.
+
+Parity, stage by stage against the oracle composition on the same inputs:
+* 2D: each camera's alldata row vs oracle crop + fp32 ViT-B + decode + KP_THR: argmax exact and
+  keypoints within 0.5 px wherever the top-2 heatmap margin is clear (> 5e-2), scores within the
+  bf16 heatmap tolerance (2e-2 of max|H|);
+* kp2d.pickle: exactly the alldata rows of track 0;
+* 3D: step 4 on that kp2d.pickle vs the oracle (Viterbi, score < 0.5 -> NaN, DLT): kp3d 1e-6 mm,
+  scores exact, reprojection errors 1e-6 px.
+The head's final bias is shifted by +1 so random-weight heatmap peaks score above the thresholds.
+"""
+import os
+
+import numpy as np
+import pytest
+import yaml
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+
+def _scene(tmp_path, n_views=4):
+    from mqhip import io as mqio
+    from mqhip import synth
+    cams = synth.make_cameras(n_views)
+    skel = synth.make_skeletons(1, 2)
+    truth = synth.make_kp2d(cams, skel, noise_px=0.0, drop=0.0)            # (1, 2, C, J, 3)
+    raw = tmp_path / "videos"
+    for c, cam in enumerate(cams):
+        frames, tracks = [], []
+        for f in range(2):
+            frames.append(synth.make_frames(1, truth[0, f, c][None, None], seed=10 * c + f)[0])
+            b = synth.boxes_from_kp2d(truth[:, f].transpose(1, 0, 2, 3))[c, 0]
+            tracks.append([[float(b[0]), float(b[1]), float(b[2]), float(b[3]), 0.0, 0.95]])
+        mqio.write_frame_store(str(raw / f"demo.{cam['name']}"), np.stack(frames), [100.0, 100.0 + 1 / 24],
+                               [0, 1], tracks, cam["name"])
+    res = tmp_path / "results3D"
+    (res / "demo").mkdir(parents=True)
+    synth.write_calibration_toml(cams, str(res / "demo" / "calibration.toml"))
+    cal = tmp_path / "calib"
+    cal.mkdir()
+    with open(cal / "config.yaml", "w") as f:
+        yaml.safe_dump({"camera_id": [int(c["name"]) for c in cams]}, f)
+    return cams, str(raw), str(res), str(cal / "config.yaml")
+
+
+def test_run_demo_config1_vitb_chain(tmp_path):
+    import torch
+    from mqhip import io as mqio
+    from mqhip.apis import PoseModelHip
+    from mqhip.weights import VIT_B, make_random_weights
+    from oracle.crop import preprocess, topdown_crop
+    from oracle.decode import decode_batch
+    from oracle.geometry import CameraGroupOracle
+    from oracle.postprocess import expand_boxes
+    from oracle.viterbi import step4_filter
+    import run_demo
+    cams, raw, res, cfg = _scene(tmp_path)
+    w = make_random_weights(VIT_B, seed=3, device="cuda")
+    w["head.final_layer.bias"] = w["head.final_layer.bias"] + 1.0
+    model = PoseModelHip(VIT_B, w, 0)
+    data = run_demo.proc("demo", 24, res, "cuda:0", cfg, raw, 17, n_animal=1, pose_model=model)
+    rd = os.path.join(res, "demo")
+    # ---- 2D stage vs the oracle
+    from oracle.vitpose import forward_flip_test
+    rows = []
+    for c, cam in enumerate(cams):
+        alld = mqio.FrameStore(os.path.join(raw, f"demo.{cam['name']}"))
+        import json
+        with open(os.path.join(rd, cam["name"], "alldata.json")) as f:
+            frames_rows = json.load(f)
+        assert len(frames_rows) == 1 and len(frames_rows[0]) == 1
+        row = frames_rows[0][0]
+        rows.append(row)
+        box = np.array([row[1:5]], dtype=np.int32)
+        bb = expand_boxes(box)[0]
+        c_u8, ctr, scl = topdown_crop(alld.image(0), bb)
+        x = torch.from_numpy(preprocess(c_u8)[None]).cuda()
+        with torch.no_grad():
+            hm, _, _ = forward_flip_test(x, w, VIT_B)
+        hm = hm.cpu().numpy()
+        rkp, rsc, ram = decode_batch(hm, ctr[None], scl[None])
+        flat = hm.reshape(1, 17, -1)
+        top2 = np.sort(flat, axis=-1)[..., -2:]
+        clear = ((top2[..., 1] - top2[..., 0]) / np.abs(flat).max(axis=-1) > 5e-2)[0]
+        got = np.array(row[5], dtype=np.float64)                        # (17, 3) x, y, s
+        np.testing.assert_allclose(got[:, 2], rsc[0], rtol=0, atol=2e-2 * np.abs(hm).max())
+        ok = clear & (got[:, 2] >= 0.3) & (rsc[0] >= 0.3)
+        assert ok.sum() > 0
+        np.testing.assert_allclose(got[ok, :2], rkp[0][ok], rtol=0, atol=0.5)
+        low = got[:, 2] < 0.3
+        assert np.isnan(got[low, :2]).all()
+    # ---- kp2d.pickle = the rows of track 0
+    kp2d = mqio.load_array_pickle(os.path.join(rd, "kp2d.pickle"))
+    assert kp2d.shape == (1, 1, 4, 17, 3)
+    np.testing.assert_array_equal(kp2d[0, 0], np.array([r[5] for r in rows], dtype=np.float64))
+    # ---- 3D stage vs the oracle on that kp2d
+    kf = step4_filter(kp2d).transpose((2, 4, 0, 1, 3))[0]                # (C, F, J, 3)
+    p2 = kf[..., :2].copy()
+    sc = kf[..., 2].copy()
+    p2[sc < 0.5] = np.nan
+    o = CameraGroupOracle(cams)
+    p3 = o.triangulate(p2.reshape(4, -1, 2)).reshape(1, 17, 3)
+    np.testing.assert_allclose(data["kp3d"][0], p3, rtol=0, atol=1e-6)
+    good = ~np.isnan(p2[..., 0])
+    s = sc.copy()
+    s[~good] = 2
+    s3 = s.min(0)
+    s3[good.sum(0) < 1] = np.nan
+    np.testing.assert_array_equal(data["kp3d_score"][0], s3)
+    err = o.reprojection_error(p3.reshape(-1, 3), p2.reshape(4, -1, 2), mean=True).reshape(1, 17)
+    err[good.sum(0) < 1] = np.nan
+    np.testing.assert_allclose(data["kp3d_err"][0], err, rtol=0, atol=1e-6)
+    assert np.isfinite(data["kp3d"]).sum() > 0

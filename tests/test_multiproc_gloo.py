@@ -62,3 +62,57 @@ def test_frame_block_partition():
             sizes = [e - s for s, e in blocks]
             assert max(sizes) - min(sizes) <= 1 and sizes[0] == max(sizes)
     assert frame_block(300, 8, 0) == (0, 38) and frame_block(300, 8, 7) == (263, 300)
+
+
+def _clip_worker(rank, world, port, root, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.join(os.path.dirname(here), "macaque-3d-pose-estimation_amd")]
+    import json
+    import torch.distributed as dist
+    from _fakes import fake_pose_batch, open_stores
+    from mqhip.shard import pose_clip_sharded
+    from src.pipeline import step1_proc2d as s1
+    s1.inference_topdown_batch = fake_pose_batch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        stores = open_stores(root)
+        T = np.arange(stores[0].frame_time[0], stores[0].frame_time[-1], 1.0 / 24)
+        got = pose_clip_sharded(None, stores, T, world, rank, steps_per_batch=4)
+        q.put((rank, json.dumps(got)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pose_clip_sharded_world2_equals_single_rank(tmp_path):
+    """BASELINE config 3's clip driver: time steps sharded over 2 ranks (gloo), one all-gather of
+    the raw keypoints, then the sequential KP_THR / EMA post-process -- identical alldata rows on
+    every rank and identical to the single-rank step-1 pass."""
+    import json
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from _fakes import fake_pose_batch, make_stores
+    from src.pipeline import step1_proc2d as s1
+    stores = make_stores(str(tmp_path), n_cams=3, n_frames=23, seed=5)
+    T = np.arange(stores[0].frame_time[0], stores[0].frame_time[-1], 1.0 / 24)
+    orig = s1.inference_topdown_batch
+    s1.inference_topdown_batch = fake_pose_batch
+    try:
+        ref = json.dumps(s1.process_stores(None, stores, T, steps_per_batch=5))
+    finally:
+        s1.inference_topdown_batch = orig
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_clip_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(T) > 10
+    for _, got in res:
+        assert got == ref

@@ -1,0 +1,74 @@
+"""CPU: the host logic of the step-1 pose slice over frame stores and of step 3's kp2d writer.
+
+* step 1's time-grid walk (step1_proc2d.py:210-223: nearest stored frame, repeats keep the
+  previous result) and the batched multi-camera ``process_stores`` against a camera-by-camera
+  loop written the reference's way -- the ViTPose call is replaced by a deterministic stand-in
+  that depends on the image and the box, so batching / ordering / EMA state are what is tested;
+* step 3's ``create_kp2dfile`` (step3_crossframematching.py:872-915) fed by a known assignment.
+"""
+import json
+from types import SimpleNamespace
+
+import numpy as np
+
+
+from _fakes import fake_pose_batch as _fake_pose
+
+
+def _stores(tmp_path, n_cams=3, n_frames=9, seed=0):
+    from _fakes import make_stores
+    return make_stores(str(tmp_path), n_cams, n_frames, seed)
+
+
+def test_frame_plan_repeats_like_the_reference():
+    from src.pipeline.step1_proc2d import _frame_plan
+    st = SimpleNamespace(get_frame_metadata=lambda: {"frame_time": np.array([0.0, 0.1, 0.2]),
+                                                      "frame_number": np.array([4, 5, 6])})
+    T = np.arange(0.0, 0.2, 1 / 24)
+    plan = _frame_plan(st, T)
+    assert plan == [(4, False), (4, True), (5, False), (5, True), (6, False)]
+
+
+def test_process_stores_equals_camera_by_camera_loop(tmp_path, monkeypatch):
+    from src.pipeline import step1_proc2d as s1
+    monkeypatch.setattr(s1, "inference_topdown_batch", _fake_pose)
+    stores = _stores(tmp_path)
+    t0 = stores[0].frame_time[0]
+    T = np.arange(t0, stores[0].frame_time[-1], 1.0 / 24)
+    got = s1.process_stores(None, stores, T, steps_per_batch=3)
+    for c, st in enumerate(stores):           # the reference's per-camera walk (step1:210-362)
+        sm = s1.KeypointSmoother()
+        md = st.get_frame_metadata()
+        res, fns, fn = [], [], -1
+        for t in T:
+            idx = int(np.abs(md["frame_time"] - t).argmin())
+            if fn >= md["frame_number"][idx]:
+                res.append(res[-1] if res else [])
+                fns.append(fn)
+                continue
+            fn = int(md["frame_number"][idx])
+            boxes, tids = s1.filter_tracks(st.tracks_of(fn))
+            if len(boxes) == 0:
+                res.append([])
+            else:
+                r = _fake_pose(None, [st.image(fn)], [s1.expand_boxes(boxes)])[0]
+                res.append(s1._rows(r, boxes, tids, sm, fn, None, s1.KP_PARAMS))
+            fns.append(fn)
+        assert got[c][1] == fns
+        assert json.dumps(got[c][0]) == json.dumps(res)
+
+
+def test_known_assignment_kp2d_writer(tmp_path):
+    from mqhip import io as mqio
+    from src.pipeline import step3_crossframematching as s3
+    kp = lambda v: [[v, v + 1, 0.5]] * 17
+    T = [[[[0, 0, 0, 1, 1, kp(1.0), -1, 0.0], [1, 0, 0, 1, 1, kp(2.0), -1, 0.0]], []],
+         [[[1, 0, 0, 1, 1, kp(3.0), -1, 0.0]], [[0, 0, 0, 1, 1, kp(4.0), -1, 0.0], [0, 0, 0, 1, 1, kp(5.0), -1, 0.0]]]]
+    Trk, Cid = s3.known_assignment(T, 2)
+    assert Trk[0].tolist() == [[0, -1], [-1, 0]] and Trk[1].tolist() == [[1, 1], [-1, -1]]
+    k = s3.create_kp2dfile(str(tmp_path), T, Trk, Cid, n_animal=2)
+    assert k.shape == (2, 2, 2, 17, 3)
+    assert k[0, 0, 0, 0, 0] == 1.0 and k[1, 0, 0, 0, 0] == 2.0 and k[1, 0, 1, 0, 0] == 3.0
+    assert k[0, 1, 1, 0, 0] == 5.0     # every matching row of the camera is written: the last one stays
+    assert not k[0, 0, 1].any() and not k[1, 1].any()  # zero fill where absent
+    np.testing.assert_array_equal(mqio.load_array_pickle(str(tmp_path / "kp2d.pickle")), k)

@@ -1,5 +1,5 @@
-"""Time mq_attention_bf16 at the ViT-H bench shape (64 images x 192 tokens, 16 heads x 80) and its
-timing ablations (MQ_TUNE_ATTENTION_ABLATE: 1 staging only, 2 no K/V loads, 3 no stores)."""
+"""Time mq_attention_bf16 at the ViT-H bench shape (64 images x 192 tokens, 16 heads x 80): the
+shipped kernel (v2) against the first-generation one (v1, MQ_TUNE_ATTENTION_V2 = 0) in one process."""
 import os
 import sys
 
@@ -15,11 +15,9 @@ def main():
     qkv = torch.randn((n * T, 3 * D), device="cuda").to(torch.bfloat16)
     out = torch.empty((n * T, D), device="cuda", dtype=torch.bfloat16)
     s = _lib.stream_ptr()
-    for rnd in range(2):
-        for mode in ("p", 0, 1, 2, 3):
-            # "p": the persistent kernel (MQ_TUNE_ATTENTION_PERSIST); the others run the per-item kernel
-            assert ctx.lib.mq_set_tuning(15, 1 if mode == "p" else 0) == 0
-            assert ctx.lib.mq_set_tuning(8, 0 if mode == "p" else mode) == 0
+    for rnd in range(3):
+        for ver in (0, 1):
+            assert ctx.lib.mq_set_tuning(17, ver) == 0
             for _ in range(3):
                 ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), n, T, D, H, s)
             torch.cuda.synchronize()
@@ -30,10 +28,9 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / 20 * 1e3
-            print(f"attention mode={mode} r={rnd}: {us:.1f} us  ({2 * 2 * n * H * T * T * (D // H) / (us * 1e-6) / 1e12:.0f} TFLOP/s)",
-                  flush=True)
-    ctx.lib.mq_set_tuning(8, 0)
-    ctx.lib.mq_set_tuning(15, 1)
+            print(f"attention v{ver + 1} r={rnd}: {us:.1f} us  "
+                  f"({2 * 2 * n * H * T * T * (D // H) / (us * 1e-6) / 1e12:.0f} TFLOP/s)", flush=True)
+    ctx.lib.mq_set_tuning(17, 1)
 
 
 if __name__ == "__main__":

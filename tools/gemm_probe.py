@@ -18,7 +18,7 @@ SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
     "fc2": (12288, 1280, 5120, 2),
     "dc1": (12288, 4096, 1280, 0),
     "dc2": (49152, 4096, 256, 0),
-    "f32": (12288, 1280, 5120, 4),   # fc2 shape, plain f32 epilogue (ablation target)
+    "f32": (12288, 1280, 5120, 4),   # fc2 shape, plain f32 epilogue
     "fc1_f32": (12288, 5120, 1280, 4),
     "fc1_bf16": (12288, 5120, 1280, 0),
     "n5120_k5120": (12288, 5120, 5120, 0),
@@ -30,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shape", default="all")
-    ap.add_argument("--variants", default="4,5,small", help="GEMM variants to A/B in this process")
+    ap.add_argument("--variants", default="pp,il,torch", help="GEMM routes to A/B in this process: pp, il, small, torch")
     ap.add_argument("--cold", action="store_true",
                     help="evict L2/Infinity Cache (384 MB write) before every launch; time each launch alone")
     args = ap.parse_args()
@@ -43,72 +43,20 @@ def main():
     res = {}
     variants = args.variants.split(",")
     for rnd in range(2):
-      for var in variants:
-        ctx.lib.mq_set_tuning(3, 0)
-        ctx.lib.mq_set_tuning(5, 0)
-        ctx.lib.mq_set_tuning(6, 0)
-        ctx.lib.mq_set_tuning(7, 1)
-        ctx.lib.mq_set_tuning(9, 0)
-        var_st = var
-        ctx.lib.mq_set_tuning(10, 0)
-        if var in ("p1", "p2"):  # static young-half priority / no priority
-            ctx.lib.mq_set_tuning(10, int(var[1]))
-            var_st = "4"
-        ctx.lib.mq_set_tuning(11, 0)
-        ctx.lib.mq_set_tuning(12, 0)
-        ctx.lib.mq_set_tuning(13, 0)
-        ctx.lib.mq_set_tuning(14, 0)
-        ctx.lib.mq_set_tuning(16, 1)
-        if var == "pf0":  # short-K residual GEMMs back on the interleaved kernel
-            ctx.lib.mq_set_tuning(12, 1)
-            ctx.lib.mq_set_tuning(16, 0)
-            var_st = "4"
-        if var == "pd":  # ping-pong, DMA issued inside the MFMA segment
-            ctx.lib.mq_set_tuning(12, 1)
-            ctx.lib.mq_set_tuning(14, 1)
-            var_st = "4"
-        if var.startswith("pa"):  # ping-pong timing ablations (bf16 epilogue shapes only; wrong results)
-            ctx.lib.mq_set_tuning(12, 1)
-            ctx.lib.mq_set_tuning(13, int(var[2:]))
-            var_st = "4"
-        if var == "pp":  # ping-pong kernel (gemm_pp.hip)
-            ctx.lib.mq_set_tuning(12, 1)
-            var_st = "4"
-        if var == "s5":  # 5-stage ring on the interleaved K-step
-            var_st = "5"
-        if var == "y2":  # 5 stages, one wait + barrier per two K-steps
-            ctx.lib.mq_set_tuning(11, 1)
-            var_st = "5"
-        if var == "b128":  # 128-row tiles for narrow grids
-            ctx.lib.mq_set_tuning(9, 1)
-            var_st = "4"
-        if var == "nosch":
-            ctx.lib.mq_set_tuning(7, 0)
-            var_st = "4"
-        if var in ("m32", "bm32"):
-            ctx.lib.mq_set_tuning(6, 1)
-            ctx.lib.mq_set_tuning(5, 1 if var == "bm32" else 0)
-            var_st = "4"
-        elif var.startswith("buf"):
-            ctx.lib.mq_set_tuning(5, 1)
-            var_st = var[3:]
-        if var == "torch":
+        for var in variants:
+            if var == "torch":
+                for name in names:
+                    res[f"{name}/{var}/r{rnd}"] = bench_torch(torch, name, args.iters)
+                    print(f"{name} v={var} r={rnd}", res[f"{name}/{var}/r{rnd}"], flush=True)
+                continue
+            # routing knobs (include/mq_hip.h): pp = ping-pong (default), il = interleaved K-step, small = 128x128
+            _lib.check(ctx.lib.mq_set_tuning(12, 0 if var == "il" else 1), "tuning")
+            _lib.check(ctx.lib.mq_set_tuning(2, 1 if var == "small" else 0), "tuning")
             for name in names:
-                res[f"{name}/{var}/r{rnd}"] = bench_torch(torch, name, args.iters)
+                res[f"{name}/{var}/r{rnd}"] = bench_one(ctx, _lib, torch, name, args.iters)
                 print(f"{name} v={var} r={rnd}", res[f"{name}/{var}/r{rnd}"], flush=True)
-            continue
-        if var == "small":
-            ctx.lib.mq_set_tuning(2, 1)
-        elif var.startswith("abl"):
-            ctx.lib.mq_set_tuning(2, 0)
-            ctx.lib.mq_set_tuning(1, 4)
-            ctx.lib.mq_set_tuning(3, int(var[3:]))
-        else:
-            ctx.lib.mq_set_tuning(2, 0)
-            ctx.lib.mq_set_tuning(1, int(var_st))
-        for name in names:
-            res[f"{name}/{var}/r{rnd}"] = bench_one(ctx, _lib, torch, name, args.iters)
-            print(f"{name} v={var} r={rnd}", res[f"{name}/{var}/r{rnd}"], flush=True)
+    _lib.check(ctx.lib.mq_set_tuning(12, 1), "tuning")
+    _lib.check(ctx.lib.mq_set_tuning(2, 0), "tuning")
     print(json.dumps(res))
 
 
