@@ -51,6 +51,22 @@ def parse():
     return ap.parse_args()
 
 
+def log(msg):
+    """Progress to stderr (the harness takes a silent run for a hung one)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_share():
+    """Threads for the CPU baseline: the CPU share this process is given.  On the GPU pool nproc and
+    os.cpu_count() report the whole machine while the job's share is OMP_NUM_THREADS (16 per GPU);
+    oversubscribing a CPU quota would time the scheduler, not the restatement."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
+
+
 def cpu_info():
     """Host cores this process may use (what `nproc` reports) and the CPU model (`lscpu`)."""
     model = "unknown"
@@ -91,8 +107,9 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
     from oracle.geometry import CameraGroupOracle
     from oracle.vitpose import forward_flip_test
     info = cpu_info()
-    threads = info["nproc"]
+    threads = cpu_share()
     torch.set_num_threads(threads)
+    log(f"cpu baseline: {threads} threads (nproc {info['nproc']}, os.cpu_count {info['os_cpu_count']})")
     g = CameraGroupOracle(cams_np)
 
     def frame_pass(cfg, n_crops, n_views):
@@ -115,6 +132,7 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
 
         t_vit, _ = _median_time(run, reps)
         t_tri, _ = _median_time(lambda: gv.triangulate(p), reps)
+        log(f"cpu baseline: ViT-{cfg.name} {n_crops} crops {t_vit:.3f} s (median of {reps})")
         return t_vit, t_tri
 
     crops = N_VIEWS * N_ANIMALS
@@ -122,6 +140,7 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
     t_frame2 = t2 * crops / n_crops_sample + tri2
     t1, tri1 = frame_pass(CONFIGS["base"], 4, 4)
     lift = lift_cpu(cams_np)
+    log(f"cpu baseline: config-4 lift {lift['total_s']:.1f} s")
     return {"value": round(N_ANIMALS / t_frame2, 5), "unit": "individuals×frames/s", "cores": threads,
             "kind": "port", "nproc": info["nproc"], "os_cpu_count": info["os_cpu_count"], "cpu_model": info["model"],
             "statistic": f"median of {reps} after 1 warm-up",
@@ -160,12 +179,14 @@ def lift_cpu(cams_np):
     t0 = time.perf_counter()
     kf = step4_filter_batched(kp2d).transpose((2, 4, 0, 1, 3))           # (A, C, F, J, 3)
     t["viterbi_a15"] = time.perf_counter() - t0
+    log(f"cpu lift: viterbi {t['viterbi_a15']:.2f} s")
     pts = kf[..., :2].copy()
     pts[kf[..., 2] < 0.5] = np.nan
     flat = np.ascontiguousarray(pts.transpose(1, 0, 2, 3, 4).reshape(C, -1, 2))
     t0 = time.perf_counter()
     p3, _, _, _ = o.triangulate_ransac_batched(flat, min_cams=2)
     t["ransac_a13"] = time.perf_counter() - t0
+    log(f"cpu lift: ransac {t['ransac_a13']:.2f} s")
     init = p3.reshape(A, F, J, 3)
     t0 = time.perf_counter()
     r0 = optim_points(o, pts[0], init[0], cons, weak, **LIFT_ARGS)
@@ -220,6 +241,8 @@ def lift_gpu(device, reps=3):
         for k, v in (("viterbi_a15", t1 - t0), ("ransac_a13", t3 - t2), ("optim_points_a16", t5 - t4),
                      ("reproj_a14", t6 - t5)):
             times[k].append(v)
+        log(f"gpu lift: viterbi {1e3 * (t1 - t0):.1f} ms, ransac {1e3 * (t3 - t2):.1f} ms, "
+            f"optim {1e3 * (t5 - t4):.1f} ms, reproj {1e3 * (t6 - t5):.1f} ms")
     med = {k: float(np.median(v[1:])) * 1e3 for k, v in times.items()}
     tot = sum(med.values())
     return {"gpu_ms": {k: round(v, 3) for k, v in med.items()}, "total_ms": round(tot, 3),
@@ -309,6 +332,7 @@ def main():
             kp_log[log_slot, :, :, :2] = kp.float()
             kp_log[log_slot, :, :, 2] = score
 
+    log(f"model ready; {args.warmup} warm-up + {args.steps} timed steps")
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
@@ -380,6 +404,7 @@ def main():
         "end_to_end_mfma_frac": round(model_tflops / (world * PEAK_BF16_TFLOPS), 4),
         "roofline": roof,
     }
+    log(f"timed region {dt:.3f} s")
     if rank == 0 and world == 1 and not args.no_lift:
         result["lift_config4"] = lift_gpu(local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

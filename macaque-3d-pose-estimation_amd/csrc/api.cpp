@@ -736,8 +736,8 @@ int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int A, int F, int C, int J,
   if (n_back < 1 || n_back > 8) return fail("mq_viterbi_filter: n_back must be in [1, 8]", -2);
   if ((int64_t)A * F * C * J == 0) return 0;
   HIP_TRY(hipSetDevice(ctx->device));
-  if (ctx->scratch.ensure((size_t)A * C * J * F * 8)) return fail("viterbi scratch alloc failed", -5);
-  K_TRY(mq::viterbi_filter(kp, A, F, C, J, score_threshold, n_back, offset_threshold, ctx->scratch.as<int8_t>(), out,
+  if (ctx->scratch.ensure(mq::viterbi_scratch_bytes(A, F, C, J, n_back))) return fail("viterbi scratch alloc failed", -5);
+  K_TRY(mq::viterbi_filter(kp, A, F, C, J, score_threshold, n_back, offset_threshold, ctx->scratch.p, out,
                            (hipStream_t)stream));
   return 0;
 }

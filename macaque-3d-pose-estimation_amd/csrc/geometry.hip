@@ -595,26 +595,33 @@ __device__ __forceinline__ double trans_logprob(double d, double thres) {
   return r;
 }
 
-// One thread per chain (animal, camera, joint): kp (A,F,C,J,3) -> filtered (A,F,C,J,3).
-__global__ void viterbi_kernel(const double* __restrict__ kp, int A, int F, int C, int J, double score_thr,
-                               int n_back, double thres_dist, int8_t* __restrict__ back, double* __restrict__ out) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= A * C * J) return;
-  const int j = ch % J, c = (ch / J) % C, a = ch / (J * C);
-  auto at = [&](int f) -> const double* { return kp + ((((size_t)a * F + f) * C + c) * J + j) * 3; };
-  auto valid = [&](int f) -> bool {
-    const double* p = at(f);
+// The Viterbi filter in two launches (filter_pose.py:48-120, chain = (animal, camera, joint)):
+//  1. viterbi_trans_kernel, one thread per (chain, frame i >= 1, particle q of frame i, particle p
+//     of frame i-1): the transition log-probability log(Phi((d+2)/s) - Phi((d-2)/s)) -- the fp64
+//     log_ndtr work, which is all of the arithmetic -- for every chain and frame in parallel;
+//  2. viterbi_dp_kernel, one thread per chain: the max-product recursion over frames on the
+//     precomputed transitions (a few adds and compares per frame, the next frames' inputs
+//     prefetched), then the first-argmax backtrack.
+// Same operations in the same order per value as the single-pass form, so outputs are identical.
+struct VitChain {
+  const double* kp;
+  int F, C, J, n_back;
+  double score_thr;
+  __device__ const double* at(int a, int c, int j, int f) const {
+    return kp + ((((size_t)a * F + f) * C + c) * J + j) * 3;
+  }
+  __device__ bool valid(const double* p) const {
     const bool masked = p[2] < score_thr;  // points_full[scores < thr] = NaN
     return !masked && !(p[0] != p[0]);
-  };
+  }
   // particles of frame i: (x, y, score * 2^-jj) for valid frames i-jj, jj < n_back
-  auto particles = [&](int i, double (&px)[8], double (&py)[8], double (&ps)[8]) -> int {
+  __device__ int particles(int a, int c, int j, int i, double* px, double* py, double* ps) const {
     int s = 0;
     double w = 1.0;
     for (int jj = 0; jj < n_back && jj < 8; ++jj) {
       if (i - jj < 0) break;
-      if (valid(i - jj)) {
-        const double* p = at(i - jj);
+      const double* p = at(a, c, j, i - jj);
+      if (valid(p)) {
         px[s] = p[0];
         py[s] = p[1];
         ps[s] = p[2] * w;
@@ -629,27 +636,54 @@ __global__ void viterbi_kernel(const double* __restrict__ kp, int A, int F, int 
       s = 1;
     }
     return s;
-  };
-  int8_t* bk = back + (size_t)ch * F * 8;
+  }
+};
+
+// trans[((ch * F + i) * NB + q) * NB + p]; entries beyond the particle counts are not written.
+__global__ void viterbi_trans_kernel(VitChain V, int chains, double thres_dist, double* __restrict__ trans) {
+  const int NB = V.n_back;
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t per_chain = (size_t)V.F * NB * NB;
+  if (tid >= (size_t)chains * per_chain) return;
+  const int ch = (int)(tid / per_chain);
+  const int rem = (int)(tid - (size_t)ch * per_chain);
+  const int i = rem / (NB * NB), q = (rem / NB) % NB, p = rem % NB;
+  if (i == 0) return;
+  const int j = ch % V.J, c = (ch / V.J) % V.C, a = ch / (V.J * V.C);
   double ax[8], ay[8], as[8], bx[8], by[8], bs[8];
+  const int va = V.particles(a, c, j, i - 1, ax, ay, as);
+  const int vb = V.particles(a, c, j, i, bx, by, bs);
+  if (q >= vb || p >= va) return;
+  double P;
+  if (bx[q] == -1 || ax[p] == -1) {
+    P = log(0.001);
+  } else {
+    const double dx = ax[p] - bx[q], dy = ay[p] - by[q];
+    P = trans_logprob(sqrt(dx * dx + dy * dy), thres_dist);
+  }
+  trans[tid] = P;
+}
+
+__global__ void viterbi_dp_kernel(VitChain V, int chains, const double* __restrict__ trans,
+                                  int8_t* __restrict__ back, double* __restrict__ out) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= chains) return;
+  const int NB = V.n_back, F = V.F;
+  const int j = ch % V.J, c = (ch / V.J) % V.C, a = ch / (V.J * V.C);
+  int8_t* bk = back + (size_t)ch * F * 8;
+  const double* tr = trans + (size_t)ch * F * NB * NB;
+  double px[8], py[8], ps[8];
   double Tp[8], Tc[8];
-  int va = particles(0, ax, ay, as);
-  for (int p = 0; p < va; ++p) Tp[p] = log(as[p]);
-  const double lmiss = log(0.001);
+  int va = V.particles(a, c, j, 0, px, py, ps);
+  for (int p = 0; p < va; ++p) Tp[p] = log(ps[p]);
   for (int i = 1; i < F; ++i) {
-    const int vb = particles(i, bx, by, bs);
+    const int vb = V.particles(a, c, j, i, px, py, ps);
+    const double* t = tr + (size_t)i * NB * NB;
     for (int q = 0; q < vb; ++q) {
       double best = -INFINITY;
       int arg = 0;
       for (int p = 0; p < va; ++p) {
-        double P;
-        if (bx[q] == -1 || ax[p] == -1) {
-          P = lmiss;
-        } else {
-          const double dx = ax[p] - bx[q], dy = ay[p] - by[q];
-          P = trans_logprob(sqrt(dx * dx + dy * dy), thres_dist);
-        }
-        const double v = Tp[p] + P;
+        const double v = Tp[p] + t[q * NB + p];
         // np.max / np.argmax semantics: first maximum, a NaN wins and sticks
         if (p == 0) {
           best = v;
@@ -659,15 +693,10 @@ __global__ void viterbi_kernel(const double* __restrict__ kp, int A, int F, int 
           arg = p;
         }
       }
-      Tc[q] = best + log(bs[q]);
+      Tc[q] = best + log(ps[q]);
       bk[(size_t)i * 8 + q] = (int8_t)arg;
     }
-    for (int q = 0; q < vb; ++q) {
-      Tp[q] = Tc[q];
-      ax[q] = bx[q];
-      ay[q] = by[q];
-      as[q] = bs[q];
-    }
+    for (int q = 0; q < vb; ++q) Tp[q] = Tc[q];
     va = vb;
   }
   // backtrack from the first argmax of the last frame
@@ -675,9 +704,8 @@ __global__ void viterbi_kernel(const double* __restrict__ kp, int A, int F, int 
   for (int p = 1; p < va; ++p)
     if (Tp[p] > Tp[cur]) cur = p;
   for (int i = F - 1; i >= 0; --i) {
-    double px[8], py[8], ps[8];
-    particles(i, px, py, ps);
-    double* o = out + ((((size_t)a * F + i) * C + c) * J + j) * 3;
+    V.particles(a, c, j, i, px, py, ps);
+    double* o = out + ((((size_t)a * F + i) * V.C + c) * V.J + j) * 3;
     o[0] = px[cur];
     o[1] = py[cur];
     o[2] = ps[cur];
@@ -759,13 +787,24 @@ int geometry_affinity(const double* cams, int C, const double* pts, const int32_
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+size_t viterbi_scratch_bytes(int A, int F, int C, int J, int n_back) {
+  const size_t chains = (size_t)A * C * J;
+  return chains * F * 8 + 256 + chains * F * n_back * n_back * sizeof(double);
+}
+
+// scratch: viterbi_scratch_bytes() -- int8 back-pointers, then the f64 transition table.
 int viterbi_filter(const double* kp, int A, int F, int C, int J, double score_thr, int n_back, double thres_dist,
-                   int8_t* back_scratch, double* out, hipStream_t s) {
+                   void* scratch, double* out, hipStream_t s) {
   const int chains = A * C * J;
   if (chains <= 0 || F <= 0) return 0;
   if (n_back > 8 || n_back < 1) return -2;
-  hipLaunchKernelGGL(viterbi_kernel, dim3((chains + 63) / 64), dim3(64), 0, s, kp, A, F, C, J, score_thr, n_back,
-                     thres_dist, back_scratch, out);
+  int8_t* back = static_cast<int8_t*>(scratch);
+  double* trans = reinterpret_cast<double*>(static_cast<char*>(scratch) + (((size_t)chains * F * 8 + 255) & ~(size_t)255));
+  VitChain V{kp, F, C, J, n_back, score_thr};
+  const size_t work = (size_t)chains * F * n_back * n_back;
+  hipLaunchKernelGGL(viterbi_trans_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, V, chains, thres_dist,
+                     trans);
+  hipLaunchKernelGGL(viterbi_dp_kernel, dim3((chains + 63) / 64), dim3(64), 0, s, V, chains, trans, back, out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

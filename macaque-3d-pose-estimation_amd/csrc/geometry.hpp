@@ -16,5 +16,6 @@ int triangulate_pinv(const double* cams, int C, const double* und, const uint8_t
 int geometry_affinity(const double* cams, int C, const double* pts, const int32_t* cam_of_det, int B, int M, int J,
                       double thr_kp, double* rays, double* dist, double* out, hipStream_t s);
 int viterbi_filter(const double* kp, int A, int F, int C, int J, double score_thr, int n_back, double thres_dist,
-                   int8_t* back_scratch, double* out, hipStream_t s);
+                   void* scratch, double* out, hipStream_t s);
+size_t viterbi_scratch_bytes(int A, int F, int C, int J, int n_back);
 }  // namespace mq

@@ -618,6 +618,149 @@ __global__ void __launch_bounds__(64) optim_precond_kernel(OptDims D, OptBufs Bf
   Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
 }
 
+// The same preconditioner step with the series staged in LDS: one 256-thread block per (joint
+// series, animal).  The solve is a sequential recurrence over frames; run from global memory its
+// every step waits on a load that the previous kernel left in another XCD's L2 or in HBM.  Here
+// the block first copies the series' factor blocks and r / d / p / q (or g) into LDS with all its
+// threads, applies the element-wise updates r -= alpha q, d += alpha p in parallel, and one thread
+// then runs both substitutions on LDS.  Arithmetic per value is the one of solve_series (bitwise
+// equal results).  LDS: F * (24 + 9 NN) doubles (optim_precond_lds_bytes).
+template <int NN>
+__global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBufs Bf, int it) {
+  const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int F = D.F, J = D.J, J3 = 3 * J;
+  double alpha = 0;
+  const double* P = (it & 1) ? Bf.P1 : Bf.P0;
+  if (it >= 0) {
+    if (pcg_done(D, Bf, b, it)) return;
+    const double pq = Bf.pq[(size_t)b * (OPT_MAXIT + 1) + it];
+    if (!(pq > 0)) return;
+    alpha = rz_at(D, Bf, b, it) / pq;
+  }
+  const size_t base = (size_t)b * D.NV;
+  if (j == J) {  // the length variables: diagonal preconditioner (as optim_precond_kernel)
+    if (t != 0) return;
+    double rz = 0;
+    if (!D.fix)
+      for (int k = 0; k < D.NL; ++k) {
+        const size_t o = base + D.NX + k;
+        double r;
+        if (it < 0) {
+          Bf.d[o] = 0;
+          r = -Bf.g[o];
+        } else {
+          Bf.d[o] += alpha * P[o];
+          r = Bf.r[o] - alpha * Bf.q[o];
+        }
+        Bf.r[o] = r;
+        const double z = r * Bf.pinvL[(size_t)b * OPT_MAXL + k];
+        Bf.z[o] = z;
+        rz += r * z;
+      }
+    Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
+    return;
+  }
+  constexpr int FR = 9 + 9 * NN;  // factor doubles used per frame
+  extern __shared__ double lds_opt[];
+  double* sfac = lds_opt;
+  double* sr = sfac + (size_t)F * FR;
+  double* sz = sr + (size_t)F * 3;
+  const double* __restrict__ fb = Bf.fac + ((size_t)b * J + j) * F * 36;
+  for (int idx = t; idx < F * FR; idx += 256) {
+    const int f = idx / FR, e = idx - f * FR;
+    sfac[idx] = fb[(size_t)f * 36 + e];
+  }
+  for (int idx = t; idx < F * 3; idx += 256) {
+    const int f = idx / 3, i = idx - f * 3;
+    const size_t o = base + (size_t)f * J3 + 3 * j + i;
+    if (it < 0) {
+      Bf.d[o] = 0.0;
+      sr[idx] = -Bf.g[o];
+    } else {
+      Bf.d[o] = Bf.d[o] + alpha * P[o];
+      sr[idx] = Bf.r[o] - alpha * Bf.q[o];
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    double Y[NN][3];
+#pragma unroll
+    for (int k = 0; k < NN; ++k) Y[k][0] = Y[k][1] = Y[k][2] = 0.0;
+    for (int f = 0; f < F; ++f) {  // forward: L y = r
+      const double* rec = sfac + (size_t)f * FR;
+      double w[3] = {sr[3 * f], sr[3 * f + 1], sr[3 * f + 2]};
+#pragma unroll
+      for (int d = 1; d <= NN; ++d) {
+        const double* Lf = rec + 9 * d;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          w[i] -= Lf[3 * i] * Y[d - 1][0] + Lf[3 * i + 1] * Y[d - 1][1] + Lf[3 * i + 2] * Y[d - 1][2];
+      }
+      const double* I = rec;
+      const double y0 = I[0] * w[0];
+      const double y1 = I[3] * w[0] + I[4] * w[1];
+      const double y2 = I[6] * w[0] + I[7] * w[1] + I[8] * w[2];
+      sz[3 * f] = y0;
+      sz[3 * f + 1] = y1;
+      sz[3 * f + 2] = y2;
+#pragma unroll
+      for (int k = NN - 1; k >= 1; --k) {
+        Y[k][0] = Y[k - 1][0];
+        Y[k][1] = Y[k - 1][1];
+        Y[k][2] = Y[k - 1][2];
+      }
+      Y[0][0] = y0;
+      Y[0][1] = y1;
+      Y[0][2] = y2;
+    }
+    double Z[NN][3];
+#pragma unroll
+    for (int k = 0; k < NN; ++k) Z[k][0] = Z[k][1] = Z[k][2] = 0.0;
+    double rz = 0;
+    for (int f = F - 1; f >= 0; --f) {  // backward: L^T z = y
+      double w[3] = {sz[3 * f], sz[3 * f + 1], sz[3 * f + 2]};
+#pragma unroll
+      for (int d = 1; d <= NN; ++d) {
+        if (f + d < F) {
+          const double* Ld = sfac + (size_t)(f + d) * FR + 9 * d;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) w[i] -= Ld[i] * Z[d - 1][0] + Ld[3 + i] * Z[d - 1][1] + Ld[6 + i] * Z[d - 1][2];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) w[i] -= 0.0 * Z[d - 1][0] + 0.0 * Z[d - 1][1] + 0.0 * Z[d - 1][2];
+        }
+      }
+      const double* I = sfac + (size_t)f * FR;
+      const double z0 = I[0] * w[0] + I[3] * w[1] + I[6] * w[2];
+      const double z1 = I[4] * w[1] + I[7] * w[2];
+      const double z2 = I[8] * w[2];
+      sz[3 * f] = z0;
+      sz[3 * f + 1] = z1;
+      sz[3 * f + 2] = z2;
+      rz += sr[3 * f] * z0 + sr[3 * f + 1] * z1 + sr[3 * f + 2] * z2;
+#pragma unroll
+      for (int k = NN - 1; k >= 1; --k) {
+        Z[k][0] = Z[k - 1][0];
+        Z[k][1] = Z[k - 1][1];
+        Z[k][2] = Z[k - 1][2];
+      }
+      Z[0][0] = z0;
+      Z[0][1] = z1;
+      Z[0][2] = z2;
+    }
+    Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
+  }
+  __syncthreads();
+  for (int idx = t; idx < F * 3; idx += 256) {
+    const int f = idx / 3, i = idx - f * 3;
+    const size_t o = base + (size_t)f * J3 + 3 * j + i;
+    Bf.r[o] = sr[idx];
+    Bf.z[o] = sz[idx];
+  }
+}
+
+size_t optim_precond_lds_bytes(int F, int NN) { return (size_t)F * (24 + 9 * NN) * sizeof(double); }
+
 // q = (H + lam diag(H)) p_it with p_it = z + beta p_{it-1} (computed here, written to P[it & 1]).
 __global__ void __launch_bounds__(OPT_THREADS) optim_matvec_kernel(OptDims D, OptBufs Bf, int it) {
   const int f = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
@@ -822,6 +965,28 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
   std::vector<double> lam(B, 1e-3), cost(B), costt(B), hctl(2 * B, 0.0);
   std::vector<int> active(B, 1), iters(B, 0), status(B, 2);
 
+  // preconditioner step: series staged in LDS when they fit (every clip up to ~400 frames)
+  const size_t lds_b = optim_precond_lds_bytes(F, D.n);
+  const bool use_lds = lds_b <= 160 * 1024;
+  auto precond = [&](int it) {
+    if (!use_lds) {
+      hipLaunchKernelGGL(optim_precond_kernel, dim3(B), dim3(64), 0, s, D, Bf, it);
+      return;
+    }
+    const dim3 grid(J + 1, B);
+    if (D.n == 1) hipLaunchKernelGGL(optim_precond_lds_kernel<1>, grid, dim3(256), lds_b, s, D, Bf, it);
+    else if (D.n == 2) hipLaunchKernelGGL(optim_precond_lds_kernel<2>, grid, dim3(256), lds_b, s, D, Bf, it);
+    else hipLaunchKernelGGL(optim_precond_lds_kernel<3>, grid, dim3(256), lds_b, s, D, Bf, it);
+  };
+  if (use_lds) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+  }
   auto eval = [&](const double* xx, int mode, double* out) {
     hipLaunchKernelGGL(optim_eval_kernel, gridFB, dim3(OPT_THREADS), 0, s, D, Bf, xx, mode);
     hipLaunchKernelGGL(optim_reduce_kernel, dim3(B), dim3(OPT_THREADS), 0, s, D, Bf, out, mode);
@@ -847,11 +1012,11 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
     if (hipMemcpyAsync(ctl, hctl.data(), sizeof(double) * 2 * B, hipMemcpyHostToDevice, s) != hipSuccess) return -3;
     (void)hipMemsetAsync(Bf.rzJ, 0, sizeof(double) * (size_t)B * (OPT_MAXIT + 1) * (J + 2), s);
     hipLaunchKernelGGL(optim_factor_kernel, dim3(B), dim3(64), 0, s, D, Bf);
-    hipLaunchKernelGGL(optim_precond_kernel, dim3(B), dim3(64), 0, s, D, Bf, -1);
+    precond(-1);
     for (int it = 0; it < npcg; ++it) {
       hipLaunchKernelGGL(optim_matvec_kernel, gridFB, dim3(OPT_THREADS), 0, s, D, Bf, it);
       hipLaunchKernelGGL(optim_reduce_pq_kernel, dim3(B), dim3(OPT_THREADS), 0, s, D, Bf, it);
-      hipLaunchKernelGGL(optim_precond_kernel, dim3(B), dim3(64), 0, s, D, Bf, it);
+      precond(it);
     }
     hipLaunchKernelGGL(optim_axpy_kernel, dim3(ew_blocks), dim3(256), 0, s, x, Bf.d, xt, D.NX, D.NV, B, D.fix);
     eval(xt, 1, cost_t);

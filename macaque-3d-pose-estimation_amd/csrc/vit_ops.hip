@@ -345,33 +345,44 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
       }
     }
   }
-  // softmax over the tokens of query l16: registers hold tokens tb*16 + 4 g + e
+  // softmax over the tokens of query l16: registers hold tokens tb*16 + 4 g + e.  The row max and
+  // sum run as four independent chains (one per register e) so the dependent-latency chain is
+  // ntb deep instead of 4 ntb; the two query blocks interleave.
   bf16x8 P[2][MAXT / 32];
   float linv[2];
+  float mb[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    float m = -INFINITY;
+    float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-    for (int tb = 0; tb < MAXT / 16; ++tb)
-      if (tb < ntb) {
-        m = fmaxf(m, fmaxf(S[u][tb][0], S[u][tb][1]));
-        m = fmaxf(m, fmaxf(S[u][tb][2], S[u][tb][3]));
+    for (int tb = 0; tb + 1 < MAXT / 16; tb += 2)
+      if (tb + 1 < ntb) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m4[e] = fmaxf(m4[e], fmaxf(S[u][tb][e], S[u][tb + 1][e]));
+      } else if (tb < ntb) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m4[e] = fmaxf(m4[e], S[u][tb][e]);
       }
+    float m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
-    const float mb = m * scale_log2;
-    float ls = 0.f;
+    mb[u] = m * scale_log2;
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float l4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb) {
       if (tb < ntb) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float pv = __builtin_amdgcn_exp2f(S[u][tb][e] * scale_log2 - mb);
+          const float pv = __builtin_amdgcn_exp2f(S[u][tb][e] * scale_log2 - mb[u]);
           S[u][tb][e] = pv;
-          ls += pv;
+          l4[e] += pv;
         }
       }
     }
+    float ls = (l4[0] + l4[1]) + (l4[2] + l4[3]);
     ls += __shfl_xor(ls, 16, 64);
     ls += __shfl_xor(ls, 32, 64);
     linv[u] = 1.0f / ls;
