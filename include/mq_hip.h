@@ -37,10 +37,13 @@ typedef struct mq_vitpose mq_vitpose;
 int mq_abi_version(void);
 const char* mq_last_error(void);
 
-/* Process-wide routing knobs.  Every setting computes the same results (tested equal); they exist
- * for A/B measurement.  Changing one makes the next mq_vitpose_forward re-capture its graph. */
+/* Process-wide knobs for A/B measurement.  The kernel-routing knobs select variants that compute the
+ * same results (tested equal); the PCG cap changes only the inner-solve accuracy of optim_points,
+ * whose results stay within that stage's tolerance.  No knob can select a variant that computes
+ * something else.  Changing one makes the next mq_vitpose_forward re-capture its graph. */
 #define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 kernel (default 0) */
-#define MQ_TUNE_OPTIM_PCG_ITERS 4   /* conjugate-gradient iterations per Levenberg-Marquardt step (default 40) */
+#define MQ_TUNE_OPTIM_PCG_ITERS 4   /* cap on the conjugate-gradient iterations per Levenberg-Marquardt step (default 20;
+                                       results stay within the optim_points tolerance) */
 #define MQ_TUNE_GEMM_PINGPONG 12    /* 1 (default): 256x256 GEMMs with K % 64 == 0 on the ping-pong kernel (wave groups
                                        alternate LDS traffic and MFMA, gemm_pp.hip); 0: the interleaved-K-step kernel */
 #define MQ_TUNE_ATTENTION_V2 17     /* 1 (default): attention on 16x16x32 QK^T + transposed-output PV (vit_ops.hip
@@ -158,7 +161,7 @@ int mq_geometry_affinity(mq_ctx* ctx, const double* cams, int n_cams, const doub
 
 /* filter_pose_viterbi over every (animal, camera, joint) chain of kp (A,F,C,J,3)
  * [x, y, score] (step 4 layout of kp2d.pickle) -> out (A,F,C,J,3).  Scratch is
- * owned by the context.  score_threshold 0.3, n_back 3, offset_threshold 25 in step 4. */
+ * owned by the context.  score_threshold 0.3, n_back 3, offset_threshold 25 in step 4 (n_back 1..3). */
 int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int n_animals, int n_frames, int n_cams, int n_joints,
                       double score_threshold, int n_back, double offset_threshold, double* out, void* stream);
 

@@ -129,9 +129,9 @@ extern "C" {
 
 int mq_abi_version(void) { return MQ_ABI_VERSION; }
 
-// Every knob selects between variants that compute the same results (they are tested equal):
-// kernel routing for A/B measurement and the inner-solver iteration count.  A change bumps the
-// generation so that ViTPose graphs captured under the old routing are re-captured.
+// Knobs select between variants that compute the same results (kernel routing, tested equal) or
+// bound the inner-solver iterations of optim_points (results within that stage's tolerance).  A change
+// bumps the generation so that ViTPose graphs captured under the old routing are re-captured.
 int mq_set_tuning(int key, int value) {
   switch (key) {
     case MQ_TUNE_GEMM_FORCE_SMALL:
@@ -733,7 +733,7 @@ int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int A, int F, int C, int J,
                       double offset_threshold, double* out, void* stream) {
   if (!ctx || !kp || !out) return fail("mq_viterbi_filter: null argument");
   if (A < 0 || F < 0 || C < 0 || J < 0) return fail("mq_viterbi_filter: negative size", -2);
-  if (n_back < 1 || n_back > 8) return fail("mq_viterbi_filter: n_back must be in [1, 8]", -2);
+  if (n_back < 1 || n_back > 3) return fail("mq_viterbi_filter: n_back must be in [1, 3]", -2);
   if ((int64_t)A * F * C * J == 0) return 0;
   HIP_TRY(hipSetDevice(ctx->device));
   if (ctx->scratch.ensure(mq::viterbi_scratch_bytes(A, F, C, J, n_back))) return fail("viterbi scratch alloc failed", -5);

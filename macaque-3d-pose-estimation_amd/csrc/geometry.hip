@@ -596,12 +596,14 @@ __device__ __forceinline__ double trans_logprob(double d, double thres) {
 }
 
 // The Viterbi filter in two launches (filter_pose.py:48-120, chain = (animal, camera, joint)):
-//  1. viterbi_trans_kernel, one thread per (chain, frame i >= 1, particle q of frame i, particle p
-//     of frame i-1): the transition log-probability log(Phi((d+2)/s) - Phi((d-2)/s)) -- the fp64
-//     log_ndtr work, which is all of the arithmetic -- for every chain and frame in parallel;
-//  2. viterbi_dp_kernel, one thread per chain: the max-product recursion over frames on the
-//     precomputed transitions (a few adds and compares per frame, the next frames' inputs
-//     prefetched), then the first-argmax backtrack.
+//  1. viterbi_trans_kernel, one thread per (chain, frame i, particle q of frame i, particle p of
+//     frame i-1): the transition log-probability log(Phi((d+2)/s) - Phi((d-2)/s)) -- the fp64
+//     log_ndtr work, which is all of the arithmetic -- for every chain and frame in parallel; the
+//     (q, p) = (0, 0) thread of each frame also records the frame's particles (x, y, score, log score)
+//     and their count;
+//  2. viterbi_dp_kernel, one thread per chain: the max-product recursion over frames on those
+//     records (a few adds and compares per frame, the next frame's inputs loaded while the current
+//     one is combined), back-pointers and the backtracked path in LDS, then the output rows.
 // Same operations in the same order per value as the single-pass form, so outputs are identical.
 struct VitChain {
   const double* kp;
@@ -639,8 +641,14 @@ struct VitChain {
   }
 };
 
-// trans[((ch * F + i) * NB + q) * NB + p]; entries beyond the particle counts are not written.
-__global__ void viterbi_trans_kernel(VitChain V, int chains, double thres_dist, double* __restrict__ trans) {
+struct VitBufs {
+  double* trans;  // [chain][F][NB][NB]: P(q of frame i | p of frame i-1)
+  double* part;   // [chain][F][NB][4]: x, y, score, log(score)
+  int8_t* cnt;    // [chain][F]: particle count
+  int8_t* bk;     // [chain][F][NB]: back-pointers when they do not fit in LDS
+};
+
+__global__ void viterbi_trans_kernel(VitChain V, int chains, double thres_dist, VitBufs W) {
   const int NB = V.n_back;
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t per_chain = (size_t)V.F * NB * NB;
@@ -648,11 +656,22 @@ __global__ void viterbi_trans_kernel(VitChain V, int chains, double thres_dist, 
   const int ch = (int)(tid / per_chain);
   const int rem = (int)(tid - (size_t)ch * per_chain);
   const int i = rem / (NB * NB), q = (rem / NB) % NB, p = rem % NB;
-  if (i == 0) return;
   const int j = ch % V.J, c = (ch / V.J) % V.C, a = ch / (V.J * V.C);
-  double ax[8], ay[8], as[8], bx[8], by[8], bs[8];
-  const int va = V.particles(a, c, j, i - 1, ax, ay, as);
+  double bx[8], by[8], bs[8];
   const int vb = V.particles(a, c, j, i, bx, by, bs);
+  if (q == 0 && p == 0) {
+    double* rec = W.part + ((size_t)ch * V.F + i) * NB * 4;
+    for (int k = 0; k < vb; ++k) {
+      rec[4 * k] = bx[k];
+      rec[4 * k + 1] = by[k];
+      rec[4 * k + 2] = bs[k];
+      rec[4 * k + 3] = log(bs[k]);
+    }
+    W.cnt[(size_t)ch * V.F + i] = (int8_t)vb;
+  }
+  if (i == 0) return;
+  double ax[8], ay[8], as[8];
+  const int va = V.particles(a, c, j, i - 1, ax, ay, as);
   if (q >= vb || p >= va) return;
   double P;
   if (bx[q] == -1 || ax[p] == -1) {
@@ -661,28 +680,55 @@ __global__ void viterbi_trans_kernel(VitChain V, int chains, double thres_dist, 
     const double dx = ax[p] - bx[q], dy = ay[p] - by[q];
     P = trans_logprob(sqrt(dx * dx + dy * dy), thres_dist);
   }
-  trans[tid] = P;
+  W.trans[tid] = P;
 }
 
-__global__ void viterbi_dp_kernel(VitChain V, int chains, const double* __restrict__ trans,
-                                  int8_t* __restrict__ back, double* __restrict__ out) {
+constexpr int VIT_DP_THREADS = 64;
+
+// Back-pointers (then the backtracked path in slot 0 of each frame): blockDim.x * F * NB bytes of LDS
+// when that fits (the block size is chosen by the launcher), else the global fallback in W.bk.
+template <int NB>
+__global__ void __launch_bounds__(VIT_DP_THREADS) viterbi_dp_kernel(VitChain V, int chains, VitBufs W,
+                                                                    double* __restrict__ out, int bk_in_lds) {
+  extern __shared__ int8_t lds_bk[];
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= chains) return;
-  const int NB = V.n_back, F = V.F;
+  const int F = V.F;
   const int j = ch % V.J, c = (ch / V.J) % V.C, a = ch / (V.J * V.C);
-  int8_t* bk = back + (size_t)ch * F * 8;
-  const double* tr = trans + (size_t)ch * F * NB * NB;
-  double px[8], py[8], ps[8];
-  double Tp[8], Tc[8];
-  int va = V.particles(a, c, j, 0, px, py, ps);
-  for (int p = 0; p < va; ++p) Tp[p] = log(ps[p]);
+  int8_t* bk = bk_in_lds ? lds_bk + (size_t)threadIdx.x * F * NB : W.bk + (size_t)ch * F * NB;
+  const double* tr = W.trans + (size_t)ch * F * NB * NB;
+  const double* part = W.part + (size_t)ch * F * NB * 4;
+  const int8_t* cnt = W.cnt + (size_t)ch * F;
+  double Tp[NB], Tc[NB];
+  int va = cnt[0];
+#pragma unroll
+  for (int p = 0; p < NB; ++p) Tp[p] = (p < va) ? part[4 * p + 3] : -INFINITY;
+  // inputs of frame i: count, log scores, transitions; frame i+1's are loaded before frame i is combined
+  auto load = [&](int i, int& n, double (&lg)[NB], double (&t)[NB * NB]) {
+    n = cnt[i];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) lg[k] = part[((size_t)i * NB + k) * 4 + 3];
+#pragma unroll
+    for (int k = 0; k < NB * NB; ++k) t[k] = tr[(size_t)i * NB * NB + k];
+  };
+  int vb_n = 1;
+  double lg_n[NB], t_n[NB * NB];
+  if (F > 1) load(1, vb_n, lg_n, t_n);
   for (int i = 1; i < F; ++i) {
-    const int vb = V.particles(a, c, j, i, px, py, ps);
-    const double* t = tr + (size_t)i * NB * NB;
-    for (int q = 0; q < vb; ++q) {
+    const int vb = vb_n;
+    double lg[NB], t[NB * NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) lg[k] = lg_n[k];
+#pragma unroll
+    for (int k = 0; k < NB * NB; ++k) t[k] = t_n[k];
+    if (i + 1 < F) load(i + 1, vb_n, lg_n, t_n);
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
       double best = -INFINITY;
       int arg = 0;
-      for (int p = 0; p < va; ++p) {
+#pragma unroll
+      for (int p = 0; p < NB; ++p) {
+        if (p >= va) continue;
         const double v = Tp[p] + t[q * NB + p];
         // np.max / np.argmax semantics: first maximum, a NaN wins and sticks
         if (p == 0) {
@@ -693,23 +739,29 @@ __global__ void viterbi_dp_kernel(VitChain V, int chains, const double* __restri
           arg = p;
         }
       }
-      Tc[q] = best + log(ps[q]);
-      bk[(size_t)i * 8 + q] = (int8_t)arg;
+      Tc[q] = (q < vb) ? best + lg[q] : -INFINITY;
+      bk[i * NB + q] = (int8_t)arg;
     }
-    for (int q = 0; q < vb; ++q) Tp[q] = Tc[q];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) Tp[q] = Tc[q];
     va = vb;
   }
-  // backtrack from the first argmax of the last frame
+  // backtrack from the first argmax of the last frame; the path goes into slot 0 of each frame
   int cur = 0;
-  for (int p = 1; p < va; ++p)
-    if (Tp[p] > Tp[cur]) cur = p;
+#pragma unroll
+  for (int p = 1; p < NB; ++p)
+    if (p < va && Tp[p] > Tp[cur]) cur = p;
   for (int i = F - 1; i >= 0; --i) {
-    V.particles(a, c, j, i, px, py, ps);
+    const int nxt = i > 0 ? bk[i * NB + cur] : 0;
+    bk[i * NB] = (int8_t)cur;
+    cur = nxt;
+  }
+  for (int i = 0; i < F; ++i) {  // output rows (independent loads)
+    const double* r = part + ((size_t)i * NB + bk[i * NB]) * 4;
     double* o = out + ((((size_t)a * F + i) * V.C + c) * V.J + j) * 3;
-    o[0] = px[cur];
-    o[1] = py[cur];
-    o[2] = ps[cur];
-    if (i > 0) cur = bk[(size_t)i * 8 + cur];
+    o[0] = r[0];
+    o[1] = r[1];
+    o[2] = r[2];
   }
 }
 
@@ -789,22 +841,38 @@ int geometry_affinity(const double* cams, int C, const double* pts, const int32_
 
 size_t viterbi_scratch_bytes(int A, int F, int C, int J, int n_back) {
   const size_t chains = (size_t)A * C * J;
-  return chains * F * 8 + 256 + chains * F * n_back * n_back * sizeof(double);
+  const size_t rows = chains * F;
+  return rows * n_back * (n_back + 4) * sizeof(double) + rows + rows * n_back + 512;
 }
 
-// scratch: viterbi_scratch_bytes() -- int8 back-pointers, then the f64 transition table.
+// scratch: viterbi_scratch_bytes() -- transitions, particle records, particle counts, back-pointers.
 int viterbi_filter(const double* kp, int A, int F, int C, int J, double score_thr, int n_back, double thres_dist,
                    void* scratch, double* out, hipStream_t s) {
   const int chains = A * C * J;
   if (chains <= 0 || F <= 0) return 0;
-  if (n_back > 8 || n_back < 1) return -2;
-  int8_t* back = static_cast<int8_t*>(scratch);
-  double* trans = reinterpret_cast<double*>(static_cast<char*>(scratch) + (((size_t)chains * F * 8 + 255) & ~(size_t)255));
+  if (n_back > 3 || n_back < 1) return -2;
+  const size_t rows = (size_t)chains * F;
+  char* w = static_cast<char*>(scratch);
+  VitBufs W;
+  W.trans = reinterpret_cast<double*>(w);
+  W.part = reinterpret_cast<double*>(w + rows * n_back * n_back * sizeof(double));
+  W.cnt = reinterpret_cast<int8_t*>(w + rows * n_back * (n_back + 4) * sizeof(double));
+  W.bk = W.cnt + rows;
   VitChain V{kp, F, C, J, n_back, score_thr};
-  const size_t work = (size_t)chains * F * n_back * n_back;
+  const size_t work = rows * n_back * n_back;
   hipLaunchKernelGGL(viterbi_trans_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, V, chains, thres_dist,
-                     trans);
-  hipLaunchKernelGGL(viterbi_dp_kernel, dim3((chains + 63) / 64), dim3(64), 0, s, V, chains, trans, back, out);
+                     W);
+  // as many chains per block as their back-pointers fit in LDS (64 at 300 frames), else global
+  int threads = VIT_DP_THREADS;
+  while (threads > 8 && (size_t)threads * F * n_back > 160 * 1024) threads >>= 1;
+  const int in_lds = (size_t)threads * F * n_back <= 160 * 1024;
+  const size_t lds = in_lds ? (size_t)threads * F * n_back : 0;
+  const dim3 grid((chains + threads - 1) / threads);
+  switch (n_back) {
+    case 1: hipLaunchKernelGGL(viterbi_dp_kernel<1>, grid, dim3(threads), lds, s, V, chains, W, out, in_lds); break;
+    case 2: hipLaunchKernelGGL(viterbi_dp_kernel<2>, grid, dim3(threads), lds, s, V, chains, W, out, in_lds); break;
+    default: hipLaunchKernelGGL(viterbi_dp_kernel<3>, grid, dim3(threads), lds, s, V, chains, W, out, in_lds); break;
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -246,6 +246,39 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_eval_kernel(OptDims D, OptB
   if (t == 0) Bf.costF[(size_t)b * F + f] = tot;
 }
 
+// Sums over frames of the per-frame length terms, for every length variable: OPT_RCH frame chunks
+// (f = c, c + OPT_RCH, ...) per length, each an unrolled run of independent loads, then the chunk
+// partials in a fixed order -- deterministic, and latency-bound on ~F / OPT_RCH / 8 round trips
+// instead of F.  qLf: [F][NL] (qL partials); lenJ: [F][NL][5] (gradient l[4] l[3], diagonal l[3]^2).
+constexpr int OPT_RCH = OPT_THREADS / 32;
+__device__ __forceinline__ void len_partials(const OptDims& D, const double* __restrict__ qLf,
+                                             const double* __restrict__ lenJ, double (*pa)[OPT_MAXL],
+                                             double (*pb)[OPT_MAXL], int t) {
+  const int ch = t / 32;
+  for (int l = t % 32; l < D.NL; l += 32) {
+    double a = 0, bsum = 0;
+#pragma unroll 8
+    for (int f = ch; f < D.F; f += OPT_RCH) {
+      if (qLf) {
+        a += qLf[(size_t)f * D.NL + l];
+      } else {
+        const double* q = lenJ + ((size_t)f * D.NL + l) * 5;
+        a += q[4] * q[3];
+        bsum += q[3] * q[3];
+      }
+    }
+    pa[ch][l] = a;
+    if (pb) pb[ch][l] = bsum;
+  }
+}
+
+__device__ __forceinline__ double len_combine(const double (*p)[OPT_MAXL], int l) {
+  double s = p[0][l];
+#pragma unroll
+  for (int c = 1; c < OPT_RCH; ++c) s += p[c][l];
+  return s;
+}
+
 // cost[b] = sum_f costF (fixed order); mode 0 also reduces the length-variable gradient and diagonal.
 __global__ void __launch_bounds__(OPT_THREADS) optim_reduce_kernel(OptDims D, OptBufs Bf, double* cost_out, int mode) {
   const int b = blockIdx.x, t = threadIdx.x;
@@ -254,15 +287,14 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_reduce_kernel(OptDims D, Op
   for (int f = t; f < D.F; f += OPT_THREADS) s += Bf.costF[(size_t)b * D.F + f];
   const double tot = block_sum(s, red);
   if (t == 0) cost_out[b] = 0.5 * tot;  // scipy's cost convention
-  if (mode == 0 && !D.fix && t < D.NL) {
-    double gL = 0, E = 0;
-    for (int f = 0; f < D.F; ++f) {
-      const double* l = Bf.lenJ + (((size_t)b * D.F + f) * D.NL + t) * 5;
-      gL += l[4] * l[3];
-      E += l[3] * l[3];
+  if (mode == 0 && !D.fix) {
+    __shared__ double pg[OPT_RCH][OPT_MAXL], pe[OPT_RCH][OPT_MAXL];
+    len_partials(D, nullptr, Bf.lenJ + (size_t)b * D.F * D.NL * 5, pg, pe, t);
+    __syncthreads();
+    if (t < D.NL) {
+      Bf.g[(size_t)b * D.NV + D.NX + t] = len_combine(pg, t);
+      Bf.diag[(size_t)b * D.NV + D.NX + t] = len_combine(pe, t);
     }
-    Bf.g[(size_t)b * D.NV + D.NX + t] = gL;
-    Bf.diag[(size_t)b * D.NV + D.NX + t] = E;
   }
 }
 
@@ -840,11 +872,13 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_reduce_pq_kernel(OptDims D,
   __shared__ double red[OPT_THREADS];
   const double* P = (it & 1) ? Bf.P1 : Bf.P0;
   const size_t base = (size_t)b * D.NV;
+  __shared__ double part[OPT_RCH][OPT_MAXL];
   double s = 0;
   for (int f = t; f < D.F; f += OPT_THREADS) s += Bf.pqF[(size_t)b * D.F + f];
+  if (!D.fix) len_partials(D, Bf.qLf + (size_t)b * D.F * D.NL, nullptr, part, nullptr, t);
+  __syncthreads();
   if (!D.fix && t < D.NL) {
-    double qL = 0;
-    for (int f = 0; f < D.F; ++f) qL += Bf.qLf[((size_t)b * D.F + f) * D.NL + t];
+    double qL = len_combine(part, t);
     const size_t o = base + D.NX + t;
     qL += Bf.ctl[2 * b] * damp_of(Bf.diag[o]) * P[o];
     Bf.q[o] = qL;
@@ -869,7 +903,7 @@ __global__ void optim_accept_kernel(double* x, const double* xt, const double* c
 
 }  // namespace
 
-int g_optim_pcg_iters = 40;
+int g_optim_pcg_iters = 20;  // LM inner-solve cap: tools/optim_probe.py (cost within 3e-4 of scipy at 20; 40 costs 1.6x the time)
 
 size_t optim_workspace_bytes(int B, int F, int J, int NL) {
   const size_t NV = (size_t)F * J * 3 + NL;
