@@ -159,6 +159,22 @@ int mq_triangulate_pinv(mq_ctx* ctx, const double* cams, int n_cams, const doubl
 int mq_geometry_affinity(mq_ctx* ctx, const double* cams, int n_cams, const double* points, const int32_t* cam_of_det,
                          int B, int M, int J, double thr_kp, double* affinity, void* stream);
 
+/* step-2 matchSVT (step2_crossviewmatching.py:130-216) batched over B keyframes:
+ *   S          : float64 (B, Nmax, Nmax) affinity W of each keyframe (first n_det[b] rows / columns used)
+ *   n_det      : int32 (B) detections per keyframe (0 = empty keyframe), Nmax <= 64
+ *   cam_of_det : int32 (B, Nmax) camera index of each detection (the dimGroup slot); detections of one
+ *                camera form one zero block of X
+ *   alpha, lambda, mu, tol, max_iter, pselect: matchSVT's keywords (step 2 calls alpha 0.5, lambda 50,
+ *                mu 64, tol 5e-4, maxIter 500, pselect 1; dual_stochastic_SVT False -- not supported)
+ *   match      : uint8 (B, Nmax, Nmax) = X > 0.5 after the final symmetrisation (0 outside n_det)
+ *   x_out      : optional float64 (B, Nmax, Nmax) final X (NULL to skip)
+ *   iters      : int32 (B) the last iteration index (the reference's info["iter"]; -1 for empty keyframes)
+ * The SVD of the symmetric Y/mu + X is taken as its eigen-decomposition (parallel Jacobi in LDS,
+ * warm-started across iterations); see association.hip. */
+int mq_match_svt(mq_ctx* ctx, const double* S, const int32_t* n_det, const int32_t* cam_of_det, int B, int Nmax,
+                 double alpha, double lambda, double mu, double tol, int max_iter, int pselect, uint8_t* match,
+                 double* x_out, int32_t* iters, void* stream);
+
 /* filter_pose_viterbi over every (animal, camera, joint) chain of kp (A,F,C,J,3)
  * [x, y, score] (step 4 layout of kp2d.pickle) -> out (A,F,C,J,3).  Scratch is
  * owned by the context.  score_threshold 0.3, n_back 3, offset_threshold 25 in step 4 (n_back 1..3). */

@@ -729,6 +729,23 @@ int mq_geometry_affinity(mq_ctx* ctx, const double* cams, int C, const double* p
   return 0;
 }
 
+int mq_match_svt(mq_ctx* ctx, const double* S, const int32_t* n_det, const int32_t* cam_of_det, int B, int Nmax,
+                 double alpha, double lambda, double mu, double tol, int max_iter, int pselect, uint8_t* match,
+                 double* x_out, int32_t* iters, void* stream) {
+  if (!ctx || !S || !n_det || !cam_of_det || !match || !iters) return fail("mq_match_svt: null argument");
+  if (B < 0 || Nmax < 0) return fail("mq_match_svt: negative size", -2);
+  if (B == 0 || Nmax == 0) return 0;
+  if (Nmax > 64) return fail("mq_match_svt: at most 64 detections per keyframe", -2);
+  if ((int64_t)B * Nmax * Nmax > (int64_t)1 << 30) return fail("mq_match_svt: batch too large", -2);
+  if (max_iter < 1) return fail("mq_match_svt: max_iter must be >= 1", -2);
+  if (!(mu > 0) || !(tol >= 0)) return fail("mq_match_svt: mu must be > 0 and tol >= 0", -2);
+  HIP_TRY(hipSetDevice(ctx->device));
+  if (ctx->assoc_ws.ensure(mq::match_svt_workspace_bytes(B, Nmax))) return fail("match_svt workspace alloc failed", -5);
+  K_TRY(mq::match_svt(S, n_det, cam_of_det, B, Nmax, alpha, lambda, mu, tol, max_iter, pselect, ctx->assoc_ws.p, match,
+                      x_out, iters, (hipStream_t)stream));
+  return 0;
+}
+
 int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int A, int F, int C, int J, double score_threshold, int n_back,
                       double offset_threshold, double* out, void* stream) {
   if (!ctx || !kp || !out) return fail("mq_viterbi_filter: null argument");

@@ -18,4 +18,8 @@ int geometry_affinity(const double* cams, int C, const double* pts, const int32_
 int viterbi_filter(const double* kp, int A, int F, int C, int J, double score_thr, int n_back, double thres_dist,
                    void* scratch, double* out, hipStream_t s);
 size_t viterbi_scratch_bytes(int A, int F, int C, int J, int n_back);
+int match_svt(const double* S, const int32_t* n_det, const int32_t* cam_of_det, int B, int Nmax, double alpha,
+              double lambda, double mu, double tol, int max_iter, int pselect, void* ws, uint8_t* match,
+              double* x_out, int32_t* iters, hipStream_t s);
+size_t match_svt_workspace_bytes(int B, int Nmax);
 }  // namespace mq

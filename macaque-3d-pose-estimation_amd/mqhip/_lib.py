@@ -19,7 +19,7 @@ EXPORTED = [
     "mq_vitpose_create", "mq_vitpose_destroy", "mq_vitpose_set_param", "mq_vitpose_finalize",
     "mq_vitpose_set_graph", "mq_vitpose_timing", "mq_vitpose_timing_result", "mq_crop_udp", "mq_vitpose_forward", "mq_decode_udp", "mq_topdown",
     "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_triangulate_dlt", "mq_reproj_error",
-    "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_geometry_affinity", "mq_viterbi_filter", "mq_optim_points", "mq_attention_bf16",
+    "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_geometry_affinity", "mq_match_svt", "mq_viterbi_filter", "mq_optim_points", "mq_attention_bf16",
 ]
 
 
@@ -61,6 +61,7 @@ _SIGS = {
     "mq_triangulate_ransac": (i32, [vp, vp, i32, vp, i32, i32, f64, vp, vp, vp, vp, vp]),
     "mq_triangulate_pinv": (i32, [vp, vp, i32, vp, vp, i32, vp, vp]),
     "mq_geometry_affinity": (i32, [vp, vp, i32, vp, vp, i32, i32, i32, f64, vp, vp]),
+    "mq_match_svt": (i32, [vp, vp, vp, vp, i32, i32, f64, f64, f64, f64, i32, i32, vp, vp, vp, vp]),
     "mq_viterbi_filter": (i32, [vp, vp, i32, i32, i32, i32, f64, i32, f64, vp, vp]),
     "mq_attention_bf16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "mq_optim_points": (i32, [vp, vp, i32, vp, vp, i32, i32, i32, vp, i32, i32, vp, f64, f64, f64, i32, i32, i32,

@@ -308,3 +308,55 @@ def write_calibration_toml(cams, path):
             "translation": np.ravel(c["tvec"]).tolist(), "fisheye": False, "omnidir": True,
             "xi": np.ravel(c["xi"]).tolist(), "K": np.asarray(c["K"]).tolist(), "D": np.ravel(c["D"]).tolist()}
     dump_toml(calib, path)
+
+
+# ----------------------------------------------------------------------------- step-2 scenes
+
+def camparam_from_cams(cams):
+    """The reference's step-2 ``camparam`` dict (step2:35-75) of synthetic cameras."""
+    out = {"camera_id": [c["name"] for c in cams], "K": [], "xi": [], "D": [], "rvecs": [], "tvecs": [], "pmat": []}
+    for c in cams:
+        R = rodrigues_to_mat(c["rvec"])
+        t = np.asarray(c["tvec"], dtype=np.float64).reshape(3, 1)
+        out["K"].append(np.asarray(c["K"], dtype=np.float64))
+        out["xi"].append(np.asarray(c["xi"], dtype=np.float64).reshape(1, 1))
+        out["D"].append(np.asarray(c["D"], dtype=np.float64).reshape(1, 4))
+        out["rvecs"].append(np.asarray(c["rvec"], dtype=np.float64).reshape(3, 1))
+        out["tvecs"].append(t)
+        out["pmat"].append(np.hstack([R, t]))
+    return out
+
+
+ID_LABELS = (0, 2, 3, 5)  # the ID classifier's individual classes (step2:734)
+
+
+def make_alldata(cams, skel, noise_px=2.0, p_seen=0.9, p_dup=0.1, id_score=0.95, seed=5):
+    """Per-camera step-1 rows T[c][f] = [track id, x1, y1, x2, y2, [[x, y, s] x J], id, id score] of
+    skeletons (A, F, J, 3): each individual is seen by a camera with probability p_seen and gets a
+    spurious second (shifted) detection with probability p_dup; track id = individual index
+    (duplicates 10 + index); low-score keypoints are NaN as step 1 writes them."""
+    rng = np.random.default_rng(seed)
+    A, F, J, _ = skel.shape
+    T = []
+    for cam in cams:
+        uv_all = project_numpy(cam, skel.reshape(-1, 3)).reshape(A, F, J, 2)
+        rows_cam = []
+        for f in range(F):
+            rows = []
+            for a in range(A):
+                if rng.random() > p_seen:
+                    continue
+                for dup in ((False, True) if rng.random() < p_dup else (False,)):
+                    uv = uv_all[a, f] + rng.normal(0, noise_px, (J, 2)) + (rng.normal(0, 25.0, 2) if dup else 0.0)
+                    sc = rng.uniform(0.2, 1.0, J)
+                    sc[rng.random(J) < 0.08] = 0.05
+                    kp = np.concatenate([uv, sc[:, None]], axis=1)
+                    kp[sc < 0.1, :2] = np.nan
+                    x1, y1 = np.nanmin(uv, axis=0)
+                    x2, y2 = np.nanmax(uv, axis=0)
+                    cls = ID_LABELS[a % len(ID_LABELS)]
+                    rows.append([10 + a if dup else a, float(x1), float(y1), float(x2), float(y2), kp.tolist(),
+                                 cls, float(id_score * (0.5 if dup else 1.0))])
+            rows_cam.append(rows)
+        T.append(rows_cam)
+    return T

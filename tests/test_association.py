@@ -118,5 +118,5 @@ def test_step2_mirror_signature_matches_oracle():
     got = mirror(pts, dim, "unused.yaml", camparam=camparam)
     ref = geometry_affinity2(pts, dim, pmats, tvecs)
     np.testing.assert_allclose(got, ref, rtol=0, atol=1e-9, equal_nan=True)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(FileNotFoundError):  # as the reference: get_camparam opens config.yaml
         mirror(pts, dim, "unused.yaml")
