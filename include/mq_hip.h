@@ -114,9 +114,82 @@ int mq_topdown(mq_vitpose* model, const uint8_t* frames, int64_t frame_stride, i
 /* bf16 MFMA GEMM building block used by the forward: C[M,N] = A[M,K] * W[N,K]^T + bias
  * (A, W bf16 K-contiguous; leading dims in elements).  epilogue: 0 C bf16, 1 C bf16 with
  * exact-erf GELU, 2 C f32 += (residual), 3 C f32 = . + aux[m % aux_rows][n] (pos_embed),
- * 4 C f32, 5 C f32 scattered to [m / aux_rows][n][m % aux_rows] (NCHW).  bias/aux may be NULL. */
+ * 4 C f32, 5 C f32 scattered to [m / aux_rows][n][m % aux_rows] (NCHW), 6 C bf16 = max(., 0) (ReLU).
+ * bias/aux may be NULL. */
 int mq_gemm_bf16(mq_ctx* ctx, const void* A, const void* W, void* C, const float* bias, const float* aux, int M,
                  int N, int K, int lda, int ldw, int ldc, int aux_rows, int epilogue, void* stream);
+
+/* ======================================================================= detector
+ * Building blocks of the step-1 detector, Swin-S Mask R-CNN bbox only
+ * (model/detection/SWIN-Mask_R-CNN_bbox_only.py:29-226, inference_detector at step1_proc2d.py:226):
+ * the GEMMs and LayerNorms of the backbone / FPN / heads go through mq_gemm_bf16 and mq_layernorm;
+ * mqhip/detector.py sequences them.  Feature maps are NHWC f32, GEMM operands bf16 (uint16 storage).
+ * Pointers are device pointers unless marked host. */
+
+/* cv2.resize(INTER_LINEAR) of uint8 BGR frames (n_img, height, width, 3) to (new_h, new_w) with the
+ * 11-bit coefficient tables xofs/xalpha (new_w, 2 per x) and yofs/yalpha (new_h) (device int32), then
+ * BGR->RGB, (x - mean) / std, zero pad to (pad_h, pad_w), written as the 4x4 stride-4 patch-embed
+ * im2col operand: patches bf16 (n_img * pad_h/4 * pad_w/4, 64), k = c * 16 + kh * 4 + kw, k >= 48 zero. */
+int mq_det_resize_patch(mq_ctx* ctx, const uint8_t* frames, int64_t frame_stride, int n_img, int height, int width,
+                        int new_h, int new_w, int pad_h, int pad_w, const int32_t* xofs, const int32_t* xalpha,
+                        const int32_t* yofs, const int32_t* yalpha, uint16_t* patches, void* stream);
+
+/* LayerNorm over rows of f32 x (rows, dim), dim % 4 == 0 and <= 3072: y bf16 (out_f32 = 0) or f32. */
+int mq_layernorm(mq_ctx* ctx, const float* x, const float* gamma, const float* beta, void* y, int rows, int dim,
+                 float eps, int out_f32, void* stream);
+
+/* Swin (shifted) window attention, window 7, head_dim 32 (dim = 32 * heads): qkv bf16 (n_img * height *
+ * width, 3 * dim) of the LayerNorm-ed tokens, qkv_bias f32 (3 * dim) (the q/k/v of the zero-padded
+ * tokens), rel_table f32 (169, heads); out bf16 (n_img * height * width, dim).  shift 0 (W-MSA) or 3
+ * (SW-MSA); the zero pad to a multiple of 7, the cyclic shift and its -100 mask, window partition
+ * and reverse are done inside (ShiftWindowMSA + WindowMSA, mmdet swin.py). */
+int mq_window_attention(mq_ctx* ctx, const uint16_t* qkv, const float* qkv_bias, const float* rel_table, uint16_t* out,
+                        int n_img, int height, int width, int dim, int heads, int shift, void* stream);
+
+/* PatchMerging gather: x f32 (n_img, height, width, dim) -> out f32 (n_img * ceil(h/2) * ceil(w/2), 4 dim)
+ * in nn.Unfold(2, stride 2) order c * 4 + kh * 2 + kw (odd sizes zero padded at the bottom / right). */
+int mq_patch_merge_gather(mq_ctx* ctx, const float* x, int n_img, int height, int width, int dim, float* out,
+                          void* stream);
+
+/* FPN top-down: lo (n_img, lo_h, lo_w, ch) += nearest-resized hi (n_img, hi_h, hi_w, ch). */
+int mq_upsample_add(mq_ctx* ctx, float* lo, const float* hi, int n_img, int lo_h, int lo_w, int hi_h, int hi_w, int ch,
+                    void* stream);
+
+/* 3x3 / stride 1 / pad 1 im2col: x f32 NHWC -> out bf16 (n_img * h * w, 9 * ch), k = (ky * 3 + kx) * ch + c. */
+int mq_im2col3x3(mq_ctx* ctx, const float* x, int n_img, int height, int width, int ch, uint16_t* out, void* stream);
+
+/* max_pool2d(kernel 1, stride 2) = every other pixel: x f32 NHWC -> out (n_img, ceil(h/2), ceil(w/2), ch). */
+int mq_subsample2(mq_ctx* ctx, const float* x, int n_img, int height, int width, int ch, float* out, void* stream);
+
+/* mmcv batched_nms + nms (offset 0): per image, candidates with valid != 0, visited in descending score
+ * order (ties: lower index first), offset by level * (max coordinate + 1) when level != NULL; keep
+ * int32 (n_img, max_keep) candidate indices in visiting order (-1 past n_keep). n_cand <= 8192. */
+int mq_nms(mq_ctx* ctx, const float* boxes, const float* scores, const uint8_t* valid, const int8_t* level, int n_img,
+           int n_cand, float iou_thr, int max_keep, int32_t* keep, int32_t* n_keep, void* stream);
+
+/* RPNHead._predict_by_feat_single + _bbox_post_process for a batch: head f32 rows level-major over the
+ * batch (level l, image i, position p at row n_img * sum_{l'<l} h_l' w_l' + i * h_l w_l + p), 15 columns
+ * = the 3 anchor logits then 12 deltas (anchor-major); level_hw host
+ * int32 (n_levels, 2), strides host int32, base_anchors host f32 (n_levels, 3, 4).  Sigmoid, top nms_pre
+ * per level (stable descending), delta2bbox (stds 1, clip to img_h x img_w), w,h > 0, NMS per level,
+ * first max_keep: proposals f32 (n_img, max_keep, 4), scores (n_img, max_keep) (may be NULL), counts. */
+int mq_rpn_proposals(mq_ctx* ctx, const float* head, int n_img, int n_levels, const int32_t* level_hw,
+                     const int32_t* strides, const float* base_anchors, int nms_pre, float img_h, float img_w,
+                     float iou_thr, int max_keep, float* proposals, float* scores, int32_t* counts, void* stream);
+
+/* SingleRoIExtractor + RoIAlign(7, sampling 0, aligned): P2..P5 f32 NHWC with 256 channels (level_hw /
+ * strides host), rois f32 (n_img, max_rois, 4) with counts per image -> out bf16 (n_img * max_rois,
+ * 256 * 49) in (c, 7, 7) order (rows past a count are zero). */
+int mq_roi_align(mq_ctx* ctx, const float* p2, const float* p3, const float* p4, const float* p5,
+                 const int32_t* level_hw, const int32_t* strides, const float* rois, const int32_t* counts, int n_img,
+                 int max_rois, uint16_t* out, void* stream);
+
+/* Shared2FCBBoxHead.predict_by_feat + multiclass_nms (1 class): head f32 (n_img * max_rois, 6) = 2 logits
+ * (class, background) + 4 deltas; softmax, delta2bbox (stds 0.1 0.1 0.2 0.2), clip, * (inv_scale_w,
+ * inv_scale_h), score > score_thr, NMS, first max_det: det_boxes (n_img, max_det, 4), det_scores, counts. */
+int mq_rcnn_post(mq_ctx* ctx, const float* rois, const float* head, const int32_t* counts, int n_img, int max_rois,
+                 float img_h, float img_w, float inv_scale_w, float inv_scale_h, float score_thr, float iou_thr,
+                 int max_det, float* det_boxes, float* det_scores, int32_t* det_counts, void* stream);
 
 /* ======================================================================= geometry
  * Replaces aniposelib CameraGroup (cameras.py:593-783), anipose filter_pose_viterbi

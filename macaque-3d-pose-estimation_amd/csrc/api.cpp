@@ -7,6 +7,7 @@
 // caller's input/output pointers).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -15,6 +16,7 @@
 #include <vector>
 
 #include "geometry.hpp"
+#include "detector.hpp"
 #include "kernels.hpp"
 #include "mq_hip.h"
 
@@ -71,6 +73,7 @@ struct mq_ctx {
   DevBuf decode_work;
   DevBuf optim_ws;
   DevBuf assoc_ws;  // step-2 affinity: rays + pairwise distances
+  DevBuf det_ws;    // detector post-processing (sort, NMS masks)
 };
 
 struct ParamSlot {
@@ -185,6 +188,7 @@ int mq_destroy(mq_ctx* ctx) {
   ctx->decode_work.release();
   ctx->optim_ws.release();
   ctx->assoc_ws.release();
+  ctx->det_ws.release();
   delete ctx;
   return 0;
 }
@@ -645,13 +649,173 @@ int mq_gemm_bf16(mq_ctx* ctx, const void* A, const void* W, void* C, const float
                  int N, int K, int lda, int ldw, int ldc, int aux_rows, int epilogue, void* stream) {
   if (!ctx || !A || !W || !C) return fail("mq_gemm_bf16: null argument");
   if (M <= 0 || N <= 0 || K <= 0) return fail("mq_gemm_bf16: bad sizes", -2);
-  if (epilogue < 0 || epilogue > 5) return fail("mq_gemm_bf16: bad epilogue", -2);
+  if (epilogue < 0 || epilogue > 6) return fail("mq_gemm_bf16: bad epilogue", -2);
   if ((epilogue == mq::EPI_POS_F32 || epilogue == mq::EPI_NCHW_F32) && (!aux_rows || (!aux && epilogue == 3)))
     return fail("mq_gemm_bf16: epilogue needs aux", -2);
   HIP_TRY(hipSetDevice(ctx->device));
   mq::GemmArgs g{(const unsigned short*)A, (const unsigned short*)W, C, bias, aux, M, N, K, lda, ldw, ldc, aux_rows};
   int rc = mq::gemm_bf16(g, epilogue, (hipStream_t)stream);
   if (rc) return fail("mq_gemm_bf16: launch failed / unsupported shape (K % 32, lda/ldw % 8)", -6);
+  return 0;
+}
+
+// ----------------------------------------------------------------------------- detector
+static int check_det(mq_ctx* ctx) {
+  if (!ctx) return fail("null ctx");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail("hipSetDevice failed", -5);
+  return 0;
+}
+
+int mq_det_resize_patch(mq_ctx* ctx, const uint8_t* frames, int64_t frame_stride, int n_img, int height, int width,
+                        int new_h, int new_w, int pad_h, int pad_w, const int32_t* xofs, const int32_t* xalpha,
+                        const int32_t* yofs, const int32_t* yalpha, uint16_t* patches, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!frames || !xofs || !xalpha || !yofs || !yalpha || !patches) return fail("mq_det_resize_patch: null argument");
+  if (n_img <= 0 || height <= 0 || width <= 0 || new_h <= 0 || new_w <= 0 || pad_h < new_h || pad_w < new_w ||
+      pad_h % 4 || pad_w % 4)
+    return fail("mq_det_resize_patch: bad sizes (padded size must cover the resize and be a multiple of 4)", -2);
+  K_TRY(mq::det_resize_patch(frames, frame_stride, n_img, height, width, new_h, new_w, pad_h, pad_w, xofs, xalpha, yofs,
+                             yalpha, patches, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_layernorm(mq_ctx* ctx, const float* x, const float* gamma, const float* beta, void* y, int rows, int dim,
+                 float eps, int out_f32, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !gamma || !beta || !y) return fail("mq_layernorm: null argument");
+  if (rows < 0 || dim <= 0 || dim % 4 || dim > 3072) return fail("mq_layernorm: dim must be a multiple of 4, <= 3072", -2);
+  if (rows == 0) return 0;
+  if (out_f32)
+    K_TRY(mq::layernorm_f32_f32(x, gamma, beta, (float*)y, rows, dim, eps, (hipStream_t)stream));
+  else
+    K_TRY(mq::layernorm_f32_bf16(x, gamma, beta, (unsigned short*)y, rows, dim, eps, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_window_attention(mq_ctx* ctx, const uint16_t* qkv, const float* qkv_bias, const float* rel_table, uint16_t* out,
+                        int n_img, int height, int width, int dim, int heads, int shift, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!qkv || !qkv_bias || !rel_table || !out) return fail("mq_window_attention: null argument");
+  if (n_img <= 0 || height <= 0 || width <= 0 || heads <= 0 || dim != heads * 32)
+    return fail("mq_window_attention: head_dim must be 32 (dim = 32 * heads)", -2);
+  if (shift < 0 || shift >= 7) return fail("mq_window_attention: shift must be in [0, 7)", -2);
+  K_TRY(mq::window_attention(qkv, qkv_bias, rel_table, out, n_img, height, width, dim, heads, shift,
+                             (hipStream_t)stream));
+  return 0;
+}
+
+int mq_patch_merge_gather(mq_ctx* ctx, const float* x, int n_img, int height, int width, int dim, float* out,
+                          void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !out) return fail("mq_patch_merge_gather: null argument");
+  if (n_img <= 0 || height <= 0 || width <= 0 || dim <= 0) return fail("mq_patch_merge_gather: bad sizes", -2);
+  K_TRY(mq::merge_gather(x, n_img, height, width, dim, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_upsample_add(mq_ctx* ctx, float* lo, const float* hi, int n_img, int lo_h, int lo_w, int hi_h, int hi_w, int ch,
+                    void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!lo || !hi) return fail("mq_upsample_add: null argument");
+  if (n_img <= 0 || lo_h <= 0 || lo_w <= 0 || hi_h <= 0 || hi_w <= 0 || ch <= 0) return fail("mq_upsample_add: bad sizes", -2);
+  K_TRY(mq::upsample_add(lo, hi, n_img, lo_h, lo_w, hi_h, hi_w, ch, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_im2col3x3(mq_ctx* ctx, const float* x, int n_img, int height, int width, int ch, uint16_t* out, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !out) return fail("mq_im2col3x3: null argument");
+  if (n_img <= 0 || height <= 0 || width <= 0 || ch <= 0 || ch % 4) return fail("mq_im2col3x3: bad sizes", -2);
+  K_TRY(mq::im2col3x3(x, n_img, height, width, ch, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_subsample2(mq_ctx* ctx, const float* x, int n_img, int height, int width, int ch, float* out, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !out) return fail("mq_subsample2: null argument");
+  if (n_img <= 0 || height <= 0 || width <= 0 || ch <= 0) return fail("mq_subsample2: bad sizes", -2);
+  K_TRY(mq::subsample2(x, n_img, height, width, ch, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_nms(mq_ctx* ctx, const float* boxes, const float* scores, const uint8_t* valid, const int8_t* level, int n_img,
+           int n_cand, float iou_thr, int max_keep, int32_t* keep, int32_t* n_keep, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!boxes || !scores || !valid || !keep || !n_keep) return fail("mq_nms: null argument");
+  if (n_img <= 0 || n_cand <= 0 || n_cand > 8192 || max_keep <= 0) return fail("mq_nms: 1 <= n_cand <= 8192", -2);
+  if (ctx->det_ws.ensure(mq::nms_workspace_bytes(n_img, n_cand))) return fail("nms workspace alloc failed", -5);
+  K_TRY(mq::nms_batched(boxes, scores, valid, level, n_img, n_cand, iou_thr, max_keep, ctx->det_ws.p, keep, n_keep,
+                        (hipStream_t)stream));
+  return 0;
+}
+
+int mq_rpn_proposals(mq_ctx* ctx, const float* head, int n_img, int n_levels, const int32_t* level_hw,
+                     const int32_t* strides, const float* base_anchors, int nms_pre, float img_h, float img_w,
+                     float iou_thr, int max_keep, float* proposals, float* scores, int32_t* counts, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!head || !level_hw || !strides || !base_anchors || !proposals || !counts)
+    return fail("mq_rpn_proposals: null argument");
+  if (n_img <= 0 || n_levels <= 0 || n_levels > 6 || nms_pre <= 0 || max_keep <= 0 || n_img * n_levels > 1024)
+    return fail("mq_rpn_proposals: bad sizes", -2);
+  mq::DetLevels lv{};
+  lv.n = n_levels;
+  int rows = 0, cand = 0;
+  for (int l = 0; l < n_levels; ++l) {
+    lv.h[l] = level_hw[2 * l];
+    lv.w[l] = level_hw[2 * l + 1];
+    lv.stride[l] = strides[l];
+    if (lv.h[l] <= 0 || lv.w[l] <= 0 || lv.stride[l] <= 0) return fail("mq_rpn_proposals: bad level size", -2);
+    lv.row_off[l] = rows;
+    lv.cand_off[l] = cand;
+    rows += lv.h[l] * lv.w[l];
+    cand += std::min(lv.h[l] * lv.w[l] * 3, nms_pre);
+    for (int a = 0; a < 3; ++a)
+      for (int k = 0; k < 4; ++k) lv.base[l][a][k] = base_anchors[(l * 3 + a) * 4 + k];
+  }
+  lv.cand_total = cand;
+  if (cand > 8192) return fail("mq_rpn_proposals: more than 8192 candidates per image", -2);
+  int32_t* keep_buf = nullptr;
+  const size_t keep_bytes = ((size_t)n_img * max_keep * 4 + 255) & ~(size_t)255;
+  const size_t need = mq::rpn_workspace_bytes(n_img, rows, cand, n_levels) + keep_bytes;
+  if (ctx->det_ws.ensure(need)) return fail("rpn workspace alloc failed", -5);
+  keep_buf = reinterpret_cast<int32_t*>(ctx->det_ws.as<char>() + (need - keep_bytes));
+  K_TRY(mq::rpn_proposals(head, lv, n_img, rows, img_h, img_w, iou_thr, max_keep, ctx->det_ws.p, need - keep_bytes,
+                          proposals, scores, counts, keep_buf, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_roi_align(mq_ctx* ctx, const float* p2, const float* p3, const float* p4, const float* p5,
+                 const int32_t* level_hw, const int32_t* strides, const float* rois, const int32_t* counts, int n_img,
+                 int max_rois, uint16_t* out, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!p2 || !p3 || !p4 || !p5 || !level_hw || !strides || !rois || !counts || !out)
+    return fail("mq_roi_align: null argument");
+  if (n_img <= 0 || max_rois <= 0) return fail("mq_roi_align: bad sizes", -2);
+  mq::DetFeats fs{};
+  const float* ps[4] = {p2, p3, p4, p5};
+  for (int l = 0; l < 4; ++l) {
+    fs.p[l] = ps[l];
+    fs.h[l] = level_hw[2 * l];
+    fs.w[l] = level_hw[2 * l + 1];
+    fs.stride[l] = strides[l];
+    if (fs.h[l] <= 0 || fs.w[l] <= 0 || fs.stride[l] <= 0) return fail("mq_roi_align: bad level size", -2);
+  }
+  K_TRY(mq::roi_align(fs, rois, counts, n_img, max_rois, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_rcnn_post(mq_ctx* ctx, const float* rois, const float* head, const int32_t* counts, int n_img, int max_rois,
+                 float img_h, float img_w, float inv_scale_w, float inv_scale_h, float score_thr, float iou_thr,
+                 int max_det, float* det_boxes, float* det_scores, int32_t* det_counts, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!rois || !head || !counts || !det_boxes || !det_scores || !det_counts) return fail("mq_rcnn_post: null argument");
+  if (n_img <= 0 || max_rois <= 0 || max_rois > 8192 || max_det <= 0) return fail("mq_rcnn_post: bad sizes", -2);
+  const size_t keep_bytes = ((size_t)n_img * max_det * 4 + 255) & ~(size_t)255;
+  const size_t need = mq::rcnn_workspace_bytes(n_img, max_rois) + keep_bytes;
+  if (ctx->det_ws.ensure(need)) return fail("rcnn workspace alloc failed", -5);
+  int32_t* keep_buf = reinterpret_cast<int32_t*>(ctx->det_ws.as<char>() + (need - keep_bytes));
+  K_TRY(mq::rcnn_post(rois, head, counts, n_img, max_rois, img_h, img_w, inv_scale_w, inv_scale_h, score_thr, iou_thr,
+                      max_det, ctx->det_ws.p, det_boxes, det_scores, det_counts, keep_buf, (hipStream_t)stream));
   return 0;
 }
 

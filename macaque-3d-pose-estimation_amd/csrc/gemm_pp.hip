@@ -116,7 +116,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = make_float4(bv[j][0], bv[j][1], bv[j][2], bv[j][3]);
   const bool full = (m0 + PP_BM <= p.M) && (n0 + PP_BN <= p.N);
-  if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) {
+  if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
     // pair fragments (j, j+1): v_permlane16_swap gives every lane 8 consecutive columns -> one
     // 16-byte store per lane per pair
     const bool odd = (lane >> 4) & 1;
@@ -139,6 +139,10 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
             v[1] = g0.y;
             v[2] = g1.x;
             v[3] = g1.y;
+          }
+          if constexpr (EPI == EPI_RELU_BF16) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
           }
           pk[h][0] = pack_bf16x2(v[0], v[1]);
           pk[h][1] = pack_bf16x2(v[2], v[3]);
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   if (wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
 
   // >= this many epilogue stores of a full tile are younger than the DMA the next two waits retire
-  constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16) ? 16 : 32;
+  constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) ? 16 : 32;
   bool stores_pending = false;
   for (int g = 0; g < total; ++g) {
     const int slot = g & 1;
@@ -425,6 +429,7 @@ int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
   switch (epi) {
     case EPI_BF16: launch_pp<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_RESID_F32: launch_pp<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_POS_F32: launch_pp<EPI_POS_F32>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_F32: launch_pp<EPI_F32>(grid, stream, p, tiles_m, tiles_n); break;

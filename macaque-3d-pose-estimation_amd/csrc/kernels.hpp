@@ -12,6 +12,7 @@ enum GemmEpilogue {
   EPI_POS_F32 = 3,    // C f32 = acc + bias + aux[m % aux_rows][n]   (patch embed + pos_embed)
   EPI_F32 = 4,        // C f32 = acc + bias
   EPI_NCHW_F32 = 5,   // C f32 [m / aux_rows][n][m % aux_rows] = acc + bias (1x1 conv -> NCHW)
+  EPI_RELU_BF16 = 6,  // C bf16 = max(acc + bias, 0)   (detector convs / fc layers)
 };
 
 struct GemmArgs {
@@ -36,6 +37,8 @@ int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
                        float eps, hipStream_t s);
+int layernorm_f32_f32(const float* x, const float* gamma, const float* beta, float* y, int rows, int dim, float eps,
+                      hipStream_t s);
 extern int g_attention_v2;  // 1 (default): attention2_kernel; 0: the first-generation kernel
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s);

@@ -7,10 +7,10 @@
 namespace mq {
 
 // ---------------------------------------------------------------- LayerNorm
-// One wave per row: fp32 residual stream in, bf16 normalised out (eps 1e-6).
-template <int MAXIT>
+// One wave per row: fp32 in, bf16 (GEMM operand) or f32 (residual stream) out.
+template <int MAXIT, bool OUT_F32>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                         const float* __restrict__ b, bf16_t* __restrict__ y,
+                                                         const float* __restrict__ b, void* __restrict__ yv,
                                                          int rows, int dim, float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -43,28 +43,46 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     }
   }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)dim + eps);
-  bf16_t* yr = y + (size_t)row * dim;
 #pragma unroll
   for (int it = 0; it < MAXIT; ++it) {
     const int i = it * 256 + lane * 4;
     if (i < dim) {
-      uint2 o;
-      o.x = pack_bf16x2((v[it].x - mean) * rstd * gg[it].x + bb[it].x, (v[it].y - mean) * rstd * gg[it].y + bb[it].y);
-      o.y = pack_bf16x2((v[it].z - mean) * rstd * gg[it].z + bb[it].z, (v[it].w - mean) * rstd * gg[it].w + bb[it].w);
-      *reinterpret_cast<uint2*>(yr + i) = o;
+      const float o0 = (v[it].x - mean) * rstd * gg[it].x + bb[it].x, o1 = (v[it].y - mean) * rstd * gg[it].y + bb[it].y;
+      const float o2 = (v[it].z - mean) * rstd * gg[it].z + bb[it].z, o3 = (v[it].w - mean) * rstd * gg[it].w + bb[it].w;
+      if constexpr (OUT_F32) {
+        *reinterpret_cast<float4*>((float*)yv + (size_t)row * dim + i) = make_float4(o0, o1, o2, o3);
+      } else {
+        uint2 o;
+        o.x = pack_bf16x2(o0, o1);
+        o.y = pack_bf16x2(o2, o3);
+        *reinterpret_cast<uint2*>((bf16_t*)yv + (size_t)row * dim + i) = o;
+      }
     }
   }
 }
 
+template <bool OUT_F32>
+static int launch_layernorm(const float* x, const float* gamma, const float* beta, void* y, int rows, int dim,
+                            float eps, hipStream_t s) {
+  if (dim % 4 || dim > 3072) return -1;
+  dim3 grid((rows + 3) / 4), block(256);
+  if (dim <= 512)
+    hipLaunchKernelGGL((layernorm_kernel<2, OUT_F32>), grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
+  else if (dim <= 1280)
+    hipLaunchKernelGGL((layernorm_kernel<5, OUT_F32>), grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
+  else
+    hipLaunchKernelGGL((layernorm_kernel<12, OUT_F32>), grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
                        float eps, hipStream_t s) {
-  if (dim % 4 || dim > 2048) return -1;
-  dim3 grid((rows + 3) / 4), block(256);
-  if (dim <= 1280)
-    hipLaunchKernelGGL(layernorm_kernel<5>, grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
-  else
-    hipLaunchKernelGGL(layernorm_kernel<8>, grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
+  return launch_layernorm<false>(x, gamma, beta, y, rows, dim, eps, s);
+}
+
+int layernorm_f32_f32(const float* x, const float* gamma, const float* beta, float* y, int rows, int dim, float eps,
+                      hipStream_t s) {
+  return launch_layernorm<true>(x, gamma, beta, y, rows, dim, eps, s);
 }
 
 // ---------------------------------------------------------------- attention

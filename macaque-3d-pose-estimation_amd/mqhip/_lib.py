@@ -19,7 +19,9 @@ EXPORTED = [
     "mq_vitpose_create", "mq_vitpose_destroy", "mq_vitpose_set_param", "mq_vitpose_finalize",
     "mq_vitpose_set_graph", "mq_vitpose_timing", "mq_vitpose_timing_result", "mq_crop_udp", "mq_vitpose_forward", "mq_decode_udp", "mq_topdown",
     "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_triangulate_dlt", "mq_reproj_error",
-    "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_geometry_affinity", "mq_match_svt", "mq_viterbi_filter", "mq_optim_points", "mq_attention_bf16",
+    "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_geometry_affinity", "mq_match_svt", "mq_viterbi_filter",
+    "mq_det_resize_patch", "mq_layernorm", "mq_window_attention", "mq_patch_merge_gather", "mq_upsample_add",
+    "mq_im2col3x3", "mq_subsample2", "mq_nms", "mq_rpn_proposals", "mq_roi_align", "mq_rcnn_post", "mq_optim_points", "mq_attention_bf16",
 ]
 
 
@@ -34,6 +36,7 @@ vp = C.c_void_p
 i32 = C.c_int
 i64 = C.c_int64
 f64 = C.c_double
+f32 = C.c_float
 
 _SIGS = {
     "mq_abi_version": (i32, []),
@@ -62,6 +65,17 @@ _SIGS = {
     "mq_triangulate_pinv": (i32, [vp, vp, i32, vp, vp, i32, vp, vp]),
     "mq_geometry_affinity": (i32, [vp, vp, i32, vp, vp, i32, i32, i32, f64, vp, vp]),
     "mq_match_svt": (i32, [vp, vp, vp, vp, i32, i32, f64, f64, f64, f64, i32, i32, vp, vp, vp, vp]),
+    "mq_det_resize_patch": (i32, [vp, vp, i64, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp]),
+    "mq_layernorm": (i32, [vp, vp, vp, vp, vp, i32, i32, f32, i32, vp]),
+    "mq_window_attention": (i32, [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "mq_patch_merge_gather": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+    "mq_upsample_add": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+    "mq_im2col3x3": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+    "mq_subsample2": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+    "mq_nms": (i32, [vp, vp, vp, vp, vp, i32, i32, f32, i32, vp, vp, vp]),
+    "mq_rpn_proposals": (i32, [vp, vp, i32, i32, vp, vp, vp, i32, f32, f32, f32, i32, vp, vp, vp, vp]),
+    "mq_roi_align": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, vp]),
+    "mq_rcnn_post": (i32, [vp, vp, vp, vp, i32, i32, f32, f32, f32, f32, f32, f32, i32, vp, vp, vp, vp]),
     "mq_viterbi_filter": (i32, [vp, vp, i32, i32, i32, i32, f64, i32, f64, vp, vp]),
     "mq_attention_bf16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "mq_optim_points": (i32, [vp, vp, i32, vp, vp, i32, i32, i32, vp, i32, i32, vp, f64, f64, f64, i32, i32, i32,
