@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--resident-frames", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-lift", action="store_true", help="skip the config-4 lift timing (extra keys)")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 detector + pose timing (extra keys)")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a hipGraph (disables live timing)")
     return ap.parse_args()
 
@@ -141,6 +142,7 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
     t1, tri1 = frame_pass(CONFIGS["base"], 4, 4)
     lift = lift_cpu(cams_np)
     log(f"cpu baseline: config-4 lift {lift['total_s']:.1f} s")
+    det = detector_cpu(reps=min(reps, 3))
     return {"value": round(N_ANIMALS / t_frame2, 5), "unit": "individuals×frames/s", "cores": threads,
             "kind": "port", "nproc": info["nproc"], "os_cpu_count": info["os_cpu_count"], "cpu_model": info["model"],
             "statistic": f"median of {reps} after 1 warm-up",
@@ -150,7 +152,36 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
             "seconds_per_frame": round(t_frame2, 4),
             "config1": {"seconds_per_frame": round(t1 + tri1, 4), "individuals_frames_per_s": round(1.0 / (t1 + tri1), 4),
                         "sample": "ViT-B fp32 flip-test forward + decode of 4 crops (4 views x 1 individual) + DLT"},
-            "config4_lift": lift}
+            "config4_lift": lift,
+            "config5_detector": det}
+
+
+def detector_cpu(reps=3):
+    """Config-5 detection stage on the CPU port (oracle/swin_det.py, torch fp32): resize +
+    normalise + Swin-S + FPN + RPN head convolutions of ONE 1536x2048 view, x8 views.  The RPN
+    selection, RoIAlign and box head are excluded from the sample (the oracle's RoIAlign is a
+    Python loop that would dominate and say nothing about the reference)."""
+    import numpy as np
+    import torch
+    import torch.nn.functional as F
+    from oracle import swin_det as sd
+    w = sd.make_weights(sd.SWIN_S, seed=0)
+    img = np.random.default_rng(0).integers(0, 256, (IMG_H, IMG_W, 3), dtype=np.uint8)
+
+    def run():
+        with torch.no_grad():
+            x, _, _ = sd.preprocess(img)
+            p = sd.fpn_forward(sd.swin_forward(x, w), w)
+            for f in p:
+                h = F.relu(F.conv2d(f, w["rpn_head.rpn_conv.weight"], w["rpn_head.rpn_conv.bias"], padding=1))
+                F.conv2d(h, w["rpn_head.rpn_cls.weight"], w["rpn_head.rpn_cls.bias"])
+                F.conv2d(h, w["rpn_head.rpn_reg.weight"], w["rpn_head.rpn_reg.bias"])
+
+    t, _ = _median_time(run, reps)
+    log(f"cpu baseline: detector backbone + FPN + RPN head, 1 view {t:.2f} s (median of {reps})")
+    return {"seconds_per_frame": round(t * N_VIEWS, 3), "seconds_per_view": round(t, 3),
+            "sample": "oracle Swin-S + FPN + RPN head convolutions of 1 of the frame's 8 views (x8); RPN selection, "
+                      "RoIAlign and the box head excluded", "statistic": f"median of {reps} after 1 warm-up"}
 
 
 def lift_inputs(A=4, F=300, C=8, seed=2):
@@ -250,6 +281,68 @@ def lift_gpu(device, reps=3):
             "optim_lm_iterations": stats[:, 2].tolist(), "statistic": f"median of {reps} after 1 warm-up",
             "workload": f"BASELINE config 4: {F} frames x {C} views x {A} individuals x {J} joints, ransac + optim",
             "note": "wall time per stage through the drop-in numpy API (host<->device copies included)"}
+
+
+def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
+    """BASELINE config 5 on one GPU, without the tracker / ID classifier (out of scope): per frame,
+    the Swin-S Mask R-CNN detector on all 8 views (1536x2048), the 4 best detections of every view
+    as crop boxes, ViTPose flip test + UDP decode on those 32 crops, omnidir DLT of the frame.
+    Median-free: `steps` frames timed back to back after 2 warm-ups (frames resident in HBM)."""
+    import torch
+    from mqhip import _lib
+    from mqhip.detector import SwinDetectorHip, make_random_weights
+    det = SwinDetectorHip(make_random_weights(seed=0), device=device)
+    lib, ctx = pose_model.lib, pose_model.ctx
+    dev = torch.device("cuda", device)
+    cfg = pose_model.cfg
+    n = N_VIEWS * N_ANIMALS
+    crops = torch.empty((n, 3, 256, 192), device=dev)
+    center = torch.empty((n, 2), device=dev)
+    scale = torch.empty((n, 2), device=dev)
+    hm = torch.empty((n, cfg.n_joints, 64, 48), device=dev)
+    kp = torch.empty((n, cfg.n_joints, 2), device=dev, dtype=torch.float64)
+    score = torch.empty((n, cfg.n_joints), device=dev)
+    am = torch.empty((n, cfg.n_joints), device=dev, dtype=torch.int32)
+    p3d = torch.empty((N_ANIMALS * cfg.n_joints, 3), device=dev, dtype=torch.float64)
+    box_frame = torch.arange(n, device=dev, dtype=torch.int32) // N_ANIMALS
+    s_ptr = _lib.stream_ptr(dev)
+
+    def one(i):
+        fr = frames[i % frames.shape[0]]
+        boxes, _, _ = det.forward(fr)
+        bx = boxes[:, :N_ANIMALS].reshape(-1, 4).contiguous()  # detections are score-ordered
+        _lib.check(lib.mq_crop_udp(ctx.handle, _lib.ptr(fr), IMG_H * IMG_W * 3, IMG_H, IMG_W, _lib.ptr(bx),
+                                   _lib.ptr(box_frame), n, _lib.ptr(crops), _lib.ptr(center), _lib.ptr(scale),
+                                   s_ptr), "crop")
+        _lib.check(lib.mq_vitpose_forward(pose_model.handle, _lib.ptr(crops), n, 1, _lib.ptr(hm), s_ptr), "forward")
+        _lib.check(lib.mq_decode_udp(ctx.handle, _lib.ptr(hm), n, cfg.n_joints, 64, 48, _lib.ptr(center),
+                                     _lib.ptr(scale), _lib.ptr(kp), _lib.ptr(score), _lib.ptr(am), None, s_ptr),
+                   "decode")
+        pts = torch.where((score < TRI_THR).unsqueeze(-1), torch.full_like(kp, float("nan")), kp)
+        pts = pts.view(N_VIEWS, N_ANIMALS * cfg.n_joints, 2).contiguous()
+        _lib.check(lib.mq_triangulate_dlt(ctx.handle, _lib.ptr(cams_dev), N_VIEWS, _lib.ptr(pts),
+                                          N_ANIMALS * cfg.n_joints, 1, _lib.ptr(p3d), s_ptr), "dlt")
+
+    for i in range(2):
+        one(i)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        det.forward(frames[i % frames.shape[0]])
+    torch.cuda.synchronize(dev)
+    det_ms = (time.perf_counter() - t0) * 1e3 / steps
+    t0 = time.perf_counter()
+    for i in range(steps):
+        one(i)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    log(f"config 5: detector {det_ms:.2f} ms / frame, detector + pose + DLT {ms:.2f} ms / frame")
+    return {"workload": "BASELINE config 5 per GPU without tracker / ID classifier: Swin-S Mask R-CNN on 8 views "
+                        "1536x2048 -> 4 best detections per view -> ViTPose-%s flip test + UDP decode (32 crops) "
+                        "-> omnidir DLT" % cfg.name,
+            "ms_per_frame": round(ms, 3), "detector_ms_per_frame": round(det_ms, 3),
+            "individuals_frames_per_s": round(N_ANIMALS / (ms * 1e-3), 2), "frames_timed": steps,
+            "data": "random detector and pose weights, random frames (the detector returns 100 boxes per view)"}
 
 
 def main():
@@ -407,6 +500,8 @@ def main():
     log(f"timed region {dt:.3f} s")
     if rank == 0 and world == 1 and not args.no_lift:
         result["lift_config4"] = lift_gpu(local)
+    if rank == 0 and world == 1 and not args.no_config5:
+        result["config5"] = config5_gpu(local, model, frames[:, :N_VIEWS] if frames.dim() == 5 else frames, cams_dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cams_np)
         if "lift_config4" in result:

@@ -11,7 +11,7 @@
 //   upsample_add       FPN top-down: lo += nearest(hi)
 //   im2col3x3          NHWC f32 -> bf16 (rows, 9 C), tap-major K = (ky * 3 + kx) * C + c, zero pad 1
 //   subsample2         P6 = max_pool2d(P5, 1, stride 2)
-//   rpn_scores / rpn_decode   sigmoid, per-level top-k (rocprim segmented radix sort, stable),
+//   rpn_scores / rpn_decode   sigmoid, per-level top-k (one stable rocprim radix sort on (segment, score) keys),
 //                      anchors + delta2bbox + clip + w,h > 0
 //   nms_sort / nms_mask / nms_sweep   mmcv batched_nms: level offsets, descending-score order
 //                      (ties: candidate order), bitmask IoU (inter > thr * union), greedy sweep
@@ -21,7 +21,7 @@
 // Box arithmetic follows mmdet's operation order in float32 (compiled without FMA contraction).
 #include <cstring>
 
-#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "common.hpp"
 #include "detector.hpp"
@@ -314,8 +314,11 @@ __device__ __forceinline__ int det_level_of(const DetLevels& lv, int row) {
   return l;
 }
 
+// sort key: (segment = image * levels + level) above the descending score, so one stable radix sort
+// orders every segment by descending score (ties: lower anchor index first) in place
 __global__ void rpn_scores_kernel(const float* __restrict__ head, const DetLevels lv, int rows_per_img, int n_img,
-                                  float* __restrict__ scores, int32_t* __restrict__ ids) {
+                                  float* __restrict__ scores, int32_t* __restrict__ ids,
+                                  unsigned long long* __restrict__ keys) {
   const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t per = (int64_t)rows_per_img * 3;
   if (idx >= (int64_t)n_img * per) return;
@@ -326,21 +329,16 @@ __global__ void rpn_scores_kernel(const float* __restrict__ head, const DetLevel
   const int pos = r - lv.row_off[l];
   const int64_t hrow = (int64_t)n_img * lv.row_off[l] + (int64_t)img * lv.h[l] * lv.w[l] + pos;
   const float x = head[hrow * 15 + a];
-  scores[idx] = 1.0f / (1.0f + expf(-x));
+  const float sc = 1.0f / (1.0f + expf(-x));
+  scores[idx] = sc;
   ids[idx] = local;
-}
-
-__global__ void rpn_segments_kernel(const DetLevels lv, int n_img, int rows_per_img, int32_t* __restrict__ seg) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= n_img * lv.n) return;
-  const int i = idx / lv.n, l = idx % lv.n;
-  const int b = i * rows_per_img * 3 + lv.row_off[l] * 3;
-  seg[idx] = b;
-  seg[n_img * lv.n + idx] = b + lv.h[l] * lv.w[l] * 3;
+  unsigned u = __float_as_uint(sc);
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  keys[idx] = ((unsigned long long)(img * lv.n + l) << 32) | (unsigned long long)(~u);
 }
 
 // decode the top-k of every (image, level): candidates of an image are level-major, rank order
-__global__ void rpn_decode_kernel(const float* __restrict__ head, const float* __restrict__ sorted_scores,
+__global__ void rpn_decode_kernel(const float* __restrict__ head, const float* __restrict__ scores,
                                   const int32_t* __restrict__ sorted_ids, const DetLevels lv, int n_img,
                                   int rows_per_img, float img_h, float img_w, float* __restrict__ boxes,
                                   float* __restrict__ cand_scores, uint8_t* __restrict__ valid,
@@ -354,7 +352,7 @@ __global__ void rpn_decode_kernel(const float* __restrict__ head, const float* _
   const int r = c - lv.cand_off[l];
   const int64_t seg = (int64_t)img * rows_per_img * 3 + (int64_t)lv.row_off[l] * 3;  // segment start
   const int id = sorted_ids[seg + r];  // index within the image's anchors (level offset included)
-  const float s = sorted_scores[seg + r];
+  const float s = scores[(int64_t)img * rows_per_img * 3 + id];
   const int local = id - lv.row_off[l] * 3;
   const int pos = local / 3, a = local % 3;
   const int x = pos % lv.w[l], y = pos / lv.w[l];
@@ -579,15 +577,19 @@ __device__ __forceinline__ void roi_bilinear_w(int H, int W, float y, float x, i
   i11 = yh * W + xh;
 }
 
-// block per roi (256 threads = channels); rows past an image's proposal count are zero
+// block per roi: thread = (channel quad, bin slot of 4); bilinear weights per sample shared by the 4
+// channels of a float4 load; the roi's (256, 7, 7) output is staged in LDS and stored contiguously.
+// Rows past an image's proposal count are zero.
 __global__ __launch_bounds__(256) void roi_align_kernel(const DetFeats fs, const float* __restrict__ rois,
                                                         const int32_t* __restrict__ n_rois, int max_rois,
                                                         bf16_t* __restrict__ out) {
-  const int r = blockIdx.x, c = threadIdx.x;
+  __shared__ __attribute__((aligned(16))) bf16_t o_lds[256 * 49];
+  const int r = blockIdx.x, tid = threadIdx.x;
   const int img = r / max_rois;
-  bf16_t* o = out + (size_t)r * 256 * 49;
+  uint4* o = reinterpret_cast<uint4*>(out + (size_t)r * 256 * 49);
+  constexpr int NCH = 256 * 49 * 2 / 16;  // 16-B chunks per roi
   if (r % max_rois >= n_rois[img]) {
-    for (int b = 0; b < 49; ++b) o[c * 49 + b] = 0;
+    for (int i = tid; i < NCH; i += 256) o[i] = make_uint4(0, 0, 0, 0);
     return;
   }
   const float* rb = rois + (size_t)r * 4;
@@ -597,33 +599,45 @@ __global__ __launch_bounds__(256) void roi_align_kernel(const DetFeats fs, const
   lvl = min(max(lvl, 0), 3);
   const int H = fs.h[lvl], W = fs.w[lvl];
   const float ss = 1.0f / (float)fs.stride[lvl];
-  const float* f = fs.p[lvl] + (size_t)img * H * W * 256 + c;
+  const int cq = tid & 63, slot = tid >> 6;
+  const float* f = fs.p[lvl] + (size_t)img * H * W * 256 + cq * 4;
   const float sx = x1 * ss - 0.5f, sy = y1 * ss - 0.5f;
   const float ex = x2 * ss - 0.5f, ey = y2 * ss - 0.5f;
   const float rw = ex - sx, rh = ey - sy;
   const float bw = rw / 7.0f, bh = rh / 7.0f;
   const int gh = (int)ceilf(rh / 7.0f), gw = (int)ceilf(rw / 7.0f);
   const float cnt = (float)max(gh * gw, 1);
-  for (int ph = 0; ph < 7; ++ph) {
-    for (int pw = 0; pw < 7; ++pw) {
-      float acc = 0.f;
-      for (int iy = 0; iy < gh; ++iy) {
-        const float y = sy + (float)ph * bh + ((float)iy + 0.5f) * bh / (float)gh;
-        for (int ix = 0; ix < gw; ++ix) {
-          const float x = sx + (float)pw * bw + ((float)ix + 0.5f) * bw / (float)gw;
-          int i00, i01, i10, i11;
-          float w1, w2, w3, w4;
-          bool ok;
-          roi_bilinear_w(H, W, y, x, i00, i01, i10, i11, w1, w2, w3, w4, ok);
-          if (!ok) continue;
-          const float val = ((w1 * f[(size_t)i00 * 256] + w2 * f[(size_t)i01 * 256]) + w3 * f[(size_t)i10 * 256]) +
-                            w4 * f[(size_t)i11 * 256];
-          acc += val;
-        }
+  for (int bin = slot; bin < 49; bin += 4) {
+    const int ph = bin / 7, pw = bin % 7;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int iy = 0; iy < gh; ++iy) {
+      const float y = sy + (float)ph * bh + ((float)iy + 0.5f) * bh / (float)gh;
+      for (int ix = 0; ix < gw; ++ix) {
+        const float x = sx + (float)pw * bw + ((float)ix + 0.5f) * bw / (float)gw;
+        int i00, i01, i10, i11;
+        float w1, w2, w3, w4;
+        bool ok;
+        roi_bilinear_w(H, W, y, x, i00, i01, i10, i11, w1, w2, w3, w4, ok);
+        if (!ok) continue;
+        const float4 v1 = *reinterpret_cast<const float4*>(f + (size_t)i00 * 256);
+        const float4 v2 = *reinterpret_cast<const float4*>(f + (size_t)i01 * 256);
+        const float4 v3 = *reinterpret_cast<const float4*>(f + (size_t)i10 * 256);
+        const float4 v4 = *reinterpret_cast<const float4*>(f + (size_t)i11 * 256);
+        acc.x += ((w1 * v1.x + w2 * v2.x) + w3 * v3.x) + w4 * v4.x;
+        acc.y += ((w1 * v1.y + w2 * v2.y) + w3 * v3.y) + w4 * v4.y;
+        acc.z += ((w1 * v1.z + w2 * v2.z) + w3 * v3.z) + w4 * v4.z;
+        acc.w += ((w1 * v1.w + w2 * v2.w) + w3 * v3.w) + w4 * v4.w;
       }
-      o[c * 49 + ph * 7 + pw] = f32_to_bf16(acc / cnt);
     }
+    const int c = cq * 4;
+    o_lds[(c + 0) * 49 + bin] = f32_to_bf16(acc.x / cnt);
+    o_lds[(c + 1) * 49 + bin] = f32_to_bf16(acc.y / cnt);
+    o_lds[(c + 2) * 49 + bin] = f32_to_bf16(acc.z / cnt);
+    o_lds[(c + 3) * 49 + bin] = f32_to_bf16(acc.w / cnt);
   }
+  __syncthreads();
+  const uint4* src = reinterpret_cast<const uint4*>(o_lds);
+  for (int i = tid; i < NCH; i += 256) o[i] = src[i];
 }
 
 // ------------------------------------------------------------------ RCNN post-process
@@ -729,19 +743,19 @@ int nms_batched(const float* boxes, const float* scores, const uint8_t* valid, c
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-static size_t sort_temp_bytes(size_t n, int segments) {
+static size_t sort_temp_bytes(size_t n) {
   size_t bytes = 0;
-  (void)rocprim::segmented_radix_sort_pairs_desc(nullptr, bytes, (const float*)nullptr, (float*)nullptr,
-                                                 (const int32_t*)nullptr, (int32_t*)nullptr, (unsigned)n,
-                                                 (unsigned)segments, (const int32_t*)nullptr, (const int32_t*)nullptr);
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                  (const int32_t*)nullptr, (int32_t*)nullptr, n, 0u, 44u);
   return bytes;
 }
 
 size_t rpn_workspace_bytes(int n_img, int rows_per_img, int cand_total, int n_levels) {
   const size_t n = (size_t)n_img * rows_per_img * 3;
-  const size_t sort_tmp = sort_temp_bytes(n, n_img * n_levels);
+  const size_t sort_tmp = sort_temp_bytes(n);
+  (void)n_levels;
   const size_t nc = (size_t)n_img * cand_total;
-  return n * 16 + ((sort_tmp + 255) & ~(size_t)255) + (size_t)n_img * 6 * 2 * 4 + nc * 24 + 16 * 256 +
+  return n * 32 + ((sort_tmp + 255) & ~(size_t)255) + (size_t)n_img * 6 * 2 * 4 + nc * 24 + 18 * 256 +
          nms_workspace_bytes(n_img, cand_total) + 4096;
 }
 
@@ -758,25 +772,22 @@ int rpn_proposals(const float* head, const DetLevels& lv, int n_img, int rows_pe
   };
   float* sc = reinterpret_cast<float*>(take(n * 4));
   int32_t* ids = reinterpret_cast<int32_t*>(take(n * 4));
-  float* sc_sorted = reinterpret_cast<float*>(take(n * 4));
   int32_t* ids_sorted = reinterpret_cast<int32_t*>(take(n * 4));
-  int32_t* seg = reinterpret_cast<int32_t*>(take((size_t)n_img * 6 * 2 * 4));
+  unsigned long long* keys = reinterpret_cast<unsigned long long*>(take(n * 8));
+  unsigned long long* keys_sorted = reinterpret_cast<unsigned long long*>(take(n * 8));
   float* cboxes = reinterpret_cast<float*>(take((size_t)n_img * K * 16));
   float* cscores = reinterpret_cast<float*>(take((size_t)n_img * K * 4));
   uint8_t* cvalid = reinterpret_cast<uint8_t*>(take((size_t)n_img * K));
   int8_t* clvl = reinterpret_cast<int8_t*>(take((size_t)n_img * K));
   void* nms_ws = take(nms_workspace_bytes(n_img, K));
-  size_t sort_tmp = sort_temp_bytes(n, n_img * lv.n);
+  size_t sort_tmp = sort_temp_bytes(n);
   void* sort_ws = take(sort_tmp);
   if ((size_t)(p - static_cast<char*>(ws)) > ws_bytes) return -5;
-  hipLaunchKernelGGL(rpn_segments_kernel, blocks_for((int64_t)n_img * lv.n), dim3(256), 0, s, lv, n_img, rows_per_img,
-                     seg);
-  hipLaunchKernelGGL(rpn_scores_kernel, blocks_for((int64_t)n), dim3(256), 0, s, head, lv, rows_per_img, n_img, sc, ids);
-  if (rocprim::segmented_radix_sort_pairs_desc(sort_ws, sort_tmp, sc, sc_sorted, ids, ids_sorted, (unsigned)n,
-                                               (unsigned)(n_img * lv.n), seg, seg + n_img * lv.n, 0u, 32u, s) !=
-      hipSuccess)
+  hipLaunchKernelGGL(rpn_scores_kernel, blocks_for((int64_t)n), dim3(256), 0, s, head, lv, rows_per_img, n_img, sc, ids,
+                     keys);
+  if (rocprim::radix_sort_pairs(sort_ws, sort_tmp, keys, keys_sorted, ids, ids_sorted, n, 0u, 44u, s) != hipSuccess)
     return -1;
-  hipLaunchKernelGGL(rpn_decode_kernel, blocks_for((int64_t)n_img * K), dim3(256), 0, s, head, sc_sorted, ids_sorted,
+  hipLaunchKernelGGL(rpn_decode_kernel, blocks_for((int64_t)n_img * K), dim3(256), 0, s, head, sc, ids_sorted,
                      lv, n_img, rows_per_img, img_h, img_w, cboxes, cscores, cvalid, clvl);
   int rc = nms_batched(cboxes, cscores, cvalid, clvl, n_img, K, iou_thr, max_keep, nms_ws, keep_buf, n_props, s);
   if (rc) return rc;

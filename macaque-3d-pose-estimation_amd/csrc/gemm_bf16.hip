@@ -567,8 +567,11 @@ static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return -1;
   if ((p.lda % 8) || (p.ldw % 8)) return -2;
-  const bool big = epi != EPI_NCHW_F32 && p.N >= 256 && p.M >= 256 && (p.N % 4) == 0 && (p.K % B2K) == 0 &&
-                   (p.ldc % 4) == 0 && !g_gemm_force_small;
+  bool big = epi != EPI_NCHW_F32 && p.N >= 256 && p.M >= 256 && (p.N % 4) == 0 && (p.K % B2K) == 0 &&
+             (p.ldc % 4) == 0 && !g_gemm_force_small;
+  // fewer 256x256 tiles than half the CUs (the detector's late-stage Swin GEMMs): the 128x128 kernel
+  // puts 4x as many workgroups on the chip
+  if (big && (p.K % BK) == 0 && ((p.M + B2M - 1) / B2M) * ((p.N + B2N - 1) / B2N) < 128) big = false;
   if (big) {
     return gemm256(p, epi, stream);
   }

@@ -38,6 +38,53 @@ RCNN_SCORE_THR, RCNN_IOU, RCNN_MAX = 0.05, 0.5, 100
 LN_EPS = 1e-5
 
 
+def make_random_weights(cfg=SWIN_S, seed=0, std=0.02):
+    """Seeded random detector weights under the mmdet state_dict names (no checkpoint is available
+    offline).  Scales keep the logits spread (no tied scores) so NMS / top-k see distinct inputs."""
+    g = torch.Generator().manual_seed(seed)
+
+    def rn(*shape, s=std):
+        return (torch.randn(*shape, generator=g) * s).float()
+
+    w = {}
+    C, ws = cfg["embed"], cfg["window"]
+    w["backbone.patch_embed.projection.weight"] = rn(C, 3, 4, 4, s=0.1)
+    w["backbone.patch_embed.projection.bias"] = rn(C)
+    w["backbone.patch_embed.norm.weight"] = 1 + rn(C, s=0.1)
+    w["backbone.patch_embed.norm.bias"] = rn(C)
+    for si, (depth, heads) in enumerate(zip(cfg["depths"], cfg["heads"])):
+        Cs = C * 2 ** si
+        for bi in range(depth):
+            k = f"backbone.stages.{si}.blocks.{bi}."
+            w[k + "norm1.weight"], w[k + "norm1.bias"] = 1 + rn(Cs, s=0.1), rn(Cs)
+            w[k + "attn.w_msa.relative_position_bias_table"] = rn((2 * ws - 1) ** 2, heads, s=0.5)
+            w[k + "attn.w_msa.qkv.weight"], w[k + "attn.w_msa.qkv.bias"] = rn(3 * Cs, Cs, s=Cs ** -0.5), rn(3 * Cs)
+            w[k + "attn.w_msa.proj.weight"], w[k + "attn.w_msa.proj.bias"] = rn(Cs, Cs, s=0.5 * Cs ** -0.5), rn(Cs)
+            w[k + "norm2.weight"], w[k + "norm2.bias"] = 1 + rn(Cs, s=0.1), rn(Cs)
+            w[k + "ffn.layers.0.0.weight"], w[k + "ffn.layers.0.0.bias"] = rn(4 * Cs, Cs, s=Cs ** -0.5), rn(4 * Cs)
+            w[k + "ffn.layers.1.weight"], w[k + "ffn.layers.1.bias"] = rn(Cs, 4 * Cs, s=0.5 * (4 * Cs) ** -0.5), rn(Cs)
+        if si < 3:
+            k = f"backbone.stages.{si}.downsample."
+            w[k + "norm.weight"], w[k + "norm.bias"] = 1 + rn(4 * Cs, s=0.1), rn(4 * Cs)
+            w[k + "reduction.weight"] = rn(2 * Cs, 4 * Cs, s=(4 * Cs) ** -0.5)
+        w[f"backbone.norm{si}.weight"], w[f"backbone.norm{si}.bias"] = 1 + rn(Cs, s=0.1), rn(Cs)
+    for i in range(4):
+        cin = C * 2 ** i
+        w[f"neck.lateral_convs.{i}.conv.weight"] = rn(256, cin, 1, 1, s=cin ** -0.5)
+        w[f"neck.lateral_convs.{i}.conv.bias"] = rn(256)
+        w[f"neck.fpn_convs.{i}.conv.weight"] = rn(256, 256, 3, 3, s=(9 * 256) ** -0.5)
+        w[f"neck.fpn_convs.{i}.conv.bias"] = rn(256)
+    w["rpn_head.rpn_conv.weight"], w["rpn_head.rpn_conv.bias"] = rn(256, 256, 3, 3, s=(9 * 256) ** -0.5), rn(256)
+    w["rpn_head.rpn_cls.weight"], w["rpn_head.rpn_cls.bias"] = rn(3, 256, 1, 1, s=0.02), rn(3)
+    w["rpn_head.rpn_reg.weight"], w["rpn_head.rpn_reg.bias"] = rn(12, 256, 1, 1, s=0.2 * 256 ** -0.5), rn(12)
+    k = "roi_head.bbox_head."
+    w[k + "shared_fcs.0.weight"], w[k + "shared_fcs.0.bias"] = rn(1024, 256 * 49, s=(256 * 49) ** -0.5), rn(1024)
+    w[k + "shared_fcs.1.weight"], w[k + "shared_fcs.1.bias"] = rn(1024, 1024, s=1024 ** -0.5), rn(1024)
+    w[k + "fc_cls.weight"], w[k + "fc_cls.bias"] = rn(2, 1024, s=0.05), rn(2)
+    w[k + "fc_reg.weight"], w[k + "fc_reg.bias"] = rn(4, 1024, s=0.3 * 1024 ** -0.5), rn(4)
+    return w
+
+
 def rescale_size(w, h, scale=(800, 800)):
     """mmcv rescale_size (keep_ratio): (new_w, new_h)."""
     long_e, short_e = max(scale), min(scale)

@@ -12,12 +12,15 @@ MI355X-first: ``process_frame_multiview`` sends every box of every view of a
 frame through ONE batched launch sequence instead of one ``inference_topdown``
 per camera.
 
-Out of scope: the Swin Mask R-CNN detector, BoT-SORT tracker and
-ResNet ID classifier, and imgstore video decoding.  Their outputs enter here as
-data: per-frame tracker rows ``(N, >=5)`` [x1, y1, x2, y2, track_id, ...] and,
-optionally, ID predictions -- carried by the per-camera ``mqhip.io.FrameStore``
-that ``proc`` reads; without ID predictions every box gets ``assigned_id = -1``
-(the reference's "not confident" value).
+The Swin-S Mask R-CNN detector runs on MI355X too (``init_detector`` / ``inference_detector``,
+step1:98, :226-237 -> ``mqhip.detector``); ``detect_stores`` gives, per camera and processed frame,
+the detections above SCORE_THR that the reference hands to its tracker (step1:229-240).
+
+Out of scope: the BoT-SORT tracker and ResNet ID classifier, and imgstore
+video decoding.  Their outputs enter here as data: per-frame tracker rows ``(N, >=5)``
+[x1, y1, x2, y2, track_id, ...] and, optionally, ID predictions -- carried by the per-camera
+``mqhip.io.FrameStore`` that ``proc`` reads; without ID predictions every box gets
+``assigned_id = -1`` (the reference's "not confident" value).
 """
 from __future__ import annotations
 
@@ -30,6 +33,8 @@ import numpy as np
 
 from mqhip.apis import inference_topdown, inference_topdown_batch, init_model
 
+DETECT_CONFIG = "./model/detection/SWIN-Mask_R-CNN_bbox_only.py"
+DETECT_CHECKPOINT = "./model/detection/detection.pth"
 POSE_CONFIG = "./model/pose/ViTPose_huge_macaque_256x192.py"
 POSE_CHECKPOINT = "./model/pose/pose.pth"
 
@@ -45,6 +50,48 @@ ID_CONF_THR = 0.80
 KP_PARAMS = {"score_thr": SCORE_THR, "kp_thr": KP_THR, "ema_alpha": EMA_ALPHA, "disp_thr": DISP_THR,
              "min_margin": MIN_MARGIN, "max_margin": MAX_MARGIN, "desired_ar": DESIRED_AR,
              "id_conf_thr": ID_CONF_THR}
+
+
+def init_detector(config=DETECT_CONFIG, checkpoint=DETECT_CHECKPOINT, device="cuda:0", weights=None):
+    """mmdet init_detector (step1:98) -> the MI355X Swin-S Mask R-CNN.  The checkpoint is read with
+    torch.load(weights_only=True) when it exists (mmdet keys under 'state_dict'); otherwise seeded
+    random weights (no checkpoint ships with the reference)."""
+    from mqhip.detector import SwinDetectorHip, make_random_weights
+    dev = int(device.split(":")[1]) if ":" in device else 0
+    if weights is None:
+        if checkpoint and os.path.exists(checkpoint):
+            import torch
+            ck = torch.load(checkpoint, map_location="cpu", weights_only=True)
+            weights = {k: v.float() for k, v in ck.get("state_dict", ck).items()}
+        else:
+            weights = make_random_weights(seed=0)
+    return SwinDetectorHip(weights, device=dev)
+
+
+def inference_detector(detector, imgs, test_pipeline=None):
+    """mmdet inference_detector(detector, [img], test_pipeline) (step1:226): per image
+    (bboxes (k, 4) float32, scores (k,)) in original pixels, score-ordered; the test pipeline is the
+    detector's own (Resize 800x800 keep-ratio + DetDataPreprocessor, step1:104-109)."""
+    from mqhip.detector import inference_detector as _inf
+    return _inf(detector, imgs)
+
+
+def detect_stores(detector, stores, T, score_thr=SCORE_THR):
+    """Detections per camera over step 1's frame plan (the boxes the reference's tracker receives,
+    step1:210-240): {cam: [(frame_number, boxes (k, 4), scores (k,))]} for every frame a camera
+    processes (repeats of the time-sync walk are skipped, as there); the cameras that process a frame
+    at the same time step go through one detector batch."""
+    plans = [_frame_plan(st, T) for st in stores]
+    out = {i: [] for i in range(len(stores))}
+    for k in range(len(T)):
+        cams = [i for i, p in enumerate(plans) if not p[k][1]]
+        if not cams:
+            continue
+        imgs = [stores[i].image(plans[i][k][0]) for i in cams]
+        for i, (b, sc) in zip(cams, inference_detector(detector, imgs)):
+            keep = sc > score_thr
+            out[i].append((plans[i][k][0], b[keep], sc[keep]))
+    return out
 
 
 def init_pose_model(config=POSE_CONFIG, checkpoint=POSE_CHECKPOINT, device="cuda:0"):

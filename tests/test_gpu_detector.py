@@ -269,3 +269,24 @@ def test_detector_full_size_runs():
         assert b.shape[1] == 4 and b.shape[0] == s.shape[0] <= 100
         assert np.all(np.isfinite(b)) and np.all((b[:, 0] >= 0) & (b[:, 2] <= 2048 + 1e-3))
         assert np.all(np.diff(s) <= 0) and np.all(s > 0.05)
+
+
+def test_detect_stores_follows_the_frame_plan(tmp_path, det_small):
+    """step1 detect_stores: one detection list per processed (non-repeat) frame of each camera."""
+    from mqhip import io as mqio
+    from src.pipeline.step1_proc2d import _frame_plan, detect_stores
+    rng = np.random.default_rng(11)
+    for c in range(2):
+        fr = _frames(4, 240, 320, 20 + c)
+        times = 10.0 + np.cumsum(rng.uniform(0.03, 0.06, 4))
+        mqio.write_frame_store(str(tmp_path / f"demo.{100 + c}"), fr, times, np.arange(4) * 3 + 1, [[] for _ in range(4)],
+                               100 + c)
+    stores = [mqio.FrameStore(str(tmp_path / f"demo.{100 + c}")) for c in range(2)]
+    T = np.arange(10.0, 10.25, 1 / 24)
+    res = detect_stores(det_small, stores, T, score_thr=0.5)
+    for c in range(2):
+        plan = [f for f, rep in _frame_plan(stores[c], T) if not rep]
+        assert [r[0] for r in res[c]] == plan
+        for _, b, s in res[c]:
+            assert b.shape == (len(s), 4) and np.all(s > 0.5)
+            assert np.all((b[:, 0] >= 0) & (b[:, 2] <= 320 + 1e-3) & (b[:, 1] >= 0) & (b[:, 3] <= 240 + 1e-3))
