@@ -46,6 +46,8 @@ const char* mq_last_error(void);
                                        results stay within the optim_points tolerance) */
 #define MQ_TUNE_GEMM_PINGPONG 12    /* 1 (default): 256x256 GEMMs with K % 64 == 0 on the ping-pong kernel (wave groups
                                        alternate LDS traffic and MFMA, gemm_pp.hip); 0: the interleaved-K-step kernel */
+#define MQ_TUNE_OPTIM_PRECOND_LDS 18 /* 1 (default): optim_points' preconditioner on the series staged in LDS when it
+                                        fits; 0: the global-memory substitution kernel (same preconditioner) */
 #define MQ_TUNE_ATTENTION_V2 17     /* 1 (default): attention on 16x16x32 QK^T + transposed-output PV (vit_ops.hip
                                        attention2_kernel); 0: the first-generation kernel */
 int mq_set_tuning(int key, int value);

@@ -31,6 +31,7 @@ namespace {
 constexpr int OPT_MAXJ = 32;
 constexpr int OPT_MAXL = 64;
 constexpr int OPT_MAXN = 3;
+constexpr int OPT_FS = 9 + 18 * OPT_MAXN;  // doubles per frame record of the factored preconditioner
 constexpr int OPT_MAXC = 16;
 constexpr int OPT_MAXIT = 128;  // PCG iterations per LM step (upper bound)
 constexpr int OPT_THREADS = 128;
@@ -301,9 +302,14 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_reduce_kernel(OptDims D, Op
 __device__ __forceinline__ double damp_of(double dg) { return fmax(dg, 1e-12); }
 
 // Block-banded Cholesky of the per-joint preconditioner (thread per (animal, joint)).
-// fac[((b*J + j)*F + f)*36]: [0..8] inverse of L_ff (lower), [9d .. 9d+8] L_{f,f-d} (d = 1..n).
-// The recurrence is latency-bound: the last NN frames' blocks stay in registers and frame
-// f+1's inputs are loaded while frame f is factored.
+// fac[((b*J + j)*F + f)*OPT_FS] holds the factor pre-multiplied for the two substitutions:
+//   [0 .. 8]                      I_f = inv(L_ff) (lower)
+//   [9 + 9(d-1) ..]   d = 1..n    M_{f,d} = I_f L_{f,f-d}          (zero for f - d < 0)
+//   [9 + 9n + 9(d-1)..] d = 1..n  N_{f,d} = I_f^T L_{f+d,f}^T      (zero for f + d >= F)
+// so that L y = r is y_f = I_f r_f - sum_d M_{f,d} y_{f-d} and L^T z = y is
+// z_f = I_f^T y_f - sum_d N_{f,d} z_{f+d}: the I_f r_f / I_f^T y_f products leave the sequential
+// recurrence and run frame-parallel.  The factor recurrence is latency-bound: the last NN frames'
+// blocks stay in registers and frame f+1's inputs are loaded while frame f is factored.
 struct FacRec {
   double inv[9];
   double L[OPT_MAXN][9];  // L[d-1] = L_{f,f-d}
@@ -314,7 +320,7 @@ __device__ void factor_series(const OptDims& D, const OptBufs& Bf, int b, int j,
   const int F = D.F, J = D.J;
   const double ssf = Bf.ssf[b];
   const double s2 = F > NN ? ssf * ssf : 0.0;
-  double* fb = Bf.fac + ((size_t)b * J + j) * F * 36;
+  double* fb = Bf.fac + ((size_t)b * J + j) * F * OPT_FS;
   int ck[16], nck = 0;
   bool many = false;
   for (int k = 0; k < D.NL; ++k)
@@ -415,13 +421,32 @@ __device__ void factor_series(const OptDims& D, const OptBufs& Bf, int b, int j,
     cur.inv[0] = i00; cur.inv[1] = 0; cur.inv[2] = 0;
     cur.inv[3] = i10; cur.inv[4] = i11; cur.inv[5] = 0;
     cur.inv[6] = i20; cur.inv[7] = i21; cur.inv[8] = i22;
-    double* o = fb + (size_t)f * 36;
+    double* o = fb + (size_t)f * OPT_FS;
 #pragma unroll
     for (int e = 0; e < 9; ++e) o[e] = cur.inv[e];
 #pragma unroll
-    for (int d = 1; d <= NN; ++d)
+    for (int d = 1; d <= NN; ++d) {
+      const double* Lf = cur.L[d - 1];
+      const double* I = cur.inv;
 #pragma unroll
-      for (int e = 0; e < 9; ++e) o[9 * d + e] = cur.L[d - 1][e];
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)  // M_{f,d} = I_f L_{f,f-d}
+          o[9 * d + 3 * r + c] = I[3 * r] * Lf[c] + I[3 * r + 1] * Lf[3 + c] + I[3 * r + 2] * Lf[6 + c];
+      if (f - d >= 0) {  // N_{f-d,d} = (L_{f,f-d} I_{f-d})^T, into frame f-d's record
+        const double* Ii = W[d - 1].inv;
+        double* on = fb + (size_t)(f - d) * OPT_FS + 9 + 9 * NN + 9 * (d - 1);
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            on[3 * r + c] = Lf[3 * c] * Ii[r] + Lf[3 * c + 1] * Ii[3 + r] + Lf[3 * c + 2] * Ii[6 + r];
+      }
+      if (f + d >= F) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) o[9 + 9 * NN + 9 * (d - 1) + e] = 0.0;
+      }
+    }
 #pragma unroll
     for (int k = NN - 1; k >= 1; --k) W[k] = W[k - 1];
     W[0] = cur;
@@ -465,23 +490,24 @@ __device__ __forceinline__ bool pcg_done(const OptDims& D, const OptBufs& Bf, in
 // else first d += alpha p_it, r -= alpha q_it.  Writes the series' r.z partial to rzJ[it + 1].
 // Both substitutions keep the last NN solution vectors in registers and load frame f+-1's
 // inputs while frame f is solved (the recurrence is latency-bound, one thread per series).
+// Global-memory form of optim_precond_lds_kernel, for clips too long for LDS.
 template <int NN>
 __device__ double solve_series(const OptDims& D, const OptBufs& Bf, int b, int j, int it, double alpha,
                                const double* __restrict__ P) {
   const int F = D.F, J = D.J, J3 = 3 * J;
   const size_t base = (size_t)b * D.NV + 3 * j;
-  const double* __restrict__ fb = Bf.fac + ((size_t)b * J + j) * F * 36;
+  const double* __restrict__ fb = Bf.fac + ((size_t)b * J + j) * F * OPT_FS;
   double* __restrict__ z = Bf.z;
   double* __restrict__ r = Bf.r;
   double* __restrict__ dd = Bf.d;
   const double* __restrict__ g = Bf.g;
   const double* __restrict__ q = Bf.q;
   struct In {
-    double rec[9 + 9 * NN];
+    double rec[9 + 9 * NN];  // I_f, M_{f,1..n}
     double r[3], d[3], p[3], q[3];
   };
   auto load_in = [&](int f, In& x) {
-    const double* rc = fb + (size_t)f * 36;
+    const double* rc = fb + (size_t)f * OPT_FS;
 #pragma unroll
     for (int e = 0; e < 9 + 9 * NN; ++e) x.rec[e] = rc[e];
     const size_t o = base + (size_t)f * J3;
@@ -502,7 +528,7 @@ __device__ double solve_series(const OptDims& D, const OptBufs& Bf, int b, int j
   for (int k = 0; k < NN; ++k) Y[k][0] = Y[k][1] = Y[k][2] = 0.0;
   In nx;
   load_in(0, nx);
-  for (int f = 0; f < F; ++f) {  // forward: L y = r
+  for (int f = 0; f < F; ++f) {  // forward: y_f = I_f r_f - sum_d M_{f,d} y_{f-d}
     const In cu = nx;
     if (f + 1 < F) load_in(f + 1, nx);
     const size_t o = base + (size_t)f * J3;
@@ -518,52 +544,42 @@ __device__ double solve_series(const OptDims& D, const OptBufs& Bf, int b, int j
       }
       r[o + i] = rr[i];
     }
-    double w[3] = {rr[0], rr[1], rr[2]};
+    const double* I = cu.rec;
+    double w[3] = {I[0] * rr[0], I[3] * rr[0] + I[4] * rr[1], I[6] * rr[0] + I[7] * rr[1] + I[8] * rr[2]};
 #pragma unroll
-    for (int d = 1; d <= NN; ++d) {
-      const double* Lf = cu.rec + 9 * d;
+    for (int d = NN; d >= 1; --d) {
+      const double* M = cu.rec + 9 * d;
 #pragma unroll
       for (int i = 0; i < 3; ++i)
-        w[i] -= Lf[3 * i] * Y[d - 1][0] + Lf[3 * i + 1] * Y[d - 1][1] + Lf[3 * i + 2] * Y[d - 1][2];
+        w[i] -= M[3 * i] * Y[d - 1][0] + M[3 * i + 1] * Y[d - 1][1] + M[3 * i + 2] * Y[d - 1][2];
     }
-    const double* I = cu.rec;
-    const double y0 = I[0] * w[0];
-    const double y1 = I[3] * w[0] + I[4] * w[1];
-    const double y2 = I[6] * w[0] + I[7] * w[1] + I[8] * w[2];
-    z[o] = y0;
-    z[o + 1] = y1;
-    z[o + 2] = y2;
+    z[o] = w[0];
+    z[o + 1] = w[1];
+    z[o + 2] = w[2];
 #pragma unroll
     for (int k = NN - 1; k >= 1; --k) {
       Y[k][0] = Y[k - 1][0];
       Y[k][1] = Y[k - 1][1];
       Y[k][2] = Y[k - 1][2];
     }
-    Y[0][0] = y0;
-    Y[0][1] = y1;
-    Y[0][2] = y2;
+    Y[0][0] = w[0];
+    Y[0][1] = w[1];
+    Y[0][2] = w[2];
   }
-  // backward: L^T z = y.  Frame f needs inv(L_ff), L_{f+d,f} (block d of frame f+d), y_f, r_f.
+  // backward: z_f = I_f^T y_f - sum_d N_{f,d} z_{f+d}.  Frame f needs its own record, y_f, r_f.
   struct Bk {
     double inv[9];
-    double Ld[NN][9];
+    double N[NN][9];
     double y[3], r[3];
   };
   auto load_bk = [&](int f, Bk& x) {
-    const double* rc = fb + (size_t)f * 36;
+    const double* rc = fb + (size_t)f * OPT_FS;
 #pragma unroll
     for (int e = 0; e < 9; ++e) x.inv[e] = rc[e];
 #pragma unroll
-    for (int d = 1; d <= NN; ++d) {
-      if (f + d < F) {
-        const double* rd = fb + (size_t)(f + d) * 36 + 9 * d;
+    for (int d = 0; d < NN; ++d)
 #pragma unroll
-        for (int e = 0; e < 9; ++e) x.Ld[d - 1][e] = rd[e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 9; ++e) x.Ld[d - 1][e] = 0.0;
-      }
-    }
+      for (int e = 0; e < 9; ++e) x.N[d][e] = rc[9 + 9 * NN + 9 * d + e];
     const size_t o = base + (size_t)f * J3;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -580,31 +596,29 @@ __device__ double solve_series(const OptDims& D, const OptBufs& Bf, int b, int j
   for (int f = F - 1; f >= 0; --f) {
     const Bk bc = bn;
     if (f > 0) load_bk(f - 1, bn);
-    double w[3] = {bc.y[0], bc.y[1], bc.y[2]};
-#pragma unroll
-    for (int d = 1; d <= NN; ++d) {
-      const double* Ld = bc.Ld[d - 1];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) w[i] -= Ld[i] * Z[d - 1][0] + Ld[3 + i] * Z[d - 1][1] + Ld[6 + i] * Z[d - 1][2];
-    }
     const double* I = bc.inv;
-    const double z0 = I[0] * w[0] + I[3] * w[1] + I[6] * w[2];
-    const double z1 = I[4] * w[1] + I[7] * w[2];
-    const double z2 = I[8] * w[2];
+    double w[3] = {I[0] * bc.y[0] + I[3] * bc.y[1] + I[6] * bc.y[2], I[4] * bc.y[1] + I[7] * bc.y[2], I[8] * bc.y[2]};
+#pragma unroll
+    for (int d = NN; d >= 1; --d) {
+      const double* N = bc.N[d - 1];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        w[i] -= N[3 * i] * Z[d - 1][0] + N[3 * i + 1] * Z[d - 1][1] + N[3 * i + 2] * Z[d - 1][2];
+    }
     const size_t o = base + (size_t)f * J3;
-    z[o] = z0;
-    z[o + 1] = z1;
-    z[o + 2] = z2;
-    rz += bc.r[0] * z0 + bc.r[1] * z1 + bc.r[2] * z2;
+    z[o] = w[0];
+    z[o + 1] = w[1];
+    z[o + 2] = w[2];
+    rz += bc.r[0] * w[0] + bc.r[1] * w[1] + bc.r[2] * w[2];
 #pragma unroll
     for (int k = NN - 1; k >= 1; --k) {
       Z[k][0] = Z[k - 1][0];
       Z[k][1] = Z[k - 1][1];
       Z[k][2] = Z[k - 1][2];
     }
-    Z[0][0] = z0;
-    Z[0][1] = z1;
-    Z[0][2] = z2;
+    Z[0][0] = w[0];
+    Z[0][1] = w[1];
+    Z[0][2] = w[2];
   }
   return rz;
 }
@@ -650,13 +664,83 @@ __global__ void __launch_bounds__(64) optim_precond_kernel(OptDims D, OptBufs Bf
   Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
 }
 
+// Broadcast lane K of each lane quad to the quad (DPP quad_perm, no LDS round trip).
+template <int K>
+__device__ __forceinline__ double quad_bcast(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)u, K * 0x55, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), K * 0x55, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// One sequential substitution over the series, run by lanes 0..3: lane q = 0, 1, 2 owns row q of
+// the 3-vector (lane 3 repeats row 2), so a step is 3n fused products per lane and the new
+// vector reaches every lane by three DPP broadcasts.  Forward (BACK false):
+// out_f = in_f - sum_d A[f][d] out_{f-d}; backward: out_f = in_f - sum_d A[f][n + d] out_{f+d},
+// with A[f] the 18n M / N doubles of frame f.  The nearest frame's term is summed last.
+template <int NN, bool BACK>
+__device__ __forceinline__ void lane_substitution(const double* __restrict__ smn, const double* __restrict__ in,
+                                                  double* __restrict__ out, int F, int t) {
+#pragma clang fp contract(fast)
+  const int q = t & 3, i = q < 3 ? q : 2;
+  double V[NN][3];
+#pragma unroll
+  for (int k = 0; k < NN; ++k) V[k][0] = V[k][1] = V[k][2] = 0.0;
+  // step s's 3n + 1 operands are read from LDS one step ahead (two register sets, no copies)
+  struct Ops {
+    double a[NN][3];
+    double in;
+  };
+  auto load = [&](int s, Ops& o) {
+    const int f = BACK ? F - 1 - s : s;
+    const double* A = smn + (size_t)f * (18 * NN) + (BACK ? 9 * NN : 0) + 3 * i;
+#pragma unroll
+    for (int d = 0; d < NN; ++d) {
+      o.a[d][0] = A[9 * d];
+      o.a[d][1] = A[9 * d + 1];
+      o.a[d][2] = A[9 * d + 2];
+    }
+    o.in = in[3 * f + i];
+    __builtin_amdgcn_sched_barrier(0);  // keep the look-ahead loads ahead of the step they overlap
+  };
+  auto step = [&](int s, const Ops& o) {
+    const int f = BACK ? F - 1 - s : s;
+    double w = o.in;
+#pragma unroll
+    for (int d = NN; d >= 1; --d) w = w - o.a[d - 1][0] * V[d - 1][0] - o.a[d - 1][1] * V[d - 1][1] - o.a[d - 1][2] * V[d - 1][2];
+    out[3 * f + i] = w;  // lanes 2 and 3 store the same value
+#pragma unroll
+    for (int k = NN - 1; k >= 1; --k) {
+      V[k][0] = V[k - 1][0];
+      V[k][1] = V[k - 1][1];
+      V[k][2] = V[k - 1][2];
+    }
+    V[0][0] = quad_bcast<0>(w);
+    V[0][1] = quad_bcast<1>(w);
+    V[0][2] = quad_bcast<2>(w);
+  };
+  // the look-ahead loads are unconditional (clamped to the last step) so that the LDS counter
+  // wait before a step covers only that step's operands
+  Ops ra, rb;
+  load(0, ra);
+  for (int s = 0; s < F; s += 2) {
+    load(min(s + 1, F - 1), rb);
+    step(s, ra);
+    if (s + 1 >= F) break;
+    load(min(s + 2, F - 1), ra);
+    step(s + 1, rb);
+  }
+}
+
 // The same preconditioner step with the series staged in LDS: one 256-thread block per (joint
-// series, animal).  The solve is a sequential recurrence over frames; run from global memory its
-// every step waits on a load that the previous kernel left in another XCD's L2 or in HBM.  Here
-// the block first copies the series' factor blocks and r / d / p / q (or g) into LDS with all its
-// threads, applies the element-wise updates r -= alpha q, d += alpha p in parallel, and one thread
-// then runs both substitutions on LDS.  Arithmetic per value is the one of solve_series (bitwise
-// equal results).  LDS: F * (24 + 9 NN) doubles (optim_precond_lds_bytes).
+// series, animal).  Only the two recurrences are sequential; everything else is frame-parallel.
+//   1. all threads: r_f = r_f - alpha q_f, d_f += alpha p_f, u_f = I_f r_f; stage M / N blocks;
+//   2. lanes 0..3:  y_f = u_f - sum_d M_{f,d} y_{f-d}            (forward, f = 0 .. F-1)
+//   3. all threads: v_f = I_f^T y_f
+//   4. lanes 0..3:  z_f = v_f - sum_d N_{f,d} z_{f+d}            (backward, f = F-1 .. 0)
+//   5. all threads: write r, z; block-reduce r.z.
+// Each sequential step is 3n fused products per lane on LDS operands (lane_substitution).  Run from global memory the same
+// recurrence waits on loads left in another XCD's L2.  LDS: optim_precond_lds_bytes.
 template <int NN>
 __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBufs Bf, int it) {
   const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
@@ -692,106 +776,71 @@ __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBu
     Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
     return;
   }
-  constexpr int FR = 9 + 9 * NN;  // factor doubles used per frame
+  constexpr int MN = 18 * NN;  // M and N doubles per frame
   extern __shared__ double lds_opt[];
-  double* sfac = lds_opt;
-  double* sr = sfac + (size_t)F * FR;
-  double* sz = sr + (size_t)F * 3;
-  const double* __restrict__ fb = Bf.fac + ((size_t)b * J + j) * F * 36;
-  for (int idx = t; idx < F * FR; idx += 256) {
-    const int f = idx / FR, e = idx - f * FR;
-    sfac[idx] = fb[(size_t)f * 36 + e];
+  double* smn = lds_opt;                // [F][MN]
+  double* sr = smn + (size_t)F * MN;    // [F][3] r
+  double* su = sr + (size_t)F * 3;      // [F][3] u, then v
+  double* sz = su + (size_t)F * 3;      // [F][3] y, then z
+  const double* __restrict__ fb = Bf.fac + ((size_t)b * J + j) * F * OPT_FS;
+  for (int idx = t; idx < F * MN; idx += 256) {
+    const int f = idx / MN, e = idx - f * MN;
+    smn[idx] = fb[(size_t)f * OPT_FS + 9 + e];
   }
-  for (int idx = t; idx < F * 3; idx += 256) {
-    const int f = idx / 3, i = idx - f * 3;
-    const size_t o = base + (size_t)f * J3 + 3 * j + i;
-    if (it < 0) {
-      Bf.d[o] = 0.0;
-      sr[idx] = -Bf.g[o];
-    } else {
-      Bf.d[o] = Bf.d[o] + alpha * P[o];
-      sr[idx] = Bf.r[o] - alpha * Bf.q[o];
+  for (int f = t; f < F; f += 256) {
+    const size_t o = base + (size_t)f * J3 + 3 * j;
+    double rr[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (it < 0) {
+        Bf.d[o + i] = 0.0;
+        rr[i] = -Bf.g[o + i];
+      } else {
+        Bf.d[o + i] = Bf.d[o + i] + alpha * P[o + i];
+        rr[i] = Bf.r[o + i] - alpha * Bf.q[o + i];
+      }
+      sr[3 * f + i] = rr[i];
     }
-  }
-  __syncthreads();
-  if (t == 0) {
-    double Y[NN][3];
-#pragma unroll
-    for (int k = 0; k < NN; ++k) Y[k][0] = Y[k][1] = Y[k][2] = 0.0;
-    for (int f = 0; f < F; ++f) {  // forward: L y = r
-      const double* rec = sfac + (size_t)f * FR;
-      double w[3] = {sr[3 * f], sr[3 * f + 1], sr[3 * f + 2]};
-#pragma unroll
-      for (int d = 1; d <= NN; ++d) {
-        const double* Lf = rec + 9 * d;
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-          w[i] -= Lf[3 * i] * Y[d - 1][0] + Lf[3 * i + 1] * Y[d - 1][1] + Lf[3 * i + 2] * Y[d - 1][2];
-      }
-      const double* I = rec;
-      const double y0 = I[0] * w[0];
-      const double y1 = I[3] * w[0] + I[4] * w[1];
-      const double y2 = I[6] * w[0] + I[7] * w[1] + I[8] * w[2];
-      sz[3 * f] = y0;
-      sz[3 * f + 1] = y1;
-      sz[3 * f + 2] = y2;
-#pragma unroll
-      for (int k = NN - 1; k >= 1; --k) {
-        Y[k][0] = Y[k - 1][0];
-        Y[k][1] = Y[k - 1][1];
-        Y[k][2] = Y[k - 1][2];
-      }
-      Y[0][0] = y0;
-      Y[0][1] = y1;
-      Y[0][2] = y2;
-    }
-    double Z[NN][3];
-#pragma unroll
-    for (int k = 0; k < NN; ++k) Z[k][0] = Z[k][1] = Z[k][2] = 0.0;
-    double rz = 0;
-    for (int f = F - 1; f >= 0; --f) {  // backward: L^T z = y
-      double w[3] = {sz[3 * f], sz[3 * f + 1], sz[3 * f + 2]};
-#pragma unroll
-      for (int d = 1; d <= NN; ++d) {
-        if (f + d < F) {
-          const double* Ld = sfac + (size_t)(f + d) * FR + 9 * d;
-#pragma unroll
-          for (int i = 0; i < 3; ++i) w[i] -= Ld[i] * Z[d - 1][0] + Ld[3 + i] * Z[d - 1][1] + Ld[6 + i] * Z[d - 1][2];
-        } else {
-#pragma unroll
-          for (int i = 0; i < 3; ++i) w[i] -= 0.0 * Z[d - 1][0] + 0.0 * Z[d - 1][1] + 0.0 * Z[d - 1][2];
-        }
-      }
-      const double* I = sfac + (size_t)f * FR;
-      const double z0 = I[0] * w[0] + I[3] * w[1] + I[6] * w[2];
-      const double z1 = I[4] * w[1] + I[7] * w[2];
-      const double z2 = I[8] * w[2];
-      sz[3 * f] = z0;
-      sz[3 * f + 1] = z1;
-      sz[3 * f + 2] = z2;
-      rz += sr[3 * f] * z0 + sr[3 * f + 1] * z1 + sr[3 * f + 2] * z2;
-#pragma unroll
-      for (int k = NN - 1; k >= 1; --k) {
-        Z[k][0] = Z[k - 1][0];
-        Z[k][1] = Z[k - 1][1];
-        Z[k][2] = Z[k - 1][2];
-      }
-      Z[0][0] = z0;
-      Z[0][1] = z1;
-      Z[0][2] = z2;
-    }
-    Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
+    const double* I = fb + (size_t)f * OPT_FS;
+    su[3 * f] = I[0] * rr[0];
+    su[3 * f + 1] = I[3] * rr[0] + I[4] * rr[1];
+    su[3 * f + 2] = I[6] * rr[0] + I[7] * rr[1] + I[8] * rr[2];
   }
   __syncthreads();
+  if (t < 4) lane_substitution<NN, false>(smn, su, sz, F, t);
+  __syncthreads();
+  for (int f = t; f < F; f += 256) {
+    const double* I = fb + (size_t)f * OPT_FS;
+    const double y0 = sz[3 * f], y1 = sz[3 * f + 1], y2 = sz[3 * f + 2];
+    su[3 * f] = I[0] * y0 + I[3] * y1 + I[6] * y2;
+    su[3 * f + 1] = I[4] * y1 + I[7] * y2;
+    su[3 * f + 2] = I[8] * y2;
+  }
+  __syncthreads();
+  if (t < 4) lane_substitution<NN, true>(smn, su, sz, F, t);
+  __syncthreads();
+  double rz = 0;
   for (int idx = t; idx < F * 3; idx += 256) {
     const int f = idx / 3, i = idx - f * 3;
     const size_t o = base + (size_t)f * J3 + 3 * j + i;
     Bf.r[o] = sr[idx];
     Bf.z[o] = sz[idx];
+    rz += sr[idx] * sz[idx];
   }
+  __syncthreads();
+  double* red = lds_opt;  // r / z are in registers or global memory now
+  red[t] = rz;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t == 0) Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = red[0];
 }
 
-size_t optim_precond_lds_bytes(int F, int NN) { return (size_t)F * (24 + 9 * NN) * sizeof(double); }
+size_t optim_precond_lds_bytes(int F, int NN) {
+  return std::max((size_t)F * (18 * NN + 9), (size_t)256) * sizeof(double);
+}
 
 // q = (H + lam diag(H)) p_it with p_it = z + beta p_{it-1} (computed here, written to P[it & 1]).
 __global__ void __launch_bounds__(OPT_THREADS) optim_matvec_kernel(OptDims D, OptBufs Bf, int it) {
@@ -903,6 +952,7 @@ __global__ void optim_accept_kernel(double* x, const double* xt, const double* c
 
 }  // namespace
 
+int g_optim_precond_lds = 1;
 int g_optim_pcg_iters = 20;  // LM inner-solve cap: tools/optim_probe.py (cost within 3e-4 of scipy at 20; 40 costs 1.6x the time)
 
 size_t optim_workspace_bytes(int B, int F, int J, int NL) {
@@ -913,7 +963,7 @@ size_t optim_workspace_bytes(int B, int F, int J, int NL) {
   n += (size_t)B * F * NL * 5;                   // lenJ
   n += (size_t)B * F * 2;                        // costF pqF
   n += (size_t)B * F * NL;                       // qLf
-  n += (size_t)B * J * F * 36 + (size_t)B * OPT_MAXL;  // fac pinvL
+  n += (size_t)B * J * F * OPT_FS + (size_t)B * OPT_MAXL;  // fac pinvL
   n += (size_t)B * (OPT_MAXIT + 1) * (J + 2);    // rzJ, pq
   n += (size_t)B * 4;                            // cost, cost_t, ctl(2)
   n += (size_t)NL + 2 + B;                       // constraint pairs (int32), ssf
@@ -975,7 +1025,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
   Bf.costF = take((size_t)B * F);
   Bf.pqF = take((size_t)B * F);
   Bf.qLf = take((size_t)B * F * NL);
-  Bf.fac = take((size_t)B * J * F * 36);
+  Bf.fac = take((size_t)B * J * F * OPT_FS);
   Bf.pinvL = take((size_t)B * OPT_MAXL);
   Bf.rzJ = take((size_t)B * (OPT_MAXIT + 1) * (J + 1));
   Bf.pq = take((size_t)B * (OPT_MAXIT + 1));
@@ -1001,7 +1051,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
 
   // preconditioner step: series staged in LDS when they fit (every clip up to ~400 frames)
   const size_t lds_b = optim_precond_lds_bytes(F, D.n);
-  const bool use_lds = lds_b <= 160 * 1024;
+  const bool use_lds = g_optim_precond_lds && lds_b <= 160 * 1024;
   auto precond = [&](int it) {
     if (!use_lds) {
       hipLaunchKernelGGL(optim_precond_kernel, dim3(B), dim3(64), 0, s, D, Bf, it);

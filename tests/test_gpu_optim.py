@@ -140,3 +140,36 @@ def test_optim_points_jointlenfix_matches_scipy(F, drop, gap):
         p3g.ravel(), p2, jl, np.array(cons), np.array(weak), sa[3], ARGS["scale_length"],
         ARGS["scale_length_weak"], ARGS["reproj_error_threshold"], "soft_l1", ARGS["n_deriv_smooth"]) ** 2)
     assert cg <= sa[2].cost * (1 + 1e-3), (cg, sa[2].cost, sb[2].cost)
+
+
+@pytest.mark.parametrize("F,n", [(40, 2), (24, 1), (30, 3), (480, 2)])
+def test_optim_precond_routes_agree(F, n):
+    """The preconditioner has two kernels (optim.hip): the series staged in LDS with the two
+    substitutions run by one lane quad (default when F (18 n + 9) doubles fit in 160 KB), and the
+    global-memory kernel (MQ_TUNE_OPTIM_PRECOND_LDS = 0, and every clip longer than ~450 frames).  Both
+    apply the same factor; rounding differs (fused products), so the solves agree to well inside the
+    optim_points tolerance and the objectives to 1e-6 relative.  F = 480 runs the global kernel
+    under both settings (bit-identical)."""
+    from mqhip import _lib
+    from mqhip.geometry import CameraGroup
+    from mqhip.optim import optim_points_batch
+    cams, o, p2, init, cons, weak, truth = _problem(F)
+    g = CameraGroup.from_dicts(cams)
+    args = dict(ARGS, n_deriv_smooth=n)
+    ctx = _lib.Context.get(0)
+    old = ctx.lib.mq_get_tuning(18)
+    try:
+        out = {}
+        for route in (1, 0):
+            assert ctx.lib.mq_set_tuning(18, route) == 0
+            out[route] = optim_points_batch(g, p2[None], init[None], cons, weak, return_stats=True, **args)
+    finally:
+        ctx.lib.mq_set_tuning(18, old)
+    (a, la, sa, _), (b, lb, sb, _) = out[1], out[0]
+    if F * (18 * n + 9) * 8 > 160 * 1024:
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(la, lb)
+        return
+    assert abs(sa[0, 1] - sb[0, 1]) <= 1e-6 * sb[0, 1], (sa[0], sb[0])
+    dev = np.linalg.norm(a - b, axis=-1)
+    assert np.nanmax(dev) < 0.05, np.nanmax(dev)
