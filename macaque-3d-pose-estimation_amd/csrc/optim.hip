@@ -315,133 +315,143 @@ struct FacRec {
   double L[OPT_MAXN][9];  // L[d-1] = L_{f,f-d}
 };
 
+// Indices of the constraints touching joint j, into ck[OPT_MAXL]; returns their count.
+__device__ __forceinline__ int joint_cons(const OptDims& D, const OptBufs& Bf, int j, int* ck) {
+  int n = 0;
+  for (int k = 0; k < D.NL; ++k)
+    if (Bf.cons[2 * k] == j || Bf.cons[2 * k + 1] == j) ck[n++] = k;
+  return n;
+}
+
+// Diagonal block of joint j at frame f: reprojection Gauss-Newton block + limb-length terms +
+// smoothness + lam * damped diagonal.
+template <int NN>
+__device__ __forceinline__ void assemble_block(const OptDims& D, const OptBufs& Bf, const int* ck, int nck, int b,
+                                               int j, int f, double s2, double lam, double (&A)[3][3]) {
+  const int F = D.F, J = D.J;
+  const double* Rm = Bf.R + (((size_t)b * F + f) * J + j) * 6;
+  A[0][0] = Rm[0]; A[0][1] = Rm[1]; A[0][2] = Rm[2];
+  A[1][0] = Rm[1]; A[1][1] = Rm[3]; A[1][2] = Rm[4];
+  A[2][0] = Rm[2]; A[2][1] = Rm[4]; A[2][2] = Rm[5];
+  const double* lb = Bf.lenJ + ((size_t)b * F + f) * D.NL * 5;
+  for (int t = 0; t < nck; ++t) {
+    const double* l = lb + ck[t] * 5;
+    const double l0 = l[0], l1 = l[1], l2 = l[2];
+    A[0][0] += l0 * l0; A[0][1] += l0 * l1; A[0][2] += l0 * l2;
+    A[1][0] += l1 * l0; A[1][1] += l1 * l1; A[1][2] += l1 * l2;
+    A[2][0] += l2 * l0; A[2][1] += l2 * l1; A[2][2] += l2 * l2;
+  }
+  const double* dg = Bf.diag + (size_t)b * D.NV + (size_t)f * J * 3 + 3 * j;
+  const double sd = s2 * dtd(f, f, F, NN, D.c);
+  A[0][0] += sd + lam * damp_of(dg[0]);
+  A[1][1] += sd + lam * damp_of(dg[1]);
+  A[2][2] += sd + lam * damp_of(dg[2]);
+}
+
+// One step of the block-banded Cholesky recurrence: from frame f's diagonal block A and the last
+// NN frames' factor blocks W (W[k-1] = frame f-k), the blocks L_{f,f-d} and inv(L_ff).
+template <int NN>
+__device__ __forceinline__ void factor_frame(const OptDims& D, double s2, int f, double (&A)[3][3],
+                                             const FacRec (&W)[NN], FacRec& cur) {
+  const int F = D.F;
+#pragma unroll
+  for (int d = NN; d >= 1; --d) {
+    const int i = f - d;
+    if (i < 0) {
+#pragma unroll
+      for (int e = 0; e < 9; ++e) cur.L[d - 1][e] = 0.0;
+      continue;
+    }
+    double M[3][3];
+    const double off = s2 * dtd(f, i, F, NN, D.c);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) M[r][c] = (r == c) ? off : 0.0;
+#pragma unroll
+    for (int e = d + 1; e <= NN; ++e) {
+      if (f - e < 0) continue;
+      const double* Lf = cur.L[e - 1];          // L_{f, f-e}
+      const double* Li = W[d - 1].L[e - d - 1];  // L_{i, f-e}
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          M[r][c] -= Lf[3 * r] * Li[3 * c] + Lf[3 * r + 1] * Li[3 * c + 1] + Lf[3 * r + 2] * Li[3 * c + 2];
+    }
+    const double* Ii = W[d - 1].inv;  // inv(L_ii) (lower)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        cur.L[d - 1][3 * r + c] = M[r][0] * Ii[3 * c] + M[r][1] * Ii[3 * c + 1] + M[r][2] * Ii[3 * c + 2];
+  }
+#pragma unroll
+  for (int d = 1; d <= NN; ++d) {
+    if (f - d < 0) continue;
+    const double* Lf = cur.L[d - 1];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        A[r][c] -= Lf[3 * r] * Lf[3 * c] + Lf[3 * r + 1] * Lf[3 * c + 1] + Lf[3 * r + 2] * Lf[3 * c + 2];
+  }
+  const double l00 = sqrt(fmax(A[0][0], 1e-300));
+  const double l10 = A[1][0] / l00, l20 = A[2][0] / l00;
+  const double l11 = sqrt(fmax(A[1][1] - l10 * l10, 1e-300));
+  const double l21 = (A[2][1] - l20 * l10) / l11;
+  const double l22 = sqrt(fmax(A[2][2] - l20 * l20 - l21 * l21, 1e-300));
+  const double i00 = 1 / l00, i11 = 1 / l11, i22 = 1 / l22;
+  const double i10 = -l10 * i00 * i11;
+  const double i21 = -l21 * i11 * i22;
+  const double i20 = -(l20 * i00 + l21 * i10) * i22;
+  cur.inv[0] = i00; cur.inv[1] = 0; cur.inv[2] = 0;
+  cur.inv[3] = i10; cur.inv[4] = i11; cur.inv[5] = 0;
+  cur.inv[6] = i20; cur.inv[7] = i21; cur.inv[8] = i22;
+}
+
+// M_{f,d} = I_f L_{f,f-d} and N_{f,d} = (L_{f+d,f} I_f)^T (the record layout above).
+__device__ __forceinline__ void premul_M(const double* I, const double* Lf, double* o) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[3 * r + c] = I[3 * r] * Lf[c] + I[3 * r + 1] * Lf[3 + c] + I[3 * r + 2] * Lf[6 + c];
+}
+__device__ __forceinline__ void premul_N(const double* Ii, const double* Lf, double* o) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[3 * r + c] = Lf[3 * c] * Ii[r] + Lf[3 * c + 1] * Ii[3 + r] + Lf[3 * c + 2] * Ii[6 + r];
+}
+
+// Global-memory factorization, one thread per (animal, joint): for clips too long for LDS.
 template <int NN>
 __device__ void factor_series(const OptDims& D, const OptBufs& Bf, int b, int j, double lam) {
   const int F = D.F, J = D.J;
   const double ssf = Bf.ssf[b];
   const double s2 = F > NN ? ssf * ssf : 0.0;
   double* fb = Bf.fac + ((size_t)b * J + j) * F * OPT_FS;
-  int ck[16], nck = 0;
-  bool many = false;
-  for (int k = 0; k < D.NL; ++k)
-    if (Bf.cons[2 * k] == j || Bf.cons[2 * k + 1] == j) {
-      if (nck < 16) ck[nck++] = k;
-      else many = true;
-    }
-  auto load_A = [&](int f, double (&A)[3][3]) {
-    const double* Rm = Bf.R + (((size_t)b * F + f) * J + j) * 6;
-    A[0][0] = Rm[0]; A[0][1] = Rm[1]; A[0][2] = Rm[2];
-    A[1][0] = Rm[1]; A[1][1] = Rm[3]; A[1][2] = Rm[4];
-    A[2][0] = Rm[2]; A[2][1] = Rm[4]; A[2][2] = Rm[5];
-    const double* lb = Bf.lenJ + ((size_t)b * F + f) * D.NL * 5;
-    if (!many) {
-      for (int t = 0; t < nck; ++t) {
-        const double* l = lb + ck[t] * 5;
-        const double l0 = l[0], l1 = l[1], l2 = l[2];
-        A[0][0] += l0 * l0; A[0][1] += l0 * l1; A[0][2] += l0 * l2;
-        A[1][0] += l1 * l0; A[1][1] += l1 * l1; A[1][2] += l1 * l2;
-        A[2][0] += l2 * l0; A[2][1] += l2 * l1; A[2][2] += l2 * l2;
-      }
-    } else {
-      for (int k = 0; k < D.NL; ++k) {
-        if (Bf.cons[2 * k] != j && Bf.cons[2 * k + 1] != j) continue;
-        const double* l = lb + k * 5;
-        for (int r = 0; r < 3; ++r)
-          for (int c = 0; c < 3; ++c) A[r][c] += l[r] * l[c];
-      }
-    }
-    const double* dg = Bf.diag + (size_t)b * D.NV + (size_t)f * J * 3 + 3 * j;
-    const double sd = s2 * dtd(f, f, F, NN, D.c);
-    A[0][0] += sd + lam * damp_of(dg[0]);
-    A[1][1] += sd + lam * damp_of(dg[1]);
-    A[2][2] += sd + lam * damp_of(dg[2]);
-  };
+  int ck[OPT_MAXL];
+  const int nck = joint_cons(D, Bf, j, ck);
   FacRec W[NN];  // W[k-1] = frame f-k
   double An[3][3];
-  load_A(0, An);
+  assemble_block<NN>(D, Bf, ck, nck, b, j, 0, s2, lam, An);
   for (int f = 0; f < F; ++f) {
     double A[3][3];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
       for (int c = 0; c < 3; ++c) A[r][c] = An[r][c];
-    if (f + 1 < F) load_A(f + 1, An);
+    if (f + 1 < F) assemble_block<NN>(D, Bf, ck, nck, b, j, f + 1, s2, lam, An);
     FacRec cur;
-#pragma unroll
-    for (int d = NN; d >= 1; --d) {
-      const int i = f - d;
-      if (i < 0) {
-#pragma unroll
-        for (int e = 0; e < 9; ++e) cur.L[d - 1][e] = 0.0;
-        continue;
-      }
-      double M[3][3];
-      const double off = s2 * dtd(f, i, F, NN, D.c);
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) M[r][c] = (r == c) ? off : 0.0;
-#pragma unroll
-      for (int e = d + 1; e <= NN; ++e) {
-        if (f - e < 0) continue;
-        const double* Lf = cur.L[e - 1];          // L_{f, f-e}
-        const double* Li = W[d - 1].L[e - d - 1];  // L_{i, f-e}
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int c = 0; c < 3; ++c)
-            M[r][c] -= Lf[3 * r] * Li[3 * c] + Lf[3 * r + 1] * Li[3 * c + 1] + Lf[3 * r + 2] * Li[3 * c + 2];
-      }
-      const double* Ii = W[d - 1].inv;  // inv(L_ii) (lower)
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          cur.L[d - 1][3 * r + c] = M[r][0] * Ii[3 * c] + M[r][1] * Ii[3 * c + 1] + M[r][2] * Ii[3 * c + 2];
-    }
-#pragma unroll
-    for (int d = 1; d <= NN; ++d) {
-      if (f - d < 0) continue;
-      const double* Lf = cur.L[d - 1];
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          A[r][c] -= Lf[3 * r] * Lf[3 * c] + Lf[3 * r + 1] * Lf[3 * c + 1] + Lf[3 * r + 2] * Lf[3 * c + 2];
-    }
-    const double l00 = sqrt(fmax(A[0][0], 1e-300));
-    const double l10 = A[1][0] / l00, l20 = A[2][0] / l00;
-    const double l11 = sqrt(fmax(A[1][1] - l10 * l10, 1e-300));
-    const double l21 = (A[2][1] - l20 * l10) / l11;
-    const double l22 = sqrt(fmax(A[2][2] - l20 * l20 - l21 * l21, 1e-300));
-    const double i00 = 1 / l00, i11 = 1 / l11, i22 = 1 / l22;
-    const double i10 = -l10 * i00 * i11;
-    const double i21 = -l21 * i11 * i22;
-    const double i20 = -(l20 * i00 + l21 * i10) * i22;
-    cur.inv[0] = i00; cur.inv[1] = 0; cur.inv[2] = 0;
-    cur.inv[3] = i10; cur.inv[4] = i11; cur.inv[5] = 0;
-    cur.inv[6] = i20; cur.inv[7] = i21; cur.inv[8] = i22;
+    factor_frame<NN>(D, s2, f, A, W, cur);
     double* o = fb + (size_t)f * OPT_FS;
 #pragma unroll
     for (int e = 0; e < 9; ++e) o[e] = cur.inv[e];
 #pragma unroll
     for (int d = 1; d <= NN; ++d) {
-      const double* Lf = cur.L[d - 1];
-      const double* I = cur.inv;
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int c = 0; c < 3; ++c)  // M_{f,d} = I_f L_{f,f-d}
-          o[9 * d + 3 * r + c] = I[3 * r] * Lf[c] + I[3 * r + 1] * Lf[3 + c] + I[3 * r + 2] * Lf[6 + c];
-      if (f - d >= 0) {  // N_{f-d,d} = (L_{f,f-d} I_{f-d})^T, into frame f-d's record
-        const double* Ii = W[d - 1].inv;
-        double* on = fb + (size_t)(f - d) * OPT_FS + 9 + 9 * NN + 9 * (d - 1);
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int c = 0; c < 3; ++c)
-            on[3 * r + c] = Lf[3 * c] * Ii[r] + Lf[3 * c + 1] * Ii[3 + r] + Lf[3 * c + 2] * Ii[6 + r];
-      }
+      premul_M(cur.inv, cur.L[d - 1], o + 9 * d);
+      if (f - d >= 0) premul_N(W[d - 1].inv, cur.L[d - 1], fb + (size_t)(f - d) * OPT_FS + 9 + 9 * NN + 9 * (d - 1));
       if (f + d >= F) {
 #pragma unroll
         for (int e = 0; e < 9; ++e) o[9 + 9 * NN + 9 * (d - 1) + e] = 0.0;
@@ -453,16 +463,20 @@ __device__ void factor_series(const OptDims& D, const OptBufs& Bf, int b, int j,
   }
 }
 
+__device__ __forceinline__ void length_pinv(const OptDims& D, const OptBufs& Bf, int b, double lam) {
+  if (D.fix) return;
+  for (int k = 0; k < D.NL; ++k) {
+    const double E = Bf.diag[(size_t)b * D.NV + D.NX + k];
+    Bf.pinvL[(size_t)b * OPT_MAXL + k] = 1.0 / (E + lam * damp_of(E) + 1e-300);
+  }
+}
+
 __global__ void __launch_bounds__(64) optim_factor_kernel(OptDims D, OptBufs Bf) {
   const int b = blockIdx.x, j = threadIdx.x;
   const int J = D.J;
   const double lam = Bf.ctl[2 * b];
   if (j == J) {
-    if (!D.fix)
-      for (int k = 0; k < D.NL; ++k) {
-        const double E = Bf.diag[(size_t)b * D.NV + D.NX + k];
-        Bf.pinvL[(size_t)b * OPT_MAXL + k] = 1.0 / (E + lam * damp_of(E) + 1e-300);
-      }
+    length_pinv(D, Bf, b, lam);
     return;
   }
   if (j > J) return;
@@ -470,6 +484,84 @@ __global__ void __launch_bounds__(64) optim_factor_kernel(OptDims D, OptBufs Bf)
   else if (D.n == 2) factor_series<2>(D, Bf, b, j, lam);
   else factor_series<3>(D, Bf, b, j, lam);
 }
+
+// The factorization with the series in LDS, one 256-thread block per (joint, animal):
+//   1. all threads assemble the diagonal blocks A_f (frame-parallel);
+//   2. thread 0 runs the Cholesky recurrence on LDS operands (inv(L_ff), L_{f,f-d} into LDS);
+//   3. all threads write I_f and the pre-multiplied M / N blocks (frame-parallel).
+// Only the recurrence's own arithmetic is sequential.  LDS: optim_factor_lds_bytes.
+template <int NN>
+__global__ void __launch_bounds__(256) optim_factor_lds_kernel(OptDims D, OptBufs Bf) {
+  const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  const int F = D.F, J = D.J;
+  const double lam = Bf.ctl[2 * b];
+  if (j == J) {
+    if (t == 0) length_pinv(D, Bf, b, lam);
+    return;
+  }
+  constexpr int RS = 9 + 9 * NN;  // record doubles: inv(L_ff), L_{f,f-1..n}
+  extern __shared__ double lds_opt[];
+  double* sA = lds_opt;               // [F][6] upper triangle of A_f
+  double* sRec = sA + (size_t)F * 6;  // [F][RS]
+  const double ssf = Bf.ssf[b];
+  const double s2 = F > NN ? ssf * ssf : 0.0;
+  __shared__ int s_ck[OPT_MAXL];
+  __shared__ int s_nck;
+  if (t == 0) s_nck = joint_cons(D, Bf, j, s_ck);
+  __syncthreads();
+  const int nck = s_nck;
+  for (int f = t; f < F; f += 256) {
+    double A[3][3];
+    assemble_block<NN>(D, Bf, s_ck, nck, b, j, f, s2, lam, A);
+    double* o = sA + 6 * f;
+    o[0] = A[0][0]; o[1] = A[0][1]; o[2] = A[0][2];
+    o[3] = A[1][1]; o[4] = A[1][2]; o[5] = A[2][2];
+  }
+  __syncthreads();
+  if (t == 0) {
+    FacRec W[NN];
+    for (int f = 0; f < F; ++f) {
+      const double* a = sA + 6 * f;
+      double A[3][3];
+      A[0][0] = a[0]; A[0][1] = a[1]; A[0][2] = a[2];
+      A[1][0] = a[1]; A[1][1] = a[3]; A[1][2] = a[4];
+      A[2][0] = a[2]; A[2][1] = a[4]; A[2][2] = a[5];
+      FacRec cur;
+      factor_frame<NN>(D, s2, f, A, W, cur);
+      double* o = sRec + (size_t)f * RS;
+#pragma unroll
+      for (int e = 0; e < 9; ++e) o[e] = cur.inv[e];
+#pragma unroll
+      for (int d = 0; d < NN; ++d)
+#pragma unroll
+        for (int e = 0; e < 9; ++e) o[9 + 9 * d + e] = cur.L[d][e];
+#pragma unroll
+      for (int k = NN - 1; k >= 1; --k) W[k] = W[k - 1];
+      W[0] = cur;
+    }
+  }
+  __syncthreads();
+  double* fb = Bf.fac + ((size_t)b * J + j) * F * OPT_FS;
+  for (int f = t; f < F; f += 256) {
+    const double* rec = sRec + (size_t)f * RS;
+    double* o = fb + (size_t)f * OPT_FS;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) o[e] = rec[e];
+#pragma unroll
+    for (int d = 1; d <= NN; ++d) {
+      premul_M(rec, rec + 9 * d, o + 9 * d);
+      double* on = o + 9 + 9 * NN + 9 * (d - 1);
+      if (f + d < F) {
+        premul_N(rec, sRec + (size_t)(f + d) * RS + 9 * d, on);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) on[e] = 0.0;
+      }
+    }
+  }
+}
+
+size_t optim_factor_lds_bytes(int F, int NN) { return (size_t)F * (15 + 9 * NN) * sizeof(double); }
 
 __device__ __forceinline__ double rz_at(const OptDims& D, const OptBufs& Bf, int b, int it) {
   const double* p = Bf.rzJ + ((size_t)b * (OPT_MAXIT + 1) + it) * (D.J + 1);
@@ -1049,7 +1141,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
   std::vector<double> lam(B, 1e-3), cost(B), costt(B), hctl(2 * B, 0.0);
   std::vector<int> active(B, 1), iters(B, 0), status(B, 2);
 
-  // preconditioner step: series staged in LDS when they fit (every clip up to ~400 frames)
+  // preconditioner step: series staged in LDS when they fit (every clip up to ~450 frames at n = 2)
   const size_t lds_b = optim_precond_lds_bytes(F, D.n);
   const bool use_lds = g_optim_precond_lds && lds_b <= 160 * 1024;
   auto precond = [&](int it) {
@@ -1062,12 +1154,30 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
     else if (D.n == 2) hipLaunchKernelGGL(optim_precond_lds_kernel<2>, grid, dim3(256), lds_b, s, D, Bf, it);
     else hipLaunchKernelGGL(optim_precond_lds_kernel<3>, grid, dim3(256), lds_b, s, D, Bf, it);
   };
-  if (use_lds) {
+  // factorization: the same choice (the LDS kernel's footprint is smaller than the apply's)
+  const size_t fac_lds_b = optim_factor_lds_bytes(F, D.n);
+  const bool fac_lds = g_optim_precond_lds && fac_lds_b + 512 <= 160 * 1024;  // + the static constraint list
+  auto factor = [&]() {
+    if (!fac_lds) {
+      hipLaunchKernelGGL(optim_factor_kernel, dim3(B), dim3(64), 0, s, D, Bf);
+      return;
+    }
+    const dim3 grid(J + 1, B);
+    if (D.n == 1) hipLaunchKernelGGL(optim_factor_lds_kernel<1>, grid, dim3(256), fac_lds_b, s, D, Bf);
+    else if (D.n == 2) hipLaunchKernelGGL(optim_factor_lds_kernel<2>, grid, dim3(256), fac_lds_b, s, D, Bf);
+    else hipLaunchKernelGGL(optim_factor_lds_kernel<3>, grid, dim3(256), fac_lds_b, s, D, Bf);
+  };
+  if (use_lds || fac_lds) {
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      const int mx = 160 * 1024;
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      // (dynamic + static LDS may not exceed the CU's 160 KB, or the call fails and leaves a sticky error)
+      (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
+      (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
+      (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
       attr = true;
     }
   }
@@ -1095,7 +1205,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
     }
     if (hipMemcpyAsync(ctl, hctl.data(), sizeof(double) * 2 * B, hipMemcpyHostToDevice, s) != hipSuccess) return -3;
     (void)hipMemsetAsync(Bf.rzJ, 0, sizeof(double) * (size_t)B * (OPT_MAXIT + 1) * (J + 2), s);
-    hipLaunchKernelGGL(optim_factor_kernel, dim3(B), dim3(64), 0, s, D, Bf);
+    factor();
     precond(-1);
     for (int it = 0; it < npcg; ++it) {
       hipLaunchKernelGGL(optim_matvec_kernel, gridFB, dim3(OPT_THREADS), 0, s, D, Bf, it);
