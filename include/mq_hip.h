@@ -193,6 +193,38 @@ int mq_rcnn_post(mq_ctx* ctx, const float* rois, const float* head, const int32_
                  float img_h, float img_w, float inv_scale_w, float inv_scale_h, float score_thr, float iou_thr,
                  int max_det, float* det_boxes, float* det_scores, int32_t* det_counts, void* stream);
 
+/* ======================================================================= ID classifier
+ * Step-1 collar-ID classifier, ResNet-152 + GlobalAveragePooling + LinearClsHead (6 classes)
+ * (model/id/sn_resnet152_8xb32_in1k_pretrained_optimized_finetuned.py:41-73), replacing
+ * mmpretrain's ImageClassificationInferencer in classify_patches (step1_proc2d.py:140-163).  The
+ * convolutions are mq_id_im2col + mq_gemm_bf16 (folded BN bias, MQ_EPI 6 = ReLU); mqhip/resnet_id.py
+ * sequences them.  Maps are NHWC. */
+
+/* classify_patches' crop + cv2.resize(patch, (out_size, out_size), INTER_LINEAR): boxes int32 (n, 5) =
+ * (frame, x0, y0, x1, y1), the non-empty numpy slice frames[frame][y0:y1, x0:x1]; out u8 (n, out, out, 3). */
+int mq_id_crop_resize(mq_ctx* ctx, const uint8_t* frames, int64_t frame_stride, int height, int width,
+                      const int32_t* boxes, int n, int out_size, uint8_t* out, void* stream);
+
+/* The inferencer's test pipeline on square u8 BGR images (n, in_size, in_size, 3): ResizeEdge(edge,
+ * 'short', cv2 bilinear) + CenterCrop(crop) + to_rgb + (x - mean) / std -> bf16 NHWC (n, crop, crop, 3). */
+int mq_id_preprocess(mq_ctx* ctx, const uint8_t* in, int n, int in_size, int edge, int crop, uint16_t* out,
+                     void* stream);
+
+/* im2col of a bf16 NHWC map (n, h, w, c) for a kh x kw / stride / zero-pad convolution:
+ * out bf16 (n * oh * ow, kpad), k = (ky * kw + kx) * c + ch, zero for k >= kh * kw * c. */
+int mq_id_im2col(mq_ctx* ctx, const uint16_t* x, int n, int h, int w, int c, int kh, int kw, int stride, int pad,
+                 int kpad, uint16_t* out, void* stream);
+
+/* MaxPool2d(3, 2, 1) on bf16 NHWC -> (n, (h - 1) / 2 + 1, (w - 1) / 2 + 1, c). */
+int mq_id_maxpool(mq_ctx* ctx, const uint16_t* x, int n, int h, int w, int c, uint16_t* out, void* stream);
+
+/* x = relu(x) in place (f32, count % 4 == 0) and y = bf16(x). */
+int mq_id_relu_bf16(mq_ctx* ctx, float* x, uint16_t* y, int64_t count, void* stream);
+
+/* GlobalAveragePooling + fc (ncls x c f32, bias) + softmax: x f32 (n, hw, c) -> logits, probs f32 (n, ncls). */
+int mq_id_head(mq_ctx* ctx, const float* x, int n, int hw, int c, const float* fc_w, const float* fc_b, int ncls,
+               float* logits, float* probs, void* stream);
+
 /* ======================================================================= geometry
  * Replaces aniposelib CameraGroup (cameras.py:593-783), anipose filter_pose_viterbi
  * (filter_pose.py:48-186) and the mvpose DLT (multicam_toolbox.py:393-486).

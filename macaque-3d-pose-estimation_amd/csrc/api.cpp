@@ -17,6 +17,7 @@
 
 #include "geometry.hpp"
 #include "detector.hpp"
+#include "idcls.hpp"
 #include "kernels.hpp"
 #include "mq_hip.h"
 
@@ -739,6 +740,65 @@ int mq_subsample2(mq_ctx* ctx, const float* x, int n_img, int height, int width,
   if (!x || !out) return fail("mq_subsample2: null argument");
   if (n_img <= 0 || height <= 0 || width <= 0 || ch <= 0) return fail("mq_subsample2: bad sizes", -2);
   K_TRY(mq::subsample2(x, n_img, height, width, ch, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_id_crop_resize(mq_ctx* ctx, const uint8_t* frames, int64_t frame_stride, int height, int width,
+                      const int32_t* boxes, int n, int out_size, uint8_t* out, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!frames || !boxes || !out) return fail("mq_id_crop_resize: null argument");
+  if (n <= 0 || height <= 0 || width <= 0 || out_size <= 0 || frame_stride < (int64_t)height * width * 3)
+    return fail("mq_id_crop_resize: bad sizes", -2);
+  K_TRY(mq::id_crop_resize(frames, frame_stride, width, boxes, n, out_size, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_id_preprocess(mq_ctx* ctx, const uint8_t* in, int n, int in_size, int edge, int crop, uint16_t* out,
+                     void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!in || !out) return fail("mq_id_preprocess: null argument");
+  if (n <= 0 || in_size <= 0 || edge <= 0 || crop <= 0 || crop > edge) return fail("mq_id_preprocess: bad sizes", -2);
+  // mmpretrain CenterCrop: y1 = max(0, int(round((h - crop) / 2.)))  (Python round: half to even)
+  const double half = (edge - crop) / 2.0;
+  const int off = std::max(0, (int)std::nearbyint(half));
+  K_TRY(mq::id_edge_crop(in, n, in_size, edge, crop, off, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_id_im2col(mq_ctx* ctx, const uint16_t* x, int n, int h, int w, int c, int kh, int kw, int stride, int pad,
+                 int kpad, uint16_t* out, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !out) return fail("mq_id_im2col: null argument");
+  if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 || kpad < kh * kw * c ||
+      h + 2 * pad < kh || w + 2 * pad < kw)
+    return fail("mq_id_im2col: bad sizes", -2);
+  K_TRY(mq::im2col_bf16(x, n, h, w, c, kh, kw, stride, pad, kpad, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_id_maxpool(mq_ctx* ctx, const uint16_t* x, int n, int h, int w, int c, uint16_t* out, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !out) return fail("mq_id_maxpool: null argument");
+  if (n <= 0 || h <= 0 || w <= 0 || c <= 0) return fail("mq_id_maxpool: bad sizes", -2);
+  K_TRY(mq::maxpool3s2(x, n, h, w, c, out, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_id_relu_bf16(mq_ctx* ctx, float* x, uint16_t* y, int64_t count, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !y) return fail("mq_id_relu_bf16: null argument");
+  if (count <= 0 || count % 4) return fail("mq_id_relu_bf16: count % 4 != 0", -2);
+  K_TRY(mq::relu_bf16(x, y, count, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_id_head(mq_ctx* ctx, const float* x, int n, int hw, int c, const float* fc_w, const float* fc_b, int ncls,
+               float* logits, float* probs, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !fc_w || !fc_b || !logits || !probs) return fail("mq_id_head: null argument");
+  if (n <= 0 || hw <= 0 || c <= 0 || c > 8192 || ncls <= 0 || ncls > mq::ID_MAX_CLASSES)
+    return fail("mq_id_head: bad sizes (c <= 8192, ncls <= 16)", -2);
+  K_TRY(mq::gap_fc_softmax(x, n, hw, c, fc_w, fc_b, ncls, logits, probs, (hipStream_t)stream));
   return 0;
 }
 

@@ -94,7 +94,7 @@ def rescale_size(w, h, scale=(800, 800)):
 
 def linear_coeffs(dst, src):
     """cv::resize INTER_LINEAR tables: source offset and the two 11-bit weights per output index."""
-    scale = src / dst
+    scale = 1.0 / (dst / src)  # resize.cpp: 1. / inv_scale_x
     d = np.arange(dst, dtype=np.float64)
     f = ((d + 0.5) * scale - 0.5).astype(np.float32)
     s = np.floor(f).astype(np.int64)

@@ -59,7 +59,7 @@ def rescale_size(w, h, scale=(800, 800)):
 
 def _linear_coeffs(dst, src):
     """cv::resize INTER_LINEAR coefficient tables: source index and 11-bit weights per output."""
-    scale = src / dst  # 1 / inv_scale
+    scale = 1.0 / (dst / src)  # resize.cpp: scale_x = 1. / inv_scale_x, inv_scale_x = dsize.width / ssize.width
     ofs = np.zeros(dst, np.int64)
     a = np.zeros((dst, 2), np.int64)
     for d in range(dst):
@@ -80,8 +80,17 @@ def _linear_coeffs(dst, src):
 
 def resize_linear_u8(img, new_w, new_h):
     """cv2.resize(img, (new_w, new_h), INTER_LINEAR) for uint8 HxWx3 (OpenCV native fixed point:
-    integer horizontal pass, vertical pass ((S0>>4)*b0 >> 16) + ((S1>>4)*b1 >> 16), +2 >> 2)."""
+    integer horizontal pass, vertical pass ((S0>>4)*b0 >> 16) + ((S1>>4)*b1 >> 16), +2 >> 2; an exact
+    2x downscale is INTER_AREA).  The vertical rounding is the SIMD kernel's (VResizeLinearVec_32s8u);
+    OpenCV's scalar tail, (S0*b0 + S1*b1 + 2^21) >> 22, can differ by one in the last pixels of a row:
+    parity with cv2 itself is unpinned (cv2 is absent here)."""
     H, W, C = img.shape
+    if W == 2 * new_w and H == 2 * new_h:
+        # resize.cpp: INTER_LINEAR with an exact 2x downscale takes the INTER_AREA fast path
+        # (resizeAreaFast_: (a + b + c + d + 2) >> 2)
+        s = img.astype(np.int64)
+        v = s[0::2, 0::2] + s[0::2, 1::2] + s[1::2, 0::2] + s[1::2, 1::2]
+        return ((v + 2) >> 2).astype(np.uint8)
     xo, xa = _linear_coeffs(new_w, W)
     yo, ya = _linear_coeffs(new_h, H)
     src = img.astype(np.int64)

@@ -1,0 +1,124 @@
+"""GPU ID classifier (mqhip/resnet_id.py, csrc/resnet_id.hip) vs the oracle (oracle/resnet_id.py):
+classify_patches' slice + cv2 resize and the inferencer's ResizeEdge / CenterCrop / normalisation
+bit-exact; im2col / max-pool bit-exact; GAP + fc + softmax within 1e-5; the full ResNet-152 in bf16
+against the fp32 restatement within the tolerance written below (parity unpinned vs mmpretrain)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+
+@pytest.fixture(scope="module")
+def frames():
+    rng = np.random.default_rng(0)
+    f = rng.integers(0, 256, (2, 480, 640, 3), dtype=np.uint8)
+    f[1, 100:300, 200:500] = (f[1, 100:300, 200:500] // 4 + 90)   # some smooth-ish structure
+    return f
+
+
+BOXES = [(0, 10, 20, 200, 300), (1, 192, 100, 640, 548), (0, 0, 0, 224, 224), (1, 5, 7, 6, 8), (0, 600, 400, 640, 480),
+         (1, 17, 3, 465, 451), (0, 100, 50, 101, 470)]   # (view, x0, y0, x1, y1): any size, 2x (448), identity, 1x1
+
+
+def _model(depth=152, seed=0):
+    from mqhip import resnet_id as rid
+    sd = rid.make_random_weights(depth, seed=seed)
+    return sd, rid.ResNetIdHip(sd, depth=depth)
+
+
+def test_crop_resize_and_preprocess_bit_exact(frames):
+    from mqhip import resnet_id as rid
+    from oracle import resnet_id as orid
+    from oracle.swin_det import resize_linear_u8
+    sd = rid.make_random_weights(50)
+    m = rid.ResNetIdHip(sd, depth=50)
+    dev = torch.as_tensor(frames).cuda()
+    x, pat = m.preprocess(dev, BOXES)
+    torch.cuda.synchronize()
+    pat, x = pat.cpu().numpy(), x.float().cpu()
+    for i, (v, x0, y0, x1, y1) in enumerate(BOXES):
+        patch = frames[v, y0:y1, x0:x1]
+        ref = resize_linear_u8(np.ascontiguousarray(patch), 224, 224)
+        assert np.array_equal(pat[i], ref), i
+        xo = orid.preprocess(patch).permute(1, 2, 0).to(torch.bfloat16).float()
+        assert torch.equal(x[i], xo), i
+
+
+@pytest.mark.parametrize("c,k,s,p", [(3, 7, 2, 3), (64, 3, 1, 1), (64, 3, 2, 1), (128, 1, 2, 0), (24, 3, 2, 1)])
+def test_im2col_matches_unfold(c, k, s, p):
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    g = torch.Generator(device="cuda").manual_seed(c + k)
+    n, h, w = 2, 15, 12
+    x = torch.randn((n, h, w, c), generator=g, device="cuda").to(torch.bfloat16)
+    kpad = (k * k * c + 31) // 32 * 32
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    out = torch.full((n * oh * ow, kpad), 7.0, device="cuda", dtype=torch.bfloat16)
+    _lib.check(ctx.lib.mq_id_im2col(ctx.handle, _lib.ptr(x), n, h, w, c, k, k, s, p, kpad, _lib.ptr(out),
+                                    _lib.stream_ptr()), "mq_id_im2col")
+    cols = F.unfold(x.float().permute(0, 3, 1, 2), (k, k), padding=p, stride=s)
+    ref = cols.view(n, c, k * k, -1).permute(0, 3, 2, 1).reshape(n * oh * ow, k * k * c)
+    ref = F.pad(ref, (0, kpad - k * k * c))
+    assert torch.equal(out.float(), ref)
+
+
+def test_maxpool_and_head():
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn((3, 17, 14, 64), generator=g, device="cuda").to(torch.bfloat16)
+    out = torch.empty((3, 9, 7, 64), device="cuda", dtype=torch.bfloat16)
+    _lib.check(ctx.lib.mq_id_maxpool(ctx.handle, _lib.ptr(x), 3, 17, 14, 64, _lib.ptr(out), _lib.stream_ptr()), "mp")
+    ref = F.max_pool2d(x.float().permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(out.float(), ref)
+    feat = torch.randn((3, 49, 2048), generator=g, device="cuda")
+    fw = torch.randn((6, 2048), generator=g, device="cuda") * 0.02
+    fb = torch.randn((6,), generator=g, device="cuda")
+    lg, pr = torch.empty((3, 6), device="cuda"), torch.empty((3, 6), device="cuda")
+    _lib.check(ctx.lib.mq_id_head(ctx.handle, _lib.ptr(feat), 3, 49, 2048, _lib.ptr(fw), _lib.ptr(fb), 6, _lib.ptr(lg),
+                                  _lib.ptr(pr), _lib.stream_ptr()), "head")
+    rl = feat.mean(1) @ fw.t() + fb
+    torch.testing.assert_close(lg, rl, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(pr, torch.softmax(rl, 1), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("depth", [50, 152])
+def test_resnet_matches_fp32_oracle(frames, depth):
+    """bf16 operands / f32 accumulation vs the fp32 restatement: logits within 3e-2 * (max |logit| + 1),
+    probabilities within 2e-2, and the same label wherever the oracle's top-2 probability margin > 0.05."""
+    from oracle import resnet_id as orid
+    sd, m = _model(depth, seed=depth)
+    dev = torch.as_tensor(frames).cuda()
+    x, _ = m.preprocess(dev, BOXES)
+    lg, pr = m.forward(x)
+    torch.cuda.synchronize()
+    xo = torch.stack([orid.preprocess(frames[v, y0:y1, x0:x1]) for v, x0, y0, x1, y1 in BOXES])
+    with torch.no_grad():
+        rl, rp = orid.forward(sd, xo, depth)
+    lg, pr = lg.cpu(), pr.cpu()
+    scale = rl.abs().max() + 1
+    assert (lg - rl).abs().max() <= 3e-2 * scale, ((lg - rl).abs().max(), scale)
+    assert (pr - rp).abs().max() <= 2e-2, (pr - rp).abs().max()
+    top2 = rp.topk(2, dim=1).values
+    sure = (top2[:, 0] - top2[:, 1]) > 0.05
+    assert torch.equal(pr.argmax(1)[sure], rp.argmax(1)[sure])
+
+
+def test_classify_equals_oracle_classify_patches(frames):
+    """classify (all views' boxes in one batch) vs the oracle's classify_patches per view, including an empty
+    slice (label -1, score 0) and a negative-start box (numpy wrap-around)."""
+    from oracle import resnet_id as orid
+    sd, m = _model(50, seed=7)
+    boxes = [np.array([(10, 20, 200, 300), (5, 5, 5, 90), (-30, 100, 630, 400)]), np.array([(200, 100, 648, 548)])]
+    got = m.classify(frames, boxes)
+    for v in range(2):
+        patches = [frames[v][y1:y2, x1:x2] for (x1, y1, x2, y2) in boxes[v]]
+        ref = orid.classify_patches(sd, patches, depth=50)
+        for a, b in zip(got[v], ref):
+            assert a["pred_label"] == b["pred_label"]
+            assert abs(a["pred_score"] - b["pred_score"]) <= 2e-2
+    assert got[0][1] == {"pred_label": -1, "pred_score": 0.0}
