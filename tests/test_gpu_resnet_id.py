@@ -20,7 +20,7 @@ def frames():
     return f
 
 
-BOXES = [(0, 10, 20, 200, 300), (1, 192, 100, 640, 548), (0, 0, 0, 224, 224), (1, 5, 7, 6, 8), (0, 600, 400, 640, 480),
+BOXES = [(0, 10, 20, 200, 300), (1, 192, 30, 640, 478), (0, 0, 0, 224, 224), (1, 5, 7, 6, 8), (0, 600, 400, 640, 480),
          (1, 17, 3, 465, 451), (0, 100, 50, 101, 470)]   # (view, x0, y0, x1, y1): any size, 2x (448), identity, 1x1
 
 
