@@ -230,6 +230,30 @@ class ResNetIdHip:
         return out
 
 
+    def classify_patches(self, patches):
+        """classify_patches (step1_proc2d.py:140-163) on a list of HxWx3 uint8 BGR patches: every non-empty one
+        resized and classified in one batch -> [{pred_label, pred_score}] (label -1, score 0 for empty)."""
+        out = [{"pred_label": -1, "pred_score": 0.0} for _ in patches]
+        valid = [i for i, p in enumerate(patches) if p.shape[0] > 0 and p.shape[1] > 0]
+        if not valid:
+            return out
+        pat = torch.empty((len(valid), INPUT_SIZE, INPUT_SIZE, 3), device=self.dev, dtype=torch.uint8)
+        for j, i in enumerate(valid):
+            p = torch.as_tensor(np.ascontiguousarray(patches[i])).to(self.dev)
+            h, w = p.shape[:2]
+            bx = torch.tensor([[0, 0, 0, w, h]], dtype=torch.int32).to(self.dev)
+            _lib.check(self.ctx.lib.mq_id_crop_resize(self.ctx.handle, _lib.ptr(p), h * w * 3, h, w, _lib.ptr(bx), 1,
+                                                      INPUT_SIZE, _lib.ptr(pat[j]), self._s()), "mq_id_crop_resize")
+        x = torch.empty((len(valid), CROP, CROP, 3), device=self.dev, dtype=torch.bfloat16)
+        _lib.check(self.ctx.lib.mq_id_preprocess(self.ctx.handle, _lib.ptr(pat), len(valid), INPUT_SIZE, EDGE, CROP,
+                                                 _lib.ptr(x), self._s()), "mq_id_preprocess")
+        _, probs = self.forward(x)
+        pr = probs.cpu().numpy()
+        for j, i in enumerate(valid):
+            out[i] = {"pred_label": int(np.argmax(pr[j])), "pred_score": float(np.max(pr[j]))}
+        return out
+
+
 def init_id_model(weights=None, device: int = 0, depth=152):
     """The model ``init_id_model`` returns (step1_proc2d.py:125-136), with random weights when none are given."""
     return ResNetIdHip(weights if weights is not None else make_random_weights(depth), depth=depth, device=device)

@@ -16,11 +16,14 @@ The Swin-S Mask R-CNN detector runs on MI355X too (``init_detector`` / ``inferen
 step1:98, :226-237 -> ``mqhip.detector``); ``detect_stores`` gives, per camera and processed frame,
 the detections above SCORE_THR that the reference hands to its tracker (step1:229-240).
 
-Out of scope: the BoT-SORT tracker and ResNet ID classifier, and imgstore
-video decoding.  Their outputs enter here as data: per-frame tracker rows ``(N, >=5)``
-[x1, y1, x2, y2, track_id, ...] and, optionally, ID predictions -- carried by the per-camera
-``mqhip.io.FrameStore`` that ``proc`` reads; without ID predictions every box gets
-``assigned_id = -1`` (the reference's "not confident" value).
+The ResNet-152 collar-ID classifier runs on MI355X too (``init_id_model`` / ``classify_patches``,
+step1:125-163 -> ``mqhip.resnet_id``); ``process_stores(..., id_model=...)`` classifies every tracked
+box of a batch of time steps x cameras in one launch sequence.
+
+Tracker rows enter as data: per-frame ``(N, >=5)`` [x1, y1, x2, y2, track_id, ...] carried by the
+per-camera ``mqhip.io.FrameStore`` that ``proc`` reads (imgstore video decoding is out of scope).
+Without an ID model or stored ID predictions every box gets ``assigned_id = -1`` (the reference's
+"not confident" value).
 """
 from __future__ import annotations
 
@@ -46,6 +49,15 @@ MIN_MARGIN = 0.20
 MAX_MARGIN = 0.50
 DESIRED_AR = 192.0 / 256.0
 ID_CONF_THR = 0.80
+
+ID_CONFIGS = {
+    "normal": "./model/id/sn_resnet152_8xb32_in1k_pretrained_optimized_finetuned.py",
+    "mff1y": "./model/id/sn_resnet152_8xb32_in1k_mff1y_pretrained_optimized.py",
+}
+ID_CKPTS = {
+    "normal": "./model/id/id_finetuned.pth",
+    "mff1y": "./model/id/id_mff1y.pth",
+}
 
 KP_PARAMS = {"score_thr": SCORE_THR, "kp_thr": KP_THR, "ema_alpha": EMA_ALPHA, "disp_thr": DISP_THR,
              "min_margin": MIN_MARGIN, "max_margin": MAX_MARGIN, "desired_ar": DESIRED_AR,
@@ -92,6 +104,43 @@ def detect_stores(detector, stores, T, score_thr=SCORE_THR):
             keep = sc > score_thr
             out[i].append((plans[i][k][0], b[keep], sc[keep]))
     return out
+
+
+def init_id_model(device: str = "cuda:0", id_variant: str = "normal", weights=None):
+    """step1:125-136: the ResNet-152 ID classifier of ``id_variant`` (None for an unknown variant, as
+    there).  The checkpoint is read with torch.load(weights_only=True) when it exists (mmpretrain keys
+    under 'state_dict'); otherwise seeded random weights (no checkpoint ships with the reference)."""
+    from mqhip.resnet_id import ResNetIdHip, make_random_weights
+    if ID_CONFIGS.get(id_variant) is None or ID_CKPTS.get(id_variant) is None:
+        return None
+    dev = int(device.split(":")[1]) if ":" in device else 0
+    if weights is None:
+        ck = ID_CKPTS[id_variant]
+        if os.path.exists(ck):
+            import torch
+            sd = torch.load(ck, map_location="cpu", weights_only=True)
+            weights = {k: v.float() for k, v in sd.get("state_dict", sd).items()}
+        else:
+            weights = make_random_weights(152, seed=0)
+    return ResNetIdHip(weights, depth=152, device=dev)
+
+
+def classify_patches(id_model, patches, input_size: int = 224):
+    """step1:140-163: crop-and-classify patches through the ID model -> [{pred_label, pred_score}] (label -1,
+    score 0 for an empty patch or without a model).  All non-empty patches go through one batch."""
+    if id_model is None or not patches:
+        return [{"pred_label": -1, "pred_score": 0.0} for _ in patches]
+    if input_size != 224:
+        raise NotImplementedError("the ID pipeline is built for input_size 224 (ResizeEdge 256, CenterCrop 224)")
+    return id_model.classify_patches(patches)
+
+
+def classify_boxes(id_model, imgs, boxes_per_view):
+    """The ID half of step1:301-302 for all views of a frame: ``img[y1:y2, x1:x2]`` per int box, classified
+    in one batch -> per view [{pred_label, pred_score}]."""
+    if id_model is None:
+        return [[{"pred_label": -1, "pred_score": 0.0} for _ in b] for b in boxes_per_view]
+    return id_model.classify(imgs, boxes_per_view)
 
 
 def init_pose_model(config=POSE_CONFIG, checkpoint=POSE_CHECKPOINT, device="cuda:0"):
@@ -184,23 +233,31 @@ def _rows(pose_results, boxes, tids, smoother, frame_number, id_preds, kp_params
     return rows
 
 
-def process_frame(pose_model, img, tracks, smoother, frame_number, id_preds=None, kp_params=KP_PARAMS):
-    """One camera frame: tracker rows -> alldata.json rows (step1:255-364)."""
+def process_frame(pose_model, img, tracks, smoother, frame_number, id_preds=None, kp_params=KP_PARAMS,
+                  id_model=None):
+    """One camera frame: tracker rows -> alldata.json rows (step1:255-364).  With ``id_model`` the
+    tracked boxes' patches are classified here (step1:301-302); else ``id_preds`` (or none)."""
     boxes, tids = filter_tracks(tracks)
     if len(boxes) == 0:
         return []
     bb = expand_boxes(boxes, kp_params)
     res = inference_topdown(pose_model, img, bboxes=bb, bbox_format="xyxy")
+    if id_model is not None:
+        id_preds = classify_patches(id_model, [img[y1:y2, x1:x2] for (x1, y1, x2, y2) in boxes])
     return _rows(res, boxes, tids, smoother, frame_number, id_preds, kp_params)
 
 
 def process_frame_multiview(pose_model, imgs, tracks_per_view, smoothers, frame_number, id_preds_per_view=None,
-                            kp_params=KP_PARAMS):
-    """All views of one frame in one batched crop -> ViT -> decode pass.  imgs: list of HxWx3
-    uint8 or a (V,H,W,3) uint8 GPU tensor; smoothers: one KeypointSmoother per view."""
+                            kp_params=KP_PARAMS, id_model=None):
+    """All views of one frame in one batched crop -> ViT -> decode pass (and, with ``id_model``, one
+    batched ID pass over every tracked box).  imgs: list of HxWx3 uint8 or a (V,H,W,3) uint8 GPU tensor;
+    smoothers: one KeypointSmoother per view."""
     per_view = [filter_tracks(t) for t in tracks_per_view]
     bbs = [expand_boxes(b, kp_params) if len(b) else np.zeros((0, 4), np.float32) for b, _ in per_view]
     results = inference_topdown_batch(pose_model, imgs, bbs)
+    if id_model is not None:
+        id_preds_per_view = classify_boxes(id_model, imgs if not isinstance(imgs, list) else np.stack(imgs),
+                                           [b for b, _ in per_view])
     out = []
     for v, ((boxes, tids), res) in enumerate(zip(per_view, results)):
         ids = None if id_preds_per_view is None else id_preds_per_view[v]
@@ -209,7 +266,7 @@ def process_frame_multiview(pose_model, imgs, tracks_per_view, smoothers, frame_
 
 
 def process_single_cam(frames, tracks, out_dir, pose_model, frame_numbers=None, id_preds=None,
-                       kp_params=KP_PARAMS):
+                       kp_params=KP_PARAMS, id_model=None):
     """Pose half of step1:166-410 for one camera.  frames: iterable of BGR uint8 images;
     tracks: per-frame tracker rows; writes alldata.json + frame_num.npy to out_dir."""
     os.makedirs(out_dir, exist_ok=True)
@@ -218,7 +275,7 @@ def process_single_cam(frames, tracks, out_dir, pose_model, frame_numbers=None, 
     for k, (img, trk) in enumerate(zip(frames, tracks)):
         fn = k if frame_numbers is None else int(frame_numbers[k])
         ids = None if id_preds is None else id_preds[k]
-        results.append(process_frame(pose_model, img, trk, smoother, fn, ids, kp_params))
+        results.append(process_frame(pose_model, img, trk, smoother, fn, ids, kp_params, id_model=id_model))
         fnums.append(fn)
     np.save(Path(out_dir) / "frame_num.npy", np.array(fnums, dtype=np.int32))
     with open(Path(out_dir) / "alldata.json", "w") as fp:
@@ -281,13 +338,32 @@ def run_pose(pose_model, stores, jobs, steps, steps_per_batch=8):
     return raw
 
 
+def run_id(id_model, stores, jobs, steps, steps_per_batch=8):
+    """The ID classification of the given time steps' tracked boxes (step1:301-302): every job of
+    ``steps_per_batch`` consecutive steps (all cameras) in ONE batched patch -> ResNet launch sequence
+    per image size.  Returns {(step, cam): [{pred_label, pred_score}] per box}."""
+    steps = [k for k in steps if k in jobs]
+    out = {}
+    for b0 in range(0, len(steps), steps_per_batch):
+        by_shape = {}
+        for k in steps[b0:b0 + steps_per_batch]:
+            for (c, fn, boxes, _, _) in jobs[k]:
+                img = stores[c].image(fn)
+                by_shape.setdefault(img.shape, []).append(((k, c), img, boxes))
+        for items in by_shape.values():
+            preds = id_model.classify(np.stack([im for _, im, _ in items]), [bx for _, _, bx in items])
+            for (key, _, _), p in zip(items, preds):
+                out[key] = p
+    return out
+
+
 def _as_results(kp, sc):
     from types import SimpleNamespace
     return [SimpleNamespace(pred_instances=SimpleNamespace(keypoints=kp[i][None], keypoint_scores=sc[i][None]))
             for i in range(len(kp))]
 
 
-def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS):
+def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS, id_raw=None):
     """KP_THR, the recursive per-track EMA and the alldata rows (step1:300-370), per camera in time
     order, from the pose results of ``run_pose``.  Returns per camera (rows per kept frame, frame
     numbers) after the reference's "valid frames only" filter."""
@@ -305,8 +381,8 @@ def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS):
             else:
                 _, _, boxes, tids, _ = job_of[c]
                 kp, sc = raw[(k, c)]
-                results[c].append(_rows(_as_results(kp, sc), boxes, tids, smoothers[c], fn, st.id_preds_of(fn),
-                                        kp_params))
+                ids = id_raw[(k, c)] if id_raw is not None else st.id_preds_of(fn)
+                results[c].append(_rows(_as_results(kp, sc), boxes, tids, smoothers[c], fn, ids, kp_params))
             fnums[c].append(fn)
     out = []
     for c, st in enumerate(stores):  # "Save valid frames only" (step1:364-370)
@@ -316,20 +392,22 @@ def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS):
     return out
 
 
-def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8):
+def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8, id_model=None):
     """Pose half of step1_proc2d_custom / process_single_cam (step1_proc2d.py:166-447) for every
     camera at once.  Per camera the reference's time-grid walk, degenerate-box filter, margin
     expansion, KP_THR and recursive EMA are kept exactly (the EMA state is per camera and runs in
     time order); the ViTPose work of ``steps_per_batch`` time steps x all cameras goes through ONE
     batched crop -> ViT -> decode launch sequence (the reference: one inference_topdown per camera
-    frame).  Returns per camera (alldata rows per kept frame, frame numbers)."""
+    frame).  With ``id_model`` the tracked boxes are classified on the GPU the same way (else the stores'
+    ID predictions, if any).  Returns per camera (alldata rows per kept frame, frame numbers)."""
     plans, jobs = plan_jobs(stores, T, kp_params)
     raw = run_pose(pose_model, stores, jobs, range(len(T)), steps_per_batch)
-    return assemble_rows(stores, T, plans, jobs, raw, kp_params)
+    id_raw = None if id_model is None else run_id(id_model, stores, jobs, range(len(T)), steps_per_batch)
+    return assemble_rows(stores, T, plans, jobs, raw, kp_params, id_raw)
 
 
 def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None, redo=False, pose_model=None,
-                        device_str="cuda:0", steps_per_batch=8):
+                        device_str="cuda:0", steps_per_batch=8, id_model=None):
     """step1_proc2d.py:389-447 with the frame stores of ``mqhip.io.FrameStore`` and the tracker
     rows they carry (detector / tracker / ID classifier run upstream).  Writes
     <results_root>/<data_name>/<cam>/alldata.json and frame_num.npy."""
@@ -356,7 +434,7 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
         return
     if pose_model is None:
         pose_model = init_pose_model(device=device_str)
-    res = process_stores(pose_model, [stores[i] for i in todo], T, steps_per_batch=steps_per_batch)
+    res = process_stores(pose_model, [stores[i] for i in todo], T, steps_per_batch=steps_per_batch, id_model=id_model)
     for i, (rows, fn) in zip(todo, res):
         os.makedirs(out_dirs[i], exist_ok=True)
         np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))

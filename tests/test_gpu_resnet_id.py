@@ -122,3 +122,35 @@ def test_classify_equals_oracle_classify_patches(frames):
             assert a["pred_label"] == b["pred_label"]
             assert abs(a["pred_score"] - b["pred_score"]) <= 2e-2
     assert got[0][1] == {"pred_label": -1, "pred_score": 0.0}
+
+
+def test_step1_classify_patches_and_process_frame(frames, monkeypatch):
+    """step1 classify_patches(id_model, patches) (step1:140-163) with the MI355X model vs the oracle, and
+    process_frame_multiview(..., id_model=...) giving every tracked box its classified id columns."""
+    from oracle import resnet_id as orid
+    from src.pipeline import step1_proc2d as s1
+    sd, m = _model(50, seed=11)
+    patches = [frames[0, 20:300, 10:200], frames[1, 0:0, 5:9], frames[1, 30:478, 192:640], frames[0, 5:6, 7:8]]
+    got = s1.classify_patches(m, patches)
+    ref = orid.classify_patches(sd, patches, depth=50)
+    for a, b in zip(got, ref):
+        assert a["pred_label"] == b["pred_label"] and abs(a["pred_score"] - b["pred_score"]) <= 2e-2
+    assert got[1] == {"pred_label": -1, "pred_score": 0.0}
+
+    from types import SimpleNamespace
+
+    def fake_pose(model, imgs, bbs):
+        return [[SimpleNamespace(pred_instances=SimpleNamespace(keypoints=np.zeros((1, 17, 2)),
+                                                                keypoint_scores=np.ones((1, 17), np.float32)))
+                 for _ in b] for b in bbs]
+    monkeypatch.setattr(s1, "inference_topdown_batch", fake_pose)
+    tracks = [np.array([[10, 20, 200, 300, 1], [300, 100, 500, 400, 2]], float), np.array([[192, 30, 640, 478, 5]], float)]
+    sm = [s1.KeypointSmoother(), s1.KeypointSmoother()]
+    rows = s1.process_frame_multiview(None, [frames[0], frames[1]], tracks, sm, 0, id_model=m)
+    for v in range(2):
+        boxes, _ = s1.filter_tracks(tracks[v])
+        ref = orid.classify_patches(sd, [frames[v][y1:y2, x1:x2] for (x1, y1, x2, y2) in boxes], depth=50)
+        for row, r in zip(rows[v], ref):
+            assert abs(row[7] - r["pred_score"]) <= 2e-2
+            if abs(r["pred_score"] - s1.ID_CONF_THR) > 2e-2:
+                assert row[6] == (r["pred_label"] if r["pred_score"] >= s1.ID_CONF_THR else -1)

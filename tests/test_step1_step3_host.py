@@ -72,3 +72,52 @@ def test_known_assignment_kp2d_writer(tmp_path):
     assert k[0, 1, 1, 0, 0] == 5.0     # every matching row of the camera is written: the last one stays
     assert not k[0, 0, 1].any() and not k[1, 1].any()  # zero fill where absent
     np.testing.assert_array_equal(mqio.load_array_pickle(str(tmp_path / "kp2d.pickle")), k)
+
+
+class _FakeId:
+    """Deterministic stand-in for the ID model: label and score from the patch's mean value."""
+
+    def classify(self, imgs, boxes_per_view):
+        out = []
+        for img, bxs in zip(imgs, boxes_per_view):
+            res = []
+            for (x1, y1, x2, y2) in np.asarray(bxs).reshape(-1, 4):
+                p = np.asarray(img)[y1:y2, x1:x2]
+                if p.size == 0:
+                    res.append({"pred_label": -1, "pred_score": 0.0})
+                    continue
+                m = float(p.mean())
+                res.append({"pred_label": int(m) % 6, "pred_score": 0.5 + (m % 1.0) * 0.5})
+            out.append(res)
+        return out
+
+    def classify_patches(self, patches):
+        return [self.classify([p], [np.array([[0, 0, p.shape[1], p.shape[0]]])])[0][0] for p in patches]
+
+
+def test_process_stores_with_id_model_classifies_every_tracked_box(tmp_path, monkeypatch):
+    """step1:301-350: the tracked boxes' patches are classified (here by a stand-in) and the id columns
+    follow ID_CONF_THR; the batched run_id equals a per-frame classify_patches of the boxes."""
+    from src.pipeline import step1_proc2d as s1
+    monkeypatch.setattr(s1, "inference_topdown_batch", _fake_pose)
+    stores = _stores(tmp_path)
+    t0 = stores[0].frame_time[0]
+    T = np.arange(t0, stores[0].frame_time[-1], 1.0 / 24)
+    fake = _FakeId()
+    got = s1.process_stores(None, stores, T, steps_per_batch=3, id_model=fake)
+    plans, jobs = s1.plan_jobs(stores, T)
+    n_rows = 0
+    for c, st in enumerate(stores):
+        rows_by_fn = dict(zip(got[c][1], got[c][0]))
+        for k, js in jobs.items():
+            for (cc, fn, boxes, tids, _) in js:
+                if cc != c:
+                    continue
+                img = st.image(fn)
+                ref = s1.classify_patches(fake, [img[y1:y2, x1:x2] for (x1, y1, x2, y2) in boxes])
+                for row, r in zip(rows_by_fn[fn], ref):
+                    assert row[7] == r["pred_score"]
+                    assert row[6] == (r["pred_label"] if r["pred_score"] >= s1.ID_CONF_THR else -1)
+                    n_rows += 1
+    assert n_rows > 0
+    assert s1.classify_patches(None, [np.zeros((3, 3, 3), np.uint8)]) == [{"pred_label": -1, "pred_score": 0.0}]
