@@ -20,8 +20,12 @@ The ResNet-152 collar-ID classifier runs on MI355X too (``init_id_model`` / ``cl
 step1:125-163 -> ``mqhip.resnet_id``); ``process_stores(..., id_model=...)`` classifies every tracked
 box of a batch of time steps x cameras in one launch sequence.
 
-Tracker rows enter as data: per-frame ``(N, >=5)`` [x1, y1, x2, y2, track_id, ...] carried by the
-per-camera ``mqhip.io.FrameStore`` that ``proc`` reads (imgstore video decoding is out of scope).
+The BoT-SORT tracker (``mqhip.tracker.BotSort`` with BOTSORT_CFG, host logic as in the reference)
+turns the detections into tracker rows: ``track_stores`` runs detector -> tracker per camera over the
+frame plan, and ``step1_proc2d_custom(..., detector=...)`` chains detector -> tracker -> pose -> ID.
+Without a detector the tracker rows enter as data: per-frame ``(N, >=5)`` [x1, y1, x2, y2,
+track_id, ...] carried by the per-camera ``mqhip.io.FrameStore`` that ``proc`` reads (imgstore video
+decoding is out of scope).
 Without an ID model or stored ID predictions every box gets ``assigned_id = -1`` (the reference's
 "not confident" value).
 """
@@ -49,6 +53,10 @@ MIN_MARGIN = 0.20
 MAX_MARGIN = 0.50
 DESIRED_AR = 192.0 / 256.0
 ID_CONF_THR = 0.80
+
+TRACK_BUFFER = 72  # frames to buffer lost tracks (~3 s at 24 fps), step1:75
+BOTSORT_CFG = dict(with_reid=False, track_high_thresh=SCORE_THR, track_low_thresh=0.10, new_track_thresh=SCORE_THR,
+                   track_buffer=TRACK_BUFFER, match_thresh=0.80, frame_rate=24, cmc_method="sift")
 
 ID_CONFIGS = {
     "normal": "./model/id/sn_resnet152_8xb32_in1k_pretrained_optimized_finetuned.py",
@@ -141,6 +149,32 @@ def classify_boxes(id_model, imgs, boxes_per_view):
     if id_model is None:
         return [[{"pred_label": -1, "pred_score": 0.0} for _ in b] for b in boxes_per_view]
     return id_model.classify(imgs, boxes_per_view)
+
+
+def init_tracker(cfg=None):
+    """step1:99 / :430 ``BotSort(**BOTSORT_CFG)`` -- one per camera (camera-motion compensation: identity,
+    see mqhip.tracker)."""
+    from mqhip.tracker import BotSort
+    return BotSort(**(cfg or BOTSORT_CFG))
+
+
+def track_stores(detector, stores, T, score_thr=SCORE_THR, tracker_cfg=None):
+    """Detector -> tracker per camera over step 1's frame plan (step1:225-252): a frame whose detections are
+    all <= score_thr gets no tracker update and no rows; otherwise ``tracker.update(dets6, img)`` with
+    dets6 = [boxes, scores, 0].  Returns per camera {frame_number: tracker rows (k, 8)}."""
+    dets = detect_stores(detector, stores, T, score_thr)
+    out = []
+    for c, st in enumerate(stores):
+        tr = init_tracker(tracker_cfg)
+        rows = {}
+        for fn, b, sc in dets[c]:
+            if len(sc) == 0:
+                rows[fn] = np.zeros((0, 8))
+                continue
+            d6 = np.hstack([np.asarray(b, np.float64), np.asarray(sc, np.float64)[:, None], np.zeros((len(sc), 1))])
+            rows[fn] = tr.update(d6, st.image(fn))
+        out.append(rows)
+    return out
 
 
 def init_pose_model(config=POSE_CONFIG, checkpoint=POSE_CHECKPOINT, device="cuda:0"):
@@ -300,10 +334,11 @@ def _frame_plan(store, T):
     return plan
 
 
-def plan_jobs(stores, T, kp_params=KP_PARAMS):
+def plan_jobs(stores, T, kp_params=KP_PARAMS, tracks=None):
     """Per camera the time-grid walk (_frame_plan) and, per time step, the pose jobs of the frames
     it newly reaches: {step: [(cam, frame_number, boxes int32, track ids, expanded boxes f32)]}
-    (degenerate-box filter and margin expansion of step1:254-292)."""
+    (degenerate-box filter and margin expansion of step1:254-292).  ``tracks``: per camera
+    {frame_number: tracker rows} (track_stores) instead of the stores' rows."""
     plans = [_frame_plan(st, T) for st in stores]
     jobs = {}
     for k in range(len(T)):
@@ -311,7 +346,8 @@ def plan_jobs(stores, T, kp_params=KP_PARAMS):
             fn, rep = plans[c][k]
             if rep:
                 continue
-            boxes, tids = filter_tracks(st.tracks_of(fn))
+            rows = st.tracks_of(fn) if tracks is None else tracks[c].get(fn, np.zeros((0, 8)))
+            boxes, tids = filter_tracks(rows)
             if len(boxes):
                 jobs.setdefault(k, []).append((c, fn, boxes, tids, expand_boxes(boxes, kp_params)))
     return plans, jobs
@@ -392,7 +428,7 @@ def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS, id_raw=None)
     return out
 
 
-def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8, id_model=None):
+def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8, id_model=None, tracks=None):
     """Pose half of step1_proc2d_custom / process_single_cam (step1_proc2d.py:166-447) for every
     camera at once.  Per camera the reference's time-grid walk, degenerate-box filter, margin
     expansion, KP_THR and recursive EMA are kept exactly (the EMA state is per camera and runs in
@@ -400,14 +436,14 @@ def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8
     batched crop -> ViT -> decode launch sequence (the reference: one inference_topdown per camera
     frame).  With ``id_model`` the tracked boxes are classified on the GPU the same way (else the stores'
     ID predictions, if any).  Returns per camera (alldata rows per kept frame, frame numbers)."""
-    plans, jobs = plan_jobs(stores, T, kp_params)
+    plans, jobs = plan_jobs(stores, T, kp_params, tracks)
     raw = run_pose(pose_model, stores, jobs, range(len(T)), steps_per_batch)
     id_raw = None if id_model is None else run_id(id_model, stores, jobs, range(len(T)), steps_per_batch)
     return assemble_rows(stores, T, plans, jobs, raw, kp_params, id_raw)
 
 
 def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None, redo=False, pose_model=None,
-                        device_str="cuda:0", steps_per_batch=8, id_model=None):
+                        device_str="cuda:0", steps_per_batch=8, id_model=None, detector=None):
     """step1_proc2d.py:389-447 with the frame stores of ``mqhip.io.FrameStore`` and the tracker
     rows they carry (detector / tracker / ID classifier run upstream).  Writes
     <results_root>/<data_name>/<cam>/alldata.json and frame_num.npy."""
@@ -434,7 +470,9 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
         return
     if pose_model is None:
         pose_model = init_pose_model(device=device_str)
-    res = process_stores(pose_model, [stores[i] for i in todo], T, steps_per_batch=steps_per_batch, id_model=id_model)
+    sel = [stores[i] for i in todo]
+    tracks = None if detector is None else track_stores(detector, sel, T)
+    res = process_stores(pose_model, sel, T, steps_per_batch=steps_per_batch, id_model=id_model, tracks=tracks)
     for i, (rows, fn) in zip(todo, res):
         os.makedirs(out_dirs[i], exist_ok=True)
         np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))
@@ -442,7 +480,10 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
             json.dump(rows, fp)
 
 
-def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0, pose_model=None):
-    """step1.proc (step1_proc2d.py:450): the pose slice over every camera's frame store.  Unlike the
-    reference (which hard-codes cuda:1, step1:50,421) the device argument is honoured."""
-    step1_proc2d_custom(data_name, results_root, raw_root, fps=fps, pose_model=pose_model, device_str=device_str)
+def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0, pose_model=None, detector=None,
+         id_model=None):
+    """step1.proc (step1_proc2d.py:450) over every camera's frame store: pose (and ID with ``id_model``) on
+    the stores' tracker rows, or the full detector -> tracker -> pose -> ID chain with ``detector``.  Unlike
+    the reference (which hard-codes cuda:1, step1:50,421) the device argument is honoured."""
+    step1_proc2d_custom(data_name, results_root, raw_root, fps=fps, pose_model=pose_model, device_str=device_str,
+                        detector=detector, id_model=id_model)

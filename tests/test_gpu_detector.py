@@ -290,3 +290,49 @@ def test_detect_stores_follows_the_frame_plan(tmp_path, det_small):
         for _, b, s in res[c]:
             assert b.shape == (len(s), 4) and np.all(s > 0.5)
             assert np.all((b[:, 0] >= 0) & (b[:, 2] <= 320 + 1e-3) & (b[:, 1] >= 0) & (b[:, 3] <= 240 + 1e-3))
+
+
+def test_step1_detector_tracker_pose_id_chain(tmp_path, det_small):
+    """Step 1 end to end on the GPU (step1_proc2d.py:225-364): detector -> BoT-SORT per camera (host) ->
+    pose + ID on the tracked boxes.  The tracker rows equal a per-camera BotSort run over detect_stores'
+    output in plan order; every alldata row carries its track's id and box."""
+    import json
+    from mqhip import io as mqio
+    from mqhip.apis import PoseModelHip
+    from mqhip.resnet_id import ResNetIdHip, make_random_weights as id_weights
+    from mqhip.tracker import BotSort
+    from mqhip.weights import VIT_TINY, make_random_weights
+    from src.pipeline import step1_proc2d as s1
+    rng = np.random.default_rng(5)
+    for c in range(2):
+        fr = _frames(5, 240, 320, 40 + c)
+        times = 10.0 + np.cumsum(rng.uniform(0.03, 0.05, 5))
+        mqio.write_frame_store(str(tmp_path / f"chain.{200 + c}"), fr, times, np.arange(5) + 1, [[] for _ in range(5)],
+                               200 + c)
+    stores = [mqio.FrameStore(str(tmp_path / f"chain.{200 + c}")) for c in range(2)]
+    T = np.arange(10.0, 10.2, 1 / 24)
+    cfg = dict(s1.BOTSORT_CFG, track_high_thresh=0.3, new_track_thresh=0.3)
+    tracks = s1.track_stores(det_small, stores, T, score_thr=0.3, tracker_cfg=cfg)
+    dets = s1.detect_stores(det_small, stores, T, score_thr=0.3)
+    n_tracked = 0
+    for c in range(2):
+        tr = BotSort(**cfg)
+        for fn, b, sc in dets[c]:
+            ref = tr.update(np.hstack([b, sc[:, None], np.zeros((len(sc), 1))]), None) if len(sc) else np.zeros((0, 8))
+            np.testing.assert_array_equal(tracks[c][fn], ref)
+            n_tracked += len(ref)
+    assert n_tracked > 0
+    pose = PoseModelHip(VIT_TINY, make_random_weights(VIT_TINY, seed=1, device="cuda"), 0)
+    idm = ResNetIdHip(id_weights(50, seed=3), depth=50)
+    res = s1.process_stores(pose, stores, T, steps_per_batch=2, id_model=idm, tracks=tracks)
+    for c in range(2):
+        for rows, fn in zip(*res[c]):
+            boxes, tids = s1.filter_tracks(tracks[c].get(fn, np.zeros((0, 8))))
+            assert [r[0] for r in rows] == [int(t) for t in tids]
+            assert [r[1:5] for r in rows] == [[float(v) for v in b] for b in boxes]
+            assert all(len(r[5]) == 17 and -1 <= r[6] < 6 for r in rows)
+    out = tmp_path / "res"
+    s1.step1_proc2d_custom("chain", str(out), str(tmp_path), pose_model=pose, detector=det_small, id_model=idm)
+    for c in range(2):
+        with open(out / "chain" / str(200 + c) / "alldata.json") as f:
+            assert isinstance(json.load(f), list)
