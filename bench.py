@@ -143,6 +143,7 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
     lift = lift_cpu(cams_np)
     log(f"cpu baseline: config-4 lift {lift['total_s']:.1f} s")
     det = detector_cpu(reps=min(reps, 3))
+    idc = id_cpu(reps=min(reps, 3))
     return {"value": round(N_ANIMALS / t_frame2, 5), "unit": "individuals×frames/s", "cores": threads,
             "kind": "port", "nproc": info["nproc"], "os_cpu_count": info["os_cpu_count"], "cpu_model": info["model"],
             "statistic": f"median of {reps} after 1 warm-up",
@@ -153,7 +154,7 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
             "config1": {"seconds_per_frame": round(t1 + tri1, 4), "individuals_frames_per_s": round(1.0 / (t1 + tri1), 4),
                         "sample": "ViT-B fp32 flip-test forward + decode of 4 crops (4 views x 1 individual) + DLT"},
             "config4_lift": lift,
-            "config5_detector": det}
+            "config5_detector": det, "config5_id": idc}
 
 
 def detector_cpu(reps=3):
@@ -182,6 +183,27 @@ def detector_cpu(reps=3):
     return {"seconds_per_frame": round(t * N_VIEWS, 3), "seconds_per_view": round(t, 3),
             "sample": "oracle Swin-S + FPN + RPN head convolutions of 1 of the frame's 8 views (x8); RPN selection, "
                       "RoIAlign and the box head excluded", "statistic": f"median of {reps} after 1 warm-up"}
+
+
+def id_cpu(reps=3):
+    """Config-5 ID stage on the CPU port (oracle/resnet_id.py, torch fp32): preprocessing + ResNet-152 of 4 of
+    the frame's 32 tracked boxes, x8."""
+    import numpy as np
+    import torch
+    from mqhip.resnet_id import make_random_weights
+    from oracle import resnet_id as orid
+    sd = make_random_weights(152, seed=0)
+    img = np.random.default_rng(1).integers(0, 256, (IMG_H, IMG_W, 3), dtype=np.uint8)
+    patches = [img[200:700, 100 + 300 * a:400 + 300 * a] for a in range(4)]
+
+    def run():
+        with torch.no_grad():
+            orid.forward(sd, torch.stack([orid.preprocess(p) for p in patches]))
+
+    t, _ = _median_time(run, reps)
+    log(f"cpu baseline: ID classifier, 4 boxes {t:.2f} s (median of {reps})")
+    return {"seconds_per_frame": round(t * 8, 3), "sample": "oracle preprocessing + ResNet-152 of 4 of the frame's "
+            "32 tracked boxes (x8)", "statistic": f"median of {reps} after 1 warm-up"}
 
 
 def lift_inputs(A=4, F=300, C=8, seed=2):
@@ -284,14 +306,22 @@ def lift_gpu(device, reps=3):
 
 
 def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
-    """BASELINE config 5 on one GPU, without the tracker / ID classifier (out of scope): per frame,
-    the Swin-S Mask R-CNN detector on all 8 views (1536x2048), the 4 best detections of every view
-    as crop boxes, ViTPose flip test + UDP decode on those 32 crops, omnidir DLT of the frame.
-    Median-free: `steps` frames timed back to back after 2 warm-ups (frames resident in HBM)."""
+    """BASELINE config 5 on one GPU: per frame, the Swin-S Mask R-CNN detector on all 8 views
+    (1536x2048), the 4 best detections of every view as crop boxes, ViTPose flip test + UDP decode on
+    those 32 crops, omnidir DLT of the frame; then (host) one BoT-SORT update per view on those
+    detections and the ResNet-152 ID classifier on the 32 tracked boxes.  With random weights the
+    detector scores sit near 0.5, so the trackers run with thresholds 0 (every detection tracked).
+    `steps` frames timed back to back after 2 warm-ups (frames resident in HBM)."""
+    import numpy as np
     import torch
     from mqhip import _lib
     from mqhip.detector import SwinDetectorHip, make_random_weights
+    from mqhip.resnet_id import ResNetIdHip, make_random_weights as id_weights, patch_bounds
+    from mqhip.tracker import BOTSORT_CFG, BotSort
     det = SwinDetectorHip(make_random_weights(seed=0), device=device)
+    idm = ResNetIdHip(id_weights(152, seed=0), depth=152, device=device)
+    trk_cfg = dict(BOTSORT_CFG, track_high_thresh=0.0, track_low_thresh=0.0, new_track_thresh=0.0)
+    trackers = [BotSort(**trk_cfg) for _ in range(N_VIEWS)]
     lib, ctx = pose_model.lib, pose_model.ctx
     dev = torch.device("cuda", device)
     cfg = pose_model.cfg
@@ -307,9 +337,23 @@ def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
     box_frame = torch.arange(n, device=dev, dtype=torch.int32) // N_ANIMALS
     s_ptr = _lib.stream_ptr(dev)
 
+    def track_and_id(fr, boxes, scores):
+        hb = boxes[:, :N_ANIMALS].double().cpu().numpy()
+        hs = scores[:, :N_ANIMALS].double().cpu().numpy()
+        rows = []
+        for v in range(N_VIEWS):
+            for r in trackers[v].update(np.hstack([hb[v], hs[v][:, None], np.zeros((N_ANIMALS, 1))]), None):
+                pb = patch_bounds((IMG_H, IMG_W), r[:4])
+                if pb is not None:
+                    rows.append((v, pb[2], pb[0], pb[3], pb[1]))
+        if rows:
+            x, _ = idm.preprocess(fr, rows)
+            idm.forward(x)
+        return len(rows)
+
     def one(i):
         fr = frames[i % frames.shape[0]]
-        boxes, _, _ = det.forward(fr)
+        boxes, scores, _ = det.forward(fr)
         bx = boxes[:, :N_ANIMALS].reshape(-1, 4).contiguous()  # detections are score-ordered
         _lib.check(lib.mq_crop_udp(ctx.handle, _lib.ptr(fr), IMG_H * IMG_W * 3, IMG_H, IMG_W, _lib.ptr(bx),
                                    _lib.ptr(box_frame), n, _lib.ptr(crops), _lib.ptr(center), _lib.ptr(scale),
@@ -322,7 +366,9 @@ def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
         pts = pts.view(N_VIEWS, N_ANIMALS * cfg.n_joints, 2).contiguous()
         _lib.check(lib.mq_triangulate_dlt(ctx.handle, _lib.ptr(cams_dev), N_VIEWS, _lib.ptr(pts),
                                           N_ANIMALS * cfg.n_joints, 1, _lib.ptr(p3d), s_ptr), "dlt")
+        return track_and_id(fr, boxes, scores)
 
+    id_rows = [(v, 100 + 300 * a, 200, 400 + 300 * a, 700) for v in range(N_VIEWS) for a in range(N_ANIMALS)]
     for i in range(2):
         one(i)
     torch.cuda.synchronize(dev)
@@ -333,16 +379,25 @@ def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
     det_ms = (time.perf_counter() - t0) * 1e3 / steps
     t0 = time.perf_counter()
     for i in range(steps):
-        one(i)
+        x, _ = idm.preprocess(frames[i % frames.shape[0]], id_rows)
+        idm.forward(x)
+    torch.cuda.synchronize(dev)
+    id_ms = (time.perf_counter() - t0) * 1e3 / steps
+    t0 = time.perf_counter()
+    n_id = 0
+    for i in range(steps):
+        n_id += one(i)
     torch.cuda.synchronize(dev)
     ms = (time.perf_counter() - t0) * 1e3 / steps
-    log(f"config 5: detector {det_ms:.2f} ms / frame, detector + pose + DLT {ms:.2f} ms / frame")
-    return {"workload": "BASELINE config 5 per GPU without tracker / ID classifier: Swin-S Mask R-CNN on 8 views "
-                        "1536x2048 -> 4 best detections per view -> ViTPose-%s flip test + UDP decode (32 crops) "
-                        "-> omnidir DLT" % cfg.name,
+    log(f"config 5: detector {det_ms:.2f} ms, ID (32 boxes) {id_ms:.2f} ms, whole frame {ms:.2f} ms / frame")
+    return {"workload": "BASELINE config 5 per GPU: Swin-S Mask R-CNN on 8 views 1536x2048 -> 4 best detections "
+                        "per view -> ViTPose-%s flip test + UDP decode (32 crops) -> omnidir DLT; BoT-SORT per view "
+                        "(host) -> ResNet-152 ID on the tracked boxes" % cfg.name,
             "ms_per_frame": round(ms, 3), "detector_ms_per_frame": round(det_ms, 3),
+            "id_classifier_ms_per_frame": round(id_ms, 3), "id_boxes_per_frame": round(n_id / steps, 1),
             "individuals_frames_per_s": round(N_ANIMALS / (ms * 1e-3), 2), "frames_timed": steps,
-            "data": "random detector and pose weights, random frames (the detector returns 100 boxes per view)"}
+            "data": "random detector, pose and ID weights, random frames (the detector returns 100 boxes per view; "
+                    "trackers at thresholds 0)"}
 
 
 def main():
