@@ -346,31 +346,36 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
   if (wave >= ntb) return;
   const bool has1 = (TT == MAXT) ? true : (wave + ATT_WAVES < ntb);
 
+  // Per query block u: QK(u) -> softmax(u) -> PV(u).  They are issued software-pipelined over the
+  // two blocks -- QK(0); QK(1) with softmax(0); PV(0) with softmax(1); PV(1) -- so that one block's
+  // VALU softmax can fill the MFMA shadow of the other block's matrix products inside the same wave
+  // (an MFMA occupies the matrix pipe for 16 cycles, in which the wave can issue about four
+  // independent VALU instructions).  K / V fragments are read from LDS once per block.  Per value, the arithmetic and its order are those of the unpipelined form.
   f32x4 S[2][MAXT / 16];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb) S[u][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // one k-step's K fragments are all read before its MFMAs, so the reads overlap each other and the
+  // matrix products instead of each MFMA waiting on its own read
+  auto qk = [&](int u) {
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    const int chunk = (HALF && ks == NKS - 1) ? 4 * ks + (g & 1) : 4 * ks + g;
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int chunk = (HALF && ks == NKS - 1) ? 4 * ks + (g & 1) : 4 * ks + g;
+      bf16x8 kf[MAXT / 16];
 #pragma unroll
-    for (int tb = 0; tb < MAXT / 16; ++tb) {
-      if (tb < ntb) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kimg + (tb * 16 + l16) * (KCH * 16) + chunk * 16);
-        S[0][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[0][ks], S[0][tb], 0, 0, 0);
-        if (has1) S[1][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[1][ks], S[1][tb], 0, 0, 0);
-      }
+      for (int tb = 0; tb < MAXT / 16; ++tb)
+        if (tb < ntb) kf[tb] = *reinterpret_cast<const bf16x8*>(Kimg + (tb * 16 + l16) * (KCH * 16) + chunk * 16);
+#pragma unroll
+      for (int tb = 0; tb < MAXT / 16; ++tb)
+        if (tb < ntb) S[u][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[tb], qf[u][ks], S[u][tb], 0, 0, 0);
     }
-  }
+  };
   // softmax over the tokens of query l16: registers hold tokens tb*16 + 4 g + e.  The row max and
-  // sum run as four independent chains (one per register e) so the dependent-latency chain is
-  // ntb deep instead of 4 ntb; the two query blocks interleave.
+  // sum run as independent chains so the dependent-latency chain is ntb deep instead of 4 ntb.
   bf16x8 P[2][MAXT / 32];
   float linv[2];
-  float mb[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  auto softmax = [&](int u) {
     float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
     for (int tb = 0; tb + 1 < MAXT / 16; tb += 2)
@@ -384,23 +389,24 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
     float m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
-    mb[u] = m * scale_log2;
-  }
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    float l4[4] = {0.f, 0.f, 0.f, 0.f};
+    const float mbu = m * scale_log2;
+    // exponent arguments and the running sums on float pairs (v_pk_fma_f32 / v_pk_add_f32)
+    const f32x2 sc2 = {scale_log2, scale_log2}, mb2 = {mbu, mbu};
+    f32x2 l2[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb) {
       if (tb < ntb) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float pv = __builtin_amdgcn_exp2f(S[u][tb][e] * scale_log2 - mb[u]);
-          S[u][tb][e] = pv;
-          l4[e] += pv;
+        for (int h = 0; h < 2; ++h) {
+          const f32x2 arg = (f32x2){S[u][tb][2 * h], S[u][tb][2 * h + 1]} * sc2 - mb2;
+          const f32x2 pv = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+          S[u][tb][2 * h] = pv.x;
+          S[u][tb][2 * h + 1] = pv.y;
+          l2[h] += pv;
         }
       }
     }
-    float ls = (l4[0] + l4[1]) + (l4[2] + l4[3]);
+    float ls = (l2[0].x + l2[1].x) + (l2[0].y + l2[1].y);
     ls += __shfl_xor(ls, 16, 64);
     ls += __shfl_xor(ls, 32, 64);
     linv[u] = 1.0f / ls;
@@ -413,8 +419,7 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
         P[u][kst][4 + e] = (__bf16)S[u][2 * kst + 1][e];
       }
     }
-  }
-
+  };
   f32x4 O[2][NDT];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
@@ -423,26 +428,43 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
   // V^T (A operand, row = d, k = the token order of P): transposed read, lane 4q+p of each 16-lane
   // group addresses token row r0+q, columns c0+4p..+3 and receives column c0 + (lane & 15)
   const int trq = l16 >> 2, trp = l16 & 3;
+  auto pv = [&](int u) {
 #pragma unroll
-  for (int kst = 0; kst < MAXT / 32; ++kst) {
-    if (kst < T / 32) {
+    for (int kst = 0; kst < MAXT / 32; ++kst) {
+      if (kst < T / 32) {
+        bf16x8 vb[NDT];
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const int ra = 2 * kst * 16 + 4 * g + trq;
-        const char* pa = Vimg + ra * (L::VCH * 16) + (dt * 16 + 4 * trp) * 2;
-        const short4v v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa));
-        const short4v v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa + 16 * (L::VCH * 16)));
-        bf16x8 vb;
-        const short4v* pv0 = &v0;
-        const short4v* pv1 = &v1;
-        __builtin_memcpy(&vb, pv0, 8);
-        __builtin_memcpy(reinterpret_cast<char*>(&vb) + 8, pv1, 8);
-        O[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb, P[0][kst], O[0][dt], 0, 0, 0);
-        if (has1) O[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb, P[1][kst], O[1][dt], 0, 0, 0);
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int ra = 2 * kst * 16 + 4 * g + trq;
+          const char* pa = Vimg + ra * (L::VCH * 16) + (dt * 16 + 4 * trp) * 2;
+          const short4v v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa));
+          const short4v v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa + 16 * (L::VCH * 16)));
+          const short4v* pv0 = &v0;
+          const short4v* pv1 = &v1;
+          __builtin_memcpy(&vb[dt], pv0, 8);
+          __builtin_memcpy(reinterpret_cast<char*>(&vb[dt]) + 8, pv1, 8);
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt)
+          O[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb[dt], P[u][kst], O[u][dt], 0, 0, 0);
       }
     }
+  };
+  qk(0);
+  if (has1) {
+    __builtin_amdgcn_sched_barrier(0);
+    qk(1);
+    softmax(0);
+    __builtin_amdgcn_sched_barrier(0);
+    pv(0);
+    softmax(1);
+    __builtin_amdgcn_sched_barrier(0);
+    pv(1);
+  } else {
+    softmax(0);
+    pv(0);
   }
   // O^T C-layout: column = query l16, rows 4 g + e = d within the 16-block dt.  Pairs (dt, dt+1):
   // after v_permlane16_swap even groups hold d 16 dt + 4 g + 0..7, odd groups 16 (dt+1) + 4 (g-1) + 0..7.
@@ -453,13 +475,16 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
     const int q = (wave + u * ATT_WAVES) * 16 + l16;
     bf16_t* orow = out + (row0 + q) * D + h * DH;
     const float inv = linv[u];
+    const f32x2 inv2 = {inv, inv};
 #pragma unroll
     for (int dp = 0; dp + 1 < NDT; dp += 2) {
       unsigned pk[2][2];
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
-        pk[hh][0] = pack_bf16x2(O[u][dp + hh][0] * inv, O[u][dp + hh][1] * inv);
-        pk[hh][1] = pack_bf16x2(O[u][dp + hh][2] * inv, O[u][dp + hh][3] * inv);
+        const f32x2 a = (f32x2){O[u][dp + hh][0], O[u][dp + hh][1]} * inv2;
+        const f32x2 b = (f32x2){O[u][dp + hh][2], O[u][dp + hh][3]} * inv2;
+        pk[hh][0] = pack_bf16x2(a.x, a.y);
+        pk[hh][1] = pack_bf16x2(b.x, b.y);
       }
       const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);

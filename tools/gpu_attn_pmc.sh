@@ -13,7 +13,7 @@ import csv, glob
 from collections import defaultdict
 vals = defaultdict(list)
 for f in sorted(glob.glob("gpurun_out/apmc/p*/run_counter_collection.csv")):
-    rows = [r for r in csv.DictReader(open(f)) if "attention_kernel<80, 0, 192>" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(f)) if "attention2_kernel<80, 192>" in r["Kernel_Name"]]
     for r in rows:
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, v in sorted(vals.items()):
