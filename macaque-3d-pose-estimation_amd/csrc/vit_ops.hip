@@ -376,29 +376,33 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
   bf16x8 P[2][MAXT / 32];
   float linv[2];
   auto softmax = [&](int u) {
+    // row max: 3-input maxes (v_max3_f32 issued directly: a plain fmaxf in IEEE mode makes the compiler
+    // canonicalise both operands first, three instructions per pair), four independent chains
     float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
     for (int tb = 0; tb + 1 < MAXT / 16; tb += 2)
       if (tb + 1 < ntb) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m4[e] = fmaxf(m4[e], fmaxf(S[u][tb][e], S[u][tb + 1][e]));
+        for (int e = 0; e < 4; ++e) m4[e] = max3_f32(m4[e], S[u][tb][e], S[u][tb + 1][e]);
       } else if (tb < ntb) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m4[e] = fmaxf(m4[e], S[u][tb][e]);
+        for (int e = 0; e < 4; ++e) m4[e] = max3_f32(m4[e], S[u][tb][e], S[u][tb][e]);
       }
-    float m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float m = max3_f32(m4[0], m4[1], max3_f32(m4[2], m4[3], m4[3]));
+    // the query's other tokens live in lane groups g ^ 1, g ^ 2: butterflies by permlane swaps (VALU,
+    // no LDS round trip as with ds_bpermute)
+    m = bfly16_max(m);
+    m = bfly32_max(m);
     const float mbu = m * scale_log2;
-    // exponent arguments and the running sums on float pairs (v_pk_fma_f32 / v_pk_add_f32)
-    const f32x2 sc2 = {scale_log2, scale_log2}, mb2 = {mbu, mbu};
+    // exponent arguments (one packed fma per pair) and the running sums on float pairs
+    const f32x2 sc2 = {scale_log2, scale_log2}, mb2 = {-mbu, -mbu};
     f32x2 l2[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb) {
       if (tb < ntb) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const f32x2 arg = (f32x2){S[u][tb][2 * h], S[u][tb][2 * h + 1]} * sc2 - mb2;
+          const f32x2 arg = __builtin_elementwise_fma((f32x2){S[u][tb][2 * h], S[u][tb][2 * h + 1]}, sc2, mb2);
           const f32x2 pv = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
           S[u][tb][2 * h] = pv.x;
           S[u][tb][2 * h + 1] = pv.y;
@@ -407,8 +411,8 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
       }
     }
     float ls = (l2[0].x + l2[1].x) + (l2[0].y + l2[1].y);
-    ls += __shfl_xor(ls, 16, 64);
-    ls += __shfl_xor(ls, 32, 64);
+    ls = bfly16_sum(ls);
+    ls = bfly32_sum(ls);
     linv[u] = 1.0f / ls;
     // B operand of P^T: element j of lane group g = token 32 kst + 16 (j >> 2) + 4 g + (j & 3)
 #pragma unroll
