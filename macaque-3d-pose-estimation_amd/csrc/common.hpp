@@ -55,14 +55,6 @@ __device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
   return pos - h;
 }
 
-// v_max3_f32 issued directly: fmaxf in the default IEEE mode canonicalises both operands first
-// (v_max_f32 x, x), three instructions per pair instead of half of one
-__device__ __forceinline__ float max3_f32(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
 // Butterflies across the 16-lane rows of a wave by v_permlane16_swap / v_permlane32_swap (VALU, no
 // LDS round trip as with ds_bpermute).  With both operands x, permlane16_swap returns
 // {x of rows 0,0,2,2 ; x of rows 1,1,3,3}, permlane32_swap {x of lanes 0-31 twice ; of 32-63 twice},
@@ -70,11 +62,11 @@ __device__ __forceinline__ float max3_f32(float a, float b, float c) {
 // equal those of a __shfl_xor butterfly bit for bit.
 __device__ __forceinline__ float bfly16_max(float x) {
   const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return max3_f32(__uint_as_float(p[0]), __uint_as_float(p[1]), __uint_as_float(p[1]));
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
 }
 __device__ __forceinline__ float bfly32_max(float x) {
   const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return max3_f32(__uint_as_float(p[0]), __uint_as_float(p[1]), __uint_as_float(p[1]));
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
 }
 __device__ __forceinline__ float bfly16_sum(float x) {
   const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);

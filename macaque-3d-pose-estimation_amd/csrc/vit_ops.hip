@@ -285,7 +285,7 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t*
 constexpr int ATT2_KCH = 10;  // K image row stride in 16-B chunks (DH <= 80)
 
 template <int DH, int TT = 0>
-__global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t* __restrict__ qkv,
                                                                      bf16_t* __restrict__ out, int T_rt, int D,
                                                                      int H, float scale_log2) {
   using L = AttLayout<DH>;
@@ -376,19 +376,18 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
   bf16x8 P[2][MAXT / 32];
   float linv[2];
   auto softmax = [&](int u) {
-    // row max: 3-input maxes (v_max3_f32 issued directly: a plain fmaxf in IEEE mode makes the compiler
-    // canonicalise both operands first, three instructions per pair), four independent chains
+    // row max: four independent chains
     float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
     for (int tb = 0; tb + 1 < MAXT / 16; tb += 2)
       if (tb + 1 < ntb) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m4[e] = max3_f32(m4[e], S[u][tb][e], S[u][tb + 1][e]);
+        for (int e = 0; e < 4; ++e) m4[e] = fmaxf(m4[e], fmaxf(S[u][tb][e], S[u][tb + 1][e]));
       } else if (tb < ntb) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m4[e] = max3_f32(m4[e], S[u][tb][e], S[u][tb][e]);
+        for (int e = 0; e < 4; ++e) m4[e] = fmaxf(m4[e], S[u][tb][e]);
       }
-    float m = max3_f32(m4[0], m4[1], max3_f32(m4[2], m4[3], m4[3]));
+    float m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
     // the query's other tokens live in lane groups g ^ 1, g ^ 2: butterflies by permlane swaps (VALU,
     // no LDS round trip as with ds_bpermute)
     m = bfly16_max(m);
@@ -457,18 +456,13 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention2_kernel(const bf16_t
     }
   };
   qk(0);
+  softmax(0);
+  pv(0);
   if (has1) {
     __builtin_amdgcn_sched_barrier(0);
     qk(1);
-    softmax(0);
-    __builtin_amdgcn_sched_barrier(0);
-    pv(0);
     softmax(1);
-    __builtin_amdgcn_sched_barrier(0);
     pv(1);
-  } else {
-    softmax(0);
-    pv(0);
   }
   // O^T C-layout: column = query l16, rows 4 g + e = d within the 16-block dt.  Pairs (dt, dt+1):
   // after v_permlane16_swap even groups hold d 16 dt + 4 g + 0..7, odd groups 16 (dt+1) + 4 (g-1) + 0..7.
