@@ -1,0 +1,91 @@
+"""A/B two builds of libmq_hip.so in ONE process (box-to-box clock spread is ~8 %, so A/B numbers
+are only taken side by side): time mq_gemm_bf16 on the ViT-H GEMM shapes (and optionally the
+attention) through each library, alternating, with hipEvents on the launch stream, and check that the
+two give bit-identical outputs.
+
+python tools/ab_gemm.py --a macaque-3d-pose-estimation_amd/lib_prev/libmq_hip.so \
+                        --b macaque-3d-pose-estimation_amd/lib/libmq_hip.so [--shape fc1,fc2] [--iters 20]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "macaque-3d-pose-estimation_amd"))
+from gemm_probe import SHAPES  # noqa: E402  (same shape table)
+
+
+def open_lib(path):
+    lib = C.CDLL(os.path.abspath(path))  # RTLD_LOCAL: the two builds keep their own symbols
+    vp, i32 = C.c_void_p, C.c_int
+    lib.mq_create.argtypes = [i32, C.POINTER(vp)]
+    lib.mq_gemm_bf16.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]
+    lib.mq_attention_bf16.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp]
+    ctx = vp()
+    assert lib.mq_create(0, C.byref(ctx)) == 0
+    return lib, ctx
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--a", required=True)
+    ap.add_argument("--b", required=True)
+    ap.add_argument("--shape", default="qkv,proj,fc1,fc2,dc1,dc2")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--attention", action="store_true")
+    args = ap.parse_args()
+    import torch
+    libs = {"A": open_lib(args.a), "B": open_lib(args.b)}
+    dev = torch.device("cuda", 0)
+    s = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    g = torch.Generator(device=dev)
+    g.manual_seed(0)
+    for name in args.shape.split(","):
+        M, N, K, epi = SHAPES[name]
+        a = torch.randn((M, K), generator=g, device=dev).to(torch.bfloat16)
+        w = (torch.randn((N, K), generator=g, device=dev) / K ** 0.5).to(torch.bfloat16)
+        bias = torch.randn((N,), generator=g, device=dev)
+        f32 = epi in (2, 3, 4, 5)
+        c0 = torch.randn((M, N), generator=g, device=dev)
+        outs = {}
+        for rnd in range(args.rounds):
+            for key, (lib, ctx) in libs.items():
+                c = c0.clone() if f32 else torch.empty((M, N), device=dev, dtype=torch.bfloat16)
+                run = lambda: lib.mq_gemm_bf16(ctx, P(a), P(w), P(c), P(bias), None, M, N, K, K, K, N, 0, epi, s)  # noqa
+                assert run() == 0
+                torch.cuda.synchronize()
+                if rnd == 0:
+                    outs[key] = c.clone()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    run()
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) / args.iters * 1e3
+                print(f"{name} {key} r={rnd}: {us:.1f} us  {2 * M * N * K / (us * 1e-6) / 1e12:.0f} TFLOP/s", flush=True)
+        print(f"{name}: A and B bit-identical = {bool(torch.equal(outs['A'], outs['B']))}", flush=True)
+    if args.attention:
+        n, T, D, H = 64, 192, 1280, 16
+        qkv = torch.randn((n * T, 3 * D), generator=g, device=dev).to(torch.bfloat16)
+        for rnd in range(args.rounds):
+            for key, (lib, ctx) in libs.items():
+                out = torch.empty((n * T, D), device=dev, dtype=torch.bfloat16)
+                for _ in range(3):
+                    lib.mq_attention_bf16(ctx, P(qkv), P(out), n, T, D, H, s)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    lib.mq_attention_bf16(ctx, P(qkv), P(out), n, T, D, H, s)
+                e1.record()
+                torch.cuda.synchronize()
+                print(f"attention {key} r={rnd}: {e0.elapsed_time(e1) / args.iters * 1e3:.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    main()
