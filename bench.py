@@ -83,14 +83,16 @@ def cpu_info():
 
 
 def _median_time(fn, reps):
+    """Median wall time of `reps` calls after a warm-up, and the last call's result."""
     import numpy as np
     fn()  # warm-up
     ts = []
+    out = None
     for _ in range(reps):
         t0 = time.perf_counter()
-        fn()
+        out = fn()
         ts.append(time.perf_counter() - t0)
-    return float(np.median(ts)), ts
+    return float(np.median(ts)), out
 
 
 def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
@@ -131,15 +133,18 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
             decode_batch(hm.numpy(), c, s)
             return hm
 
-        t_vit, _ = _median_time(run, reps)
+        t_vit, hm = _median_time(run, reps)
         t_tri, _ = _median_time(lambda: gv.triangulate(p), reps)
         log(f"cpu baseline: ViT-{cfg.name} {n_crops} crops {t_vit:.3f} s (median of {reps})")
+        sample[cfg.name] = (w, x, hm)
         return t_vit, t_tri
 
+    sample = {}
     crops = N_VIEWS * N_ANIMALS
     t2, tri2 = frame_pass(CONFIGS["huge"], n_crops_sample, N_VIEWS)
     t_frame2 = t2 * crops / n_crops_sample + tri2
     t1, tri1 = frame_pass(CONFIGS["base"], 4, 4)
+    parity = parity_check(*sample["huge"], CONFIGS["huge"], crops)
     lift = lift_cpu(cams_np)
     log(f"cpu baseline: config-4 lift {lift['total_s']:.1f} s")
     det = detector_cpu(reps=min(reps, 3))
@@ -154,7 +159,31 @@ def cpu_baseline(cams_np, n_crops_sample=8, reps=5):
             "config1": {"seconds_per_frame": round(t1 + tri1, 4), "individuals_frames_per_s": round(1.0 / (t1 + tri1), 4),
                         "sample": "ViT-B fp32 flip-test forward + decode of 4 crops (4 views x 1 individual) + DLT"},
             "config4_lift": lift,
-            "config5_detector": det, "config5_id": idc}
+            "config5_detector": det, "config5_id": idc, "parity_check": parity}
+
+
+def parity_check(w, x, hm_cpu, cfg, batch):
+    """The CPU sample's fp32 oracle heatmaps against the GPU path at the bench's batch size: a
+    `batch`-crop forward (bf16 MFMA, flip test) whose first crops are the CPU sample's crops, with the
+    same weights.  Tolerance per crop: max|dH| <= 2e-2 * max|H| (tests/test_gpu_pose.py)."""
+    import torch
+    from mqhip.pose import VitPoseHip
+    dev = torch.device("cuda", 0)
+    model = VitPoseHip(cfg, {k: v.to(dev) for k, v in w.items()}, device=0, graph=False)
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    xb = torch.randn((batch, 3, 256, 192), generator=g, device=dev)
+    xb[:x.shape[0]] = x.to(dev)
+    got = model.forward(xb, flip_test=True)[:x.shape[0]].float().cpu()
+    del model
+    torch.cuda.empty_cache()
+    ref = hm_cpu.float()
+    rel = [float((got[i] - ref[i]).abs().max() / ref[i].abs().max()) for i in range(ref.shape[0])]
+    am_equal = float((got.flatten(2).argmax(-1) == ref.flatten(2).argmax(-1)).float().mean())
+    return {"crops_checked": ref.shape[0], "gpu_batch": batch, "max_rel_err": round(max(rel), 5), "tol": 2e-2,
+            "pass": max(rel) <= 2e-2, "argmax_agreement": round(am_equal, 4),
+            "what": "fp32 CPU oracle heatmaps (the cpu_baseline sample) vs the GPU flip-test forward of a "
+                    f"{batch}-crop batch holding those crops, same weights"}
 
 
 def detector_cpu(reps=3):
