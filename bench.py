@@ -449,11 +449,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the multi-rank path on a one-GPU box (never set by the driver): MQ_BENCH_SHARE_GPU=1
+    # puts every rank on device LOCAL_RANK % device_count and MQ_BENCH_BACKEND=gloo exchanges the
+    # keypoints and timings through host tensors (RCCL refuses two ranks on one GPU).
+    backend = os.environ.get("MQ_BENCH_BACKEND", "nccl")
+    if os.environ.get("MQ_BENCH_SHARE_GPU") == "1":
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    xdev = dev if backend == "nccl" else torch.device("cpu")  # where collective tensors live
 
     from mqhip import _lib, synth
     from mqhip.geometry import CameraGroup
@@ -536,7 +546,7 @@ def main():
     if world > 1:
         # the one exchange step: every rank's per-view 2D keypoints, in frame order (mqhip.shard)
         per_frame = kp_log.view(args.steps, FPS, N_VIEWS, N_ANIMALS, cfg.n_joints, 3).flatten(0, 1)
-        gathered = gather_keypoints(per_frame, world * args.steps * FPS, world)
+        gathered = gather_keypoints(per_frame.to(xdev), world * args.steps * FPS, world)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -545,7 +555,7 @@ def main():
     if timing:
         _lib.check(lib.mq_vitpose_timing(model.handle, 0), "timing")
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=xdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
