@@ -160,6 +160,17 @@ int mq_upsample_add(mq_ctx* ctx, float* lo, const float* hi, int n_img, int lo_h
 /* 3x3 / stride 1 / pad 1 im2col: x f32 NHWC -> out bf16 (n_img * h * w, 9 * ch), k = (ky * 3 + kx) * ch + c. */
 int mq_im2col3x3(mq_ctx* ctx, const float* x, int n_img, int height, int width, int ch, uint16_t* out, void* stream);
 
+/* 3x3 / stride 1 / pad 1 convolution as an implicit GEMM (no im2col buffer): x bf16 NHWC (n_img, h, w, ch),
+ * ch % 64 == 0; w bf16 (cout, 9 * ch) with k = (ky * 3 + kx) * ch + c (the mq_im2col3x3 order); out
+ * (n_img * h * w, ldc) with epilogue 0 (bf16), 4 (f32) or 6 (ReLU bf16) of mq_gemm_bf16, plus bias.
+ * Same bits as mq_im2col3x3 + mq_gemm_bf16 on the bf16-rounded input.  Replaces the detector's FPN output
+ * convolutions (neck, SWIN-Mask_R-CNN_bbox_only.py:80-89) and the RPN head convolution (rpn_head, :137). */
+int mq_conv3x3_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch, const uint16_t* w,
+                    const float* bias, void* out, int cout, int ldc, int epilogue, void* stream);
+
+/* float32 -> bfloat16, round to nearest even (count elements). */
+int mq_f32_to_bf16(mq_ctx* ctx, const float* src, uint16_t* dst, int64_t count, void* stream);
+
 /* max_pool2d(kernel 1, stride 2) = every other pixel: x f32 NHWC -> out (n_img, ceil(h/2), ceil(w/2), ch). */
 int mq_subsample2(mq_ctx* ctx, const float* x, int n_img, int height, int width, int ch, float* out, void* stream);
 

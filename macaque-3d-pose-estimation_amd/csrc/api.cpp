@@ -664,6 +664,30 @@ int mq_gemm_bf16(mq_ctx* ctx, const void* A, const void* W, void* C, const float
   return 0;
 }
 
+int mq_conv3x3_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch, const uint16_t* w,
+                    const float* bias, void* out, int cout, int ldc, int epilogue, void* stream) {
+  if (!ctx || !x || !w || !out) return fail("mq_conv3x3_bf16: null argument");
+  if (n_img <= 0 || height <= 0 || width <= 0 || cout <= 0 || ch <= 0 || ch % 64 || ldc < cout)
+    return fail("mq_conv3x3_bf16: bad sizes (ch must be a multiple of 64)", -2);
+  if (epilogue != mq::EPI_BF16 && epilogue != mq::EPI_F32 && epilogue != mq::EPI_RELU_BF16)
+    return fail("mq_conv3x3_bf16: epilogue must be 0 (bf16), 4 (f32) or 6 (ReLU bf16)", -2);
+  HIP_TRY(hipSetDevice(ctx->device));
+  mq::GemmArgs g{(const unsigned short*)x, (const unsigned short*)w, out, bias, nullptr, n_img * height * width, cout,
+                 9 * ch, ch, 9 * ch, ldc, 0};
+  g.conv_h = height;
+  g.conv_w = width;
+  g.conv_c = ch;
+  if (mq::conv3x3_bf16(g, epilogue, (hipStream_t)stream)) return fail("mq_conv3x3_bf16: launch failed", -6);
+  return 0;
+}
+
+int mq_f32_to_bf16(mq_ctx* ctx, const float* src, uint16_t* dst, int64_t count, void* stream) {
+  if (!ctx || !src || !dst || count < 0) return fail("mq_f32_to_bf16: bad argument");
+  HIP_TRY(hipSetDevice(ctx->device));
+  K_TRY(mq::convert_f32_bf16(src, dst, count, (hipStream_t)stream));
+  return 0;
+}
+
 // ----------------------------------------------------------------------------- detector
 static int check_det(mq_ctx* ctx) {
   if (!ctx) return fail("null ctx");

@@ -564,6 +564,16 @@ static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
+int conv3x3_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
+  if (!g_num_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
+      g_num_cus = 256;
+  }
+  return gemm_pingpong_conv(p, epi, g_num_cus, stream);
+}
+
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return -1;
   if ((p.lda % 8) || (p.ldw % 8)) return -2;

@@ -218,7 +218,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
   }
 }
 
-template <int EPI>
+template <int EPI, bool CONV = false>
 __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -255,6 +255,9 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   // keeps every wait count uniform.
   int iss_t = 0, iss_k = 0;
   unsigned voff[8];
+  // implicit convolution: per A slot the output pixel's (y, x) (packed y << 16 | x); voff then holds the
+  // element offset of the tap-centre row + this lane's chunk, and the tap shift is added at issue time
+  unsigned cyx[8];
   auto set_tile_ptrs = [&](int ti) {
     int m0, n0;
     pp_tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
@@ -262,17 +265,37 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     for (int i = 0; i < 8; ++i) {
       const int row = pp_group_row(wave, i) + (lane >> 3);
       const int chunk = (lane & 7) ^ pp_swz(row);
-      if (pp_slot_is_w(i))
+      if (pp_slot_is_w(i)) {
         voff[i] = (unsigned)(((size_t)min(n0 + row, p.N - 1) * p.ldw + chunk * 8) * 2);
-      else
+      } else if constexpr (CONV) {
+        const int pix = min(m0 + row, p.M - 1);
+        const int hw = p.conv_h * p.conv_w;
+        const int rem = pix - (pix / hw) * hw;
+        const int y = rem / p.conv_w;
+        cyx[i] = ((unsigned)y << 16) | (unsigned)(rem - y * p.conv_w);
+        voff[i] = (unsigned)((size_t)pix * p.conv_c + chunk * 8);
+      } else {
         voff[i] = (unsigned)(((size_t)min(m0 + row, p.M - 1) * p.lda + chunk * 8) * 2);
+      }
     }
   };
   set_tile_ptrs(0);
   auto issue = [&](int i, int slot) {
     char* dst = smem + slot * PP_STAGE + (pp_slot_is_w(i) ? PP_OP : 0) + pp_group_row(wave, i) * 128;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(pp_slot_is_w(i) ? rsW : rsA, MQ_LDS_LOCAL(dst), 16, voff[i],
-                                             iss_k * PP_BK * 2, 0, 0);
+    if (CONV && !pp_slot_is_w(i)) {
+      // K-step iss_k = tap * (C / 64) + c64: the tap's shifted pixel, channels 64 c64 .. + 63; a pixel
+      // outside the image gets an offset past the buffer end, which the DMA turns into zeros (padding)
+      const int kpt = p.conv_c >> 6;
+      const int tap = iss_k / kpt;
+      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+      const int y = (int)(cyx[i] >> 16) + dy, x = (int)(cyx[i] & 0xffffu) + dx;
+      const bool inside = (unsigned)y < (unsigned)p.conv_h && (unsigned)x < (unsigned)p.conv_w;
+      const unsigned off = (unsigned)((int)voff[i] + (dy * p.conv_w + dx) * p.conv_c + (iss_k - tap * kpt) * 64);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(dst), 16, inside ? off * 2 : 0x80000000u, 0, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(pp_slot_is_w(i) ? rsW : rsA, MQ_LDS_LOCAL(dst), 16, voff[i],
+                                               iss_k * PP_BK * 2, 0, 0);
+    }
   };
   auto advance = [&]() {
     if (iss_k + 1 < nk) {
@@ -401,17 +424,40 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-template <int EPI>
+template <int EPI, bool CONV = false>
 void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              PP_LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, CONV>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
 }
 
 }  // namespace
+
+// Implicit-GEMM 3x3 convolution: the ping-pong GEMM with the A tile rows of every K-step gathered from
+// the tap's shifted input pixels (replaces an im2col buffer of 9x the input: the FPN / RPN convolutions
+// of the detector).  Same accumulation order as im2col + GEMM, so both give the same bits.
+int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
+  if (p.conv_c <= 0 || p.conv_c % PP_BK || p.K != 9 * p.conv_c || p.lda != p.conv_c || p.conv_h <= 0 ||
+      p.conv_w <= 0 || p.M % (p.conv_h * p.conv_w) || p.conv_w >= 65536 || p.conv_h >= 65536 ||
+      (size_t)p.M * p.lda * 2 >= (1ull << 31) || (size_t)p.N * p.ldw * 2 >= (1ull << 31))
+    return -1;
+  // the epilogue stores 8 bf16 / 4 f32 columns per lane: whole groups only
+  if (epi == EPI_F32 ? (p.N % 4 || p.ldc % 4) : (p.N % 8 || p.ldc % 8)) return -2;
+  const int tiles_m = (p.M + PP_BM - 1) / PP_BM, tiles_n = (p.N + PP_BN - 1) / PP_BN;
+  const int tiles = tiles_m * tiles_n;
+  dim3 grid(tiles < num_cus ? tiles : num_cus);
+  switch (epi) {
+    case EPI_BF16: launch_pp<EPI_BF16, true>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, true>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_F32: launch_pp<EPI_F32, true>(grid, stream, p, tiles_m, tiles_n); break;
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
 
 // Routing: every 256x256 GEMM with K % 64 == 0, except the f32 residual read-modify-write at short
 // K (proj, K = 1280: one tile per CU, 20 K-steps), which goes to the interleaved kernel: it measured

@@ -24,15 +24,22 @@ struct GemmArgs {
   int M, N, K;
   int lda, ldw, ldc;
   int aux_rows;
+  // implicit 3x3 / stride 1 / pad 1 convolution (conv_c > 0): A is the NHWC input, M = n * conv_h * conv_w
+  // output pixels, lda = conv_c channels, K = 9 * conv_c in (ky * 3 + kx) * conv_c + c order; the A tile
+  // rows of each K-step are gathered from the tap's shifted pixels (zeros outside the image)
+  int conv_h = 0, conv_w = 0, conv_c = 0;
 };
 
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
+// implicit-GEMM 3x3 convolution (ping-pong kernel only; conv_c % 64 == 0)
+int conv3x3_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 // routing knobs (mq_set_tuning): both settings give correct results
 extern bool g_gemm_force_small;  // every GEMM on the 128x128 kernel
 // ping-pong 256x256 kernel (gemm_pp.hip): the two wave groups of a block alternate LDS traffic and MFMA
 extern int g_gemm_pingpong;
 bool gemm_pingpong_fits(const GemmArgs& p, int epi);
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
+int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,

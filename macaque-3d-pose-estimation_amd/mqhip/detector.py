@@ -127,6 +127,7 @@ class SwinDetectorHip:
         self.cfg = cfg
         self.device = device
         self.scale = scale
+        self.implicit_conv = True  # FPN / RPN 3x3 convolutions as implicit GEMMs (False: im2col + GEMM)
         self.dev = torch.device("cuda", device)
         self.ctx = _lib.Context.get(device)
         self.w = {}
@@ -194,6 +195,23 @@ class SwinDetectorHip:
         _lib.check(self.ctx.lib.mq_gemm_bf16(self.ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(C),
                                              _lib.ptr(bias) if bias is not None else None, None, M, N, K, K, K,
                                              N if ldc is None else ldc, 0, epi, self._s()), "mq_gemm_bf16")
+
+    def _conv3x3(self, x, n, h, w, wt, bias, out, epi):
+        """3x3 / pad 1 conv of the f32 NHWC map x (256 channels): implicit GEMM on its bf16 copy (default), or
+        im2col + GEMM (``self.implicit_conv = False``); both give the same bits."""
+        rows = n * h * w
+        if self.implicit_conv:
+            xb = torch.empty((rows, 256), dtype=torch.bfloat16, device=self.dev)
+            _lib.check(self.ctx.lib.mq_f32_to_bf16(self.ctx.handle, _lib.ptr(x), _lib.ptr(xb), rows * 256, self._s()),
+                       "mq_f32_to_bf16")
+            _lib.check(self.ctx.lib.mq_conv3x3_bf16(self.ctx.handle, _lib.ptr(xb), n, h, w, 256, _lib.ptr(wt),
+                                                    _lib.ptr(bias), _lib.ptr(out), out.shape[1], out.shape[1], epi,
+                                                    self._s()), "mq_conv3x3_bf16")
+            return
+        cols = torch.empty((rows, 9 * 256), dtype=torch.bfloat16, device=self.dev)
+        _lib.check(self.ctx.lib.mq_im2col3x3(self.ctx.handle, _lib.ptr(x), n, h, w, 256, _lib.ptr(cols), self._s()),
+                   "mq_im2col3x3")
+        self._gemm(cols, wt, out, bias, rows, out.shape[1], 9 * 256, epi)
 
     def _ln(self, x, g, b, y, rows, dim, out_f32=False):
         _lib.check(self.ctx.lib.mq_layernorm(self.ctx.handle, _lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), rows,
@@ -298,11 +316,8 @@ class SwinDetectorHip:
         P = []
         for i in range(4):
             Hs, Ws = g["sizes"][i]
-            cols = torch.empty((n * Hs * Ws, 9 * 256), dtype=torch.bfloat16, device=dev)
-            _lib.check(self.ctx.lib.mq_im2col3x3(self.ctx.handle, _lib.ptr(lat[i]), n, Hs, Ws, 256, _lib.ptr(cols),
-                                                 self._s()), "mq_im2col3x3")
             t = torch.empty((n * Hs * Ws, 256), dtype=torch.float32, device=dev)
-            self._gemm(cols, self.w[f"fpn{i}"], t, self.w[f"fpn{i}_b"], n * Hs * Ws, 256, 9 * 256, EPI_F32)
+            self._conv3x3(lat[i], n, Hs, Ws, self.w[f"fpn{i}"], self.w[f"fpn{i}_b"], t, EPI_F32)
             P.append(t)
         h5, w5 = g["sizes"][3]
         h6, w6 = g["levels"][4]
@@ -317,14 +332,11 @@ class SwinDetectorHip:
         dev = self.dev
         rows = [n * h * w for h, w in g["levels"]]
         M = sum(rows)
-        cols = torch.empty((M, 9 * 256), dtype=torch.bfloat16, device=dev)
+        hid = torch.empty((M, 256), dtype=torch.bfloat16, device=dev)
         off = 0
         for (h, w), p, r in zip(g["levels"], P, rows):
-            _lib.check(self.ctx.lib.mq_im2col3x3(self.ctx.handle, _lib.ptr(p), n, h, w, 256,
-                                                 _lib.ptr(cols[off:off + r]), self._s()), "mq_im2col3x3")
+            self._conv3x3(p, n, h, w, self.w["rpn_conv"], self.w["rpn_conv_b"], hid[off:off + r], EPI_RELU)
             off += r
-        hid = torch.empty((M, 256), dtype=torch.bfloat16, device=dev)
-        self._gemm(cols, self.w["rpn_conv"], hid, self.w["rpn_conv_b"], M, 256, 9 * 256, EPI_RELU)
         head = torch.empty((M, 15), dtype=torch.float32, device=dev)
         self._gemm(hid, self.w["rpn_out"], head, self.w["rpn_out_b"], M, 15, 256, EPI_F32)
         return head

@@ -138,6 +138,60 @@ def test_backbone_and_fpn_match_oracle(det_small, weights_small):
             assert err <= 3e-2 * exp.abs().max().item(), (l, err)
 
 
+@pytest.mark.parametrize("n,h,w,c,cout,epi", [(2, 25, 34, 256, 256, 4), (1, 13, 17, 256, 256, 6),
+                                              (3, 40, 7, 64, 96, 4), (1, 200, 272, 256, 256, 6),
+                                              (4, 100, 136, 256, 256, 4),
+                                              (2, 9, 300, 128, 24, 0)])
+def test_implicit_conv3x3_equals_im2col_gemm(n, h, w, c, cout, epi):
+    # (ch % 64, cout % 8 for bf16 outputs: mq_conv3x3_bf16 rejects the rest, see test_implicit_conv3x3_rejects)
+    """mq_conv3x3_bf16 (implicit GEMM, zero padding from out-of-range DMA offsets) gives the bits of
+    mq_im2col3x3 + the ping-pong GEMM on the same bf16 input: same K order, same accumulation."""
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(n * 1000 + h + w + c)
+    x = torch.randn((n * h * w, c), generator=g, device="cuda")
+    xb = torch.empty((n * h * w, c), device="cuda", dtype=torch.bfloat16)
+    _lib.check(ctx.lib.mq_f32_to_bf16(ctx.handle, _lib.ptr(x), _lib.ptr(xb), x.numel(), _lib.stream_ptr()), "cvt")
+    assert torch.equal(xb, x.to(torch.bfloat16))
+    wt = (torch.randn((cout, 9 * c), generator=g, device="cuda") / (3 * c ** 0.5)).to(torch.bfloat16)
+    bias = torch.randn((cout,), generator=g, device="cuda")
+    dt = torch.float32 if epi == 4 else torch.bfloat16
+    got = torch.empty((n * h * w, cout), device="cuda", dtype=dt)
+    _lib.check(ctx.lib.mq_conv3x3_bf16(ctx.handle, _lib.ptr(xb), n, h, w, c, _lib.ptr(wt), _lib.ptr(bias),
+                                       _lib.ptr(got), cout, cout, epi, _lib.stream_ptr()), "conv")
+    cols = torch.empty((n * h * w, 9 * c), device="cuda", dtype=torch.bfloat16)
+    _lib.check(ctx.lib.mq_im2col3x3(ctx.handle, _lib.ptr(x), n, h, w, c, _lib.ptr(cols), _lib.stream_ptr()), "im2col")
+    ref = torch.empty_like(got)
+    _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(cols), _lib.ptr(wt), _lib.ptr(ref), _lib.ptr(bias), None,
+                                    n * h * w, cout, 9 * c, 9 * c, 9 * c, cout, 0, epi, _lib.stream_ptr()), "gemm")
+    torch.cuda.synchronize()
+    # the im2col GEMM may route to another (bit-identical or not) kernel at small M: compare against the
+    # fp32 product too, and require bit equality where both took the ping-pong kernel (M >= 256 rows, K % 64)
+    prod = cols.float() @ wt.float().t() + bias
+    if epi == 6:
+        prod = prod.clamp_min(0)
+    tol = 2e-2 * prod.abs().max().item()
+    assert (got.float() - prod).abs().max().item() <= tol
+    if ((n * h * w + 255) // 256) * ((cout + 255) // 256) >= 128 and cout >= 256:
+        assert torch.equal(got, ref)
+
+
+def test_implicit_conv3x3_rejects_bad_shapes():
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    x = torch.zeros((4 * 4, 256), device="cuda", dtype=torch.bfloat16)
+    w = torch.zeros((16, 9 * 256), device="cuda", dtype=torch.bfloat16)
+    out = torch.zeros((16, 16), device="cuda")
+    s = _lib.stream_ptr()
+    assert ctx.lib.mq_conv3x3_bf16(ctx.handle, _lib.ptr(x), 1, 4, 4, 96, _lib.ptr(w), None, _lib.ptr(out), 16, 16, 4,
+                                   s) != 0            # ch % 64
+    assert ctx.lib.mq_conv3x3_bf16(ctx.handle, _lib.ptr(x), 1, 4, 4, 256, _lib.ptr(w), None, _lib.ptr(out), 15, 15,
+                                   0, s) != 0         # bf16 out, cout % 8
+    assert ctx.lib.mq_conv3x3_bf16(ctx.handle, _lib.ptr(x), 1, 4, 4, 256, _lib.ptr(w), None, _lib.ptr(out), 16, 16,
+                                   2, s) != 0         # residual epilogue not offered
+
+
 def test_nms_matches_oracle():
     from mqhip import _lib
     from oracle import swin_det as sd

@@ -38,6 +38,18 @@ def main():
     torch.cuda.synchronize()
     res["eager_ms_per_frame"] = (time.perf_counter() - t0) * 1e3 / args.steps
     res["detections"] = [int(c) for c in out[2].cpu()]
+    # A/B in this process: the FPN / RPN 3x3 convolutions through im2col + GEMM instead of implicit GEMMs
+    det.implicit_conv = False
+    for _ in range(2):
+        ref = det.forward(fr)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ref = det.forward(fr)
+    torch.cuda.synchronize()
+    res["eager_ms_per_frame_im2col_convs"] = (time.perf_counter() - t0) * 1e3 / args.steps
+    res["im2col_path_same_counts"] = bool(torch.equal(ref[2], out[2]))
+    det.implicit_conv = True
     if args.graph:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
