@@ -100,7 +100,7 @@ def _run_pair(M, N, K, epi, aux_rows, seed=0):
     bias = torch.randn((N,), generator=g, device="cuda")
     aux = torch.randn((aux_rows, N), generator=g, device="cuda")
     C0 = torch.randn((M, N), generator=g, device="cuda")
-    if epi in (0, 1):
+    if epi in (0, 1, 6):
         C0 = C0.to(torch.bfloat16)
     outs = []
     old = ctx.lib.mq_get_tuning(12)
@@ -118,9 +118,10 @@ def _run_pair(M, N, K, epi, aux_rows, seed=0):
     return outs
 
 
-@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 6])
 @pytest.mark.parametrize("M,N,K", [(12288, 1280, 1280), (700, 512, 320), (4196, 5120, 256), (2048, 3840, 1280),
-                                   (1000, 1280, 2048), (3000, 1280, 5120)])
+                                   (1000, 1280, 2048), (3000, 1280, 5120), (4096, 2048, 64), (4196, 2056, 64),
+                                   (4196, 2056, 192)])
 def test_gemm_pingpong_bitwise_equals_interleaved(epi, M, N, K):
     """Both kernels accumulate every output in the same order (32-deep MFMA steps in ascending K,
     then bias, then the epilogue op), so the ping-pong kernel must reproduce the other bit for bit,
