@@ -50,6 +50,9 @@ const char* mq_last_error(void);
                                         fits; 0: the global-memory substitution kernel (same preconditioner) */
 #define MQ_TUNE_ATTENTION_V2 17     /* 1 (default): attention on 16x16x32 QK^T + transposed-output PV (vit_ops.hip
                                        attention2_kernel); 0: the first-generation kernel */
+#define MQ_TUNE_GEMM_PP_WIDE 19     /* 1 (default): ping-pong GEMMs with the GELU or long-K residual epilogue whose
+                                       shape fills whole CU rounds with 192x320 tiles take them (fc1, fc2 of
+                                       ViT-H); 0: 256x256 tiles only */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

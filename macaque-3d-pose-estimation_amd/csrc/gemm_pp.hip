@@ -34,20 +34,63 @@
 //
 // Accumulation order per output element is the one of gemm256_kernel (K in ascending 32-deep
 // MFMA steps, then + bias, then the epilogue op), so both kernels give bit-identical results.
+//
+// Two tile shapes share the kernel (template PPShape<WMF, WNF>: fragments per wave in M and N):
+//   256 x 256 (8 x 4 fragments per wave, the table above);
+//   192 x 320 (6 x 5 fragments, wave block 96 x 80): 61,440 outputs per tile instead of 65,536, which
+//     fits the ViT-H shapes into whole rounds of the 256 CUs -- fc1 1,024 tiles = 4 rounds (256 x 256:
+//     960 = 3.75 rounds, the last one a quarter idle), fc2 256 = 1 round (240).  Same 64 KiB stage,
+//     LDS reads per MAC within 2 %, DMA bytes per MAC +7 %.  Routed only where measured faster
+//     (pp_use_wide).
+//     Phases: quadrants of 3 x 3 / 3 x 2 / 3 x 3 / 3 x 2 fragments (18 / 12 / 18 / 12 MFMAs); the 64
+//     DMA groups of a stage are issued 3 / 2 / 2 / 1 per wave per phase in first-read order (P0 in
+//     phases 0-1, P1 by phase 2, P2 by phase 3), which keeps every wait a compile-time count.
 #include "common.hpp"
 #include "kernels.hpp"
 
 namespace mq {
 
 int g_gemm_pingpong = 1;
+int g_gemm_pp_wide = 1;
+
+constexpr int PP_BK = 64, PP_T = 512;
+constexpr int PP_STAGE = 64 * 1024;   // one BK slice of the A and W tiles (both shapes: (BM + BN) x 128 B)
+constexpr int PP_BIAS = 2 * PP_STAGE; // bias area after the 2-stage ring
+
+// Tile geometry: WMF x WNF MFMA fragments (16 x 16) per wave, 8 waves as 2 (M) x 4 (N).
+template <int WMF_, int WNF_>
+struct PPShape {
+  static constexpr int WMF = WMF_, WNF = WNF_;
+  static constexpr int QM = WMF / 2;          // fragments per M half (phases 0,1 | 2,3)
+  static constexpr int NA = (WNF + 1) / 2;    // fragments of the first N part (phases 0, 2)
+  static constexpr int NB = WNF - NA;         // second N part (phases 1, 3)
+  static constexpr int BM = 2 * 16 * WMF, BN = 4 * 16 * WNF;
+  static constexpr int OPA = BM * PP_BK * 2;  // A slice bytes; the W slice follows it
+  // bias slice per wave: 16 WNF floats; one dword LDS-DMA covers 64 (256 B), else one dwordx4 (1 KiB)
+  static constexpr bool BIAS_X4 = WNF > 4;
+  static constexpr int BIAS_SLOT = BIAS_X4 ? 1024 : 256;
+  static constexpr int LDS = PP_BIAS + 8 * BIAS_SLOT;
+  // DMA groups (8 rows x 128 B = one 1-KiB wave instruction) in first-read order: P0 A, P0 W, P1 W, P2 A
+  static constexpr int GA0 = BM / 16;         // P0 A groups (M half 0 of both wave groups)
+  static constexpr int GW0 = 4 * 2 * NA;      // P0 W groups (N part A of the 4 wave columns)
+  static constexpr int GW1 = 4 * 2 * NB;      // P1 W groups
+  static constexpr int GA2 = BM / 16;         // P2 A groups
+  static_assert(GA0 + GW0 + GW1 + GA2 == 64, "a stage is 64 DMA groups");
+  // per-wave DMA instructions per phase
+  static constexpr int C0 = WNF == 4 ? 2 : 3, C1 = 2, C2 = 2, C3 = WNF == 4 ? 2 : 1;
+  static_assert(C0 + C1 + C2 + C3 == 8, "8 DMA slots per wave");
+  static_assert(8 * (C0 + C1) >= GA0 + GW0, "P0 must be issued in phases 0-1");
+  static_assert(8 * (C0 + C1 + C2) >= GA0 + GW0 + GW1, "P1 must be issued by phase 2");
+  // counted waits (vector memory ops younger than the ones retired): see the kernel
+  static constexpr int N0 = C3 + C0 + 1, N1 = C0 + 1 + C1, N3 = C2 + C3;
+  // epilogue stores per wave of a full tile (bf16: pairs of fragments as 16-B rows + an 8-B tail)
+  static constexpr int STORES_BF16 = WMF * (WNF / 2 + (WNF & 1));
+  static constexpr int STORES_F32 = WMF * WNF;
+};
+using Shape256 = PPShape<8, 4>;
+using Shape320 = PPShape<6, 5>;
 
 namespace {
-
-constexpr int PP_BM = 256, PP_BN = 256, PP_BK = 64, PP_T = 512;
-constexpr int PP_OP = PP_BM * PP_BK * 2;  // 32 KiB: one operand slice of a stage
-constexpr int PP_STAGE = 2 * PP_OP;       // 64 KiB
-constexpr int PP_BIAS = 2 * PP_STAGE;     // bias area: 8 waves x 256 B
-constexpr int PP_LDS = PP_BIAS + 8 * 256;
 
 __device__ __forceinline__ int pp_swz(int row) { return (row >> 1) & 7; }
 
@@ -68,6 +111,7 @@ __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
 }
 
+template <class S>
 __device__ __forceinline__ void pp_tile_coords(int wid, int tiles_m, int tiles_n, int& m0, int& n0) {
   constexpr int GROUP_M = 8;
   const int per_group = GROUP_M * tiles_n;
@@ -75,75 +119,120 @@ __device__ __forceinline__ void pp_tile_coords(int wid, int tiles_m, int tiles_n
   const int first_m = grp * GROUP_M;
   const int gsize = min(tiles_m - first_m, GROUP_M);
   const int in_g = wid - grp * per_group;
-  m0 = (first_m + in_g % gsize) * PP_BM;
-  n0 = (in_g / gsize) * PP_BN;
+  m0 = (first_m + in_g % gsize) * S::BM;
+  n0 = (in_g / gsize) * S::BN;
 }
 
-// DMA slot i (0..7) of wave w moves the 8-row group starting at this row of its operand.
-// Slots 0,1: P0 A rows; 2,3: P0 W rows; 4,5: P1 W rows; 6,7: P2 A rows (16 groups each).
-__device__ __forceinline__ int pp_group_row(int w, int i) {
-  const int g = w * 2 + (i & 1);
-  switch (i >> 1) {
-    case 0: return g < 8 ? g * 8 : 128 + (g - 8) * 8;
-    case 1: return (g >> 2) * 64 + (g & 3) * 8;
-    case 2: return (g >> 2) * 64 + 32 + (g & 3) * 8;
-    default: return g < 8 ? 64 + g * 8 : 192 + (g - 8) * 8;
+// DMA group k (0..63, first-read order) -> operand (W?) and first tile row of its 8 rows
+template <class S>
+__device__ __forceinline__ int pp_group_row(int k, bool& is_w) {
+  constexpr int HALF = S::BM / 2;      // rows per wave group
+  constexpr int QR = 16 * S::QM;       // rows per M half
+  constexpr int WCOL = 16 * S::WNF;    // W rows per wave column
+  if (k < S::GA0) {
+    is_w = false;
+    const int gq = QR / 8;             // groups per (wave group, M half)
+    return (k / gq) * HALF + (k % gq) * 8;
   }
+  k -= S::GA0;
+  if (k < S::GW0) {
+    is_w = true;
+    const int gq = 2 * S::NA;
+    return (k / gq) * WCOL + (k % gq) * 8;
+  }
+  k -= S::GW0;
+  if (k < S::GW1) {
+    is_w = true;
+    const int gq = 2 * S::NB;
+    return (k / gq) * WCOL + 16 * S::NA + (k % gq) * 8;
+  }
+  k -= S::GW1;
+  is_w = false;
+  const int gq = QR / 8;
+  return (k / gq) * HALF + QR + (k % gq) * 8;
 }
-__device__ __forceinline__ constexpr bool pp_slot_is_w(int i) { return (i >> 1) == 1 || (i >> 1) == 2; }
+// slot i (0..7) of wave w -> its group: phase p's slots of all waves take groups 8 (C0 + .. + C_{p-1})
+// + w C_p + (slot within the phase)
+template <class S>
+__device__ __forceinline__ int pp_slot_group(int w, int i) {
+  if (i < S::C0) return w * S::C0 + i;
+  i -= S::C0;
+  if (i < S::C1) return 8 * S::C0 + w * S::C1 + i;
+  i -= S::C1;
+  if (i < S::C2) return 8 * (S::C0 + S::C1) + w * S::C2 + i;
+  i -= S::C2;
+  return 8 * (S::C0 + S::C1 + S::C2) + w * S::C3 + i;
+}
 
-// Epilogue of one wave's 128x64 block: acc[i][j] holds C[m0 + wm*128 + i*16 + (l & 15)]
-// [n0 + wn*64 + j*16 + 4*(l >> 4) + e].  Zeroes the accumulators for the next tile.
-template <int EPI>
-__device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4], const float* bias_lds, int m0,
-                                            int n0, int wm, int wn, int lane) {
+// Epilogue of one wave's (16 WMF) x (16 WNF) block: acc[i][j] holds C[m0 + wm*BM/2 + i*16 + (l & 15)]
+// [n0 + wn*16*WNF + j*16 + 4*(l >> 4) + e].  Zeroes the accumulators for the next tile.
+template <int EPI, class S>
+__device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::WMF][S::WNF], const float* bias_lds,
+                                            int m0, int n0, int wm, int wn, int lane) {
+  constexpr int WMF = S::WMF, WNF = S::WNF;
   const int mm = lane & 15;
   const int nn = 4 * (lane >> 4);
+  const int mb = m0 + wm * (S::BM / 2), nb = n0 + wn * 16 * WNF;
   // The bias slice was LDS-DMA'd and retired by this wave's own counted vmcnt.  Read it in inline asm:
   // a plain LDS read here makes the compiler wait vmcnt(0) for every DMA in flight (it cannot tell the
   // bias slot from the stage buffers the in-flight DMAs write).
-  f32x4 bv[4];
+  f32x4 bv[WNF];
   {
     const unsigned addr = (unsigned)(uintptr_t)MQ_LDS_LOCAL(bias_lds + nn);
-    asm volatile(
-        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
-        "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
-        : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
-        : "v"(addr)
-        : "memory");
+    if constexpr (WNF == 4) {
+      asm volatile(
+          "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
+          "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
+          : "v"(addr)
+          : "memory");
+    } else {
+      static_assert(WNF == 5, "bias read for 4 or 5 fragments");
+      asm volatile(
+          "ds_read_b128 %0, %5\n\tds_read_b128 %1, %5 offset:64\n\tds_read_b128 %2, %5 offset:128\n\t"
+          "ds_read_b128 %3, %5 offset:192\n\tds_read_b128 %4, %5 offset:256\n\ts_waitcnt lgkmcnt(0)"
+          : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3]), "=&v"(bv[4])
+          : "v"(addr)
+          : "memory");
+    }
   }
-  float4 bias[4];
+  float4 bias[WNF];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) bias[j] = make_float4(bv[j][0], bv[j][1], bv[j][2], bv[j][3]);
-  const bool full = (m0 + PP_BM <= p.M) && (n0 + PP_BN <= p.N);
+  for (int j = 0; j < WNF; ++j) bias[j] = make_float4(bv[j][0], bv[j][1], bv[j][2], bv[j][3]);
+  const bool full = (m0 + S::BM <= p.M) && (n0 + S::BN <= p.N);
   if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
+    auto act = [&](int i, int j, float (&v)[4]) {
+      v[0] = acc[i][j][0] + bias[j].x;
+      v[1] = acc[i][j][1] + bias[j].y;
+      v[2] = acc[i][j][2] + bias[j].z;
+      v[3] = acc[i][j][3] + bias[j].w;
+      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_GELU_BF16) {
+        const f32x2 g0 = gelu_erf2((f32x2){v[0], v[1]}), g1 = gelu_erf2((f32x2){v[2], v[3]});
+        v[0] = g0.x;
+        v[1] = g0.y;
+        v[2] = g1.x;
+        v[3] = g1.y;
+      }
+      if constexpr (EPI == EPI_RELU_BF16) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+    };
     // pair fragments (j, j+1): v_permlane16_swap gives every lane 8 consecutive columns -> one
-    // 16-byte store per lane per pair
+    // 16-byte store per lane per pair; an odd last fragment stores its 4 columns (8 B) per lane
     const bool odd = (lane >> 4) & 1;
     const int nbase = nn - (odd ? 4 : 0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = m0 + wm * 128 + i * 16 + mm;
+    for (int i = 0; i < WMF; ++i) {
+      const int m = mb + i * 16 + mm;
 #pragma unroll
-      for (int jp = 0; jp < 4; jp += 2) {
+      for (int jp = 0; jp + 1 < WNF; jp += 2) {
         unsigned pk[2][2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int j = jp + h;
-          float v[4] = {acc[i][j][0] + bias[j].x, acc[i][j][1] + bias[j].y, acc[i][j][2] + bias[j].z,
-                        acc[i][j][3] + bias[j].w};
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if constexpr (EPI == EPI_GELU_BF16) {
-            const f32x2 g0 = gelu_erf2((f32x2){v[0], v[1]}), g1 = gelu_erf2((f32x2){v[2], v[3]});
-            v[0] = g0.x;
-            v[1] = g0.y;
-            v[2] = g1.x;
-            v[3] = g1.y;
-          }
-          if constexpr (EPI == EPI_RELU_BF16) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-          }
+          float v[4];
+          act(i, jp + h, v);
           pk[h][0] = pack_bf16x2(v[0], v[1]);
           pk[h][1] = pack_bf16x2(v[2], v[3]);
         }
@@ -151,39 +240,47 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
         const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
         // even lanes: [own tile j | neighbour's tile j]; odd: [neighbour's j+1 | own j+1]
         const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-        const int n = n0 + wn * 64 + (jp + (odd ? 1 : 0)) * 16 + nbase;
+        const int n = nb + (jp + (odd ? 1 : 0)) * 16 + nbase;
         if (full || (m < p.M && n < p.N)) *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
+      }
+      if constexpr (WNF & 1) {
+        float v[4];
+        act(i, WNF - 1, v);
+        const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        const int n = nb + (WNF - 1) * 16 + nn;
+        if (full || (m < p.M && n < p.N)) *reinterpret_cast<uint2*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
       }
     }
     return;
   }
   if constexpr (EPI == EPI_RESID_F32) {
     if (full) {
-      // four fragment rows (16 independent 16-B loads) in flight per round trip: the A/W
+      // RG fragment rows (RG x WNF independent 16-B loads) in flight per round trip: the A/W
       // fragment registers are dead here and hold them
+      constexpr int RG = WMF % 4 == 0 ? 4 : 3;
 #pragma unroll
-      for (int i0 = 0; i0 < 8; i0 += 4) {
-        float4 x[4][4];
+      for (int i0 = 0; i0 < WMF; i0 += RG) {
+        float4 x[RG][WNF];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int m = m0 + wm * 128 + (i0 + c) * 16 + mm;
+        for (int c = 0; c < RG; ++c) {
+          const int m = mb + (i0 + c) * 16 + mm;
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            x[c][j] = *reinterpret_cast<const float4*>((const float*)p.C + (size_t)m * p.ldc + n0 + wn * 64 + j * 16 + nn);
+          for (int j = 0; j < WNF; ++j)
+            x[c][j] = *reinterpret_cast<const float4*>((const float*)p.C + (size_t)m * p.ldc + nb + j * 16 + nn);
         }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int c = 0; c < RG; ++c) {
           const int i = i0 + c;
-          const int m = m0 + wm * 128 + i * 16 + mm;
+          const int m = mb + i * 16 + mm;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < WNF; ++j) {
             float4 o = x[c][j];
             o.x += acc[i][j][0] + bias[j].x;
             o.y += acc[i][j][1] + bias[j].y;
             o.z += acc[i][j][2] + bias[j].z;
             o.w += acc[i][j][3] + bias[j].w;
             acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + n0 + wn * 64 + j * 16 + nn) = o;
+            *reinterpret_cast<float4*>((float*)p.C + (size_t)m * p.ldc + nb + j * 16 + nn) = o;
           }
         }
       }
@@ -191,11 +288,11 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
     }
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = m0 + wm * 128 + i * 16 + mm;
+  for (int i = 0; i < WMF; ++i) {
+    const int m = mb + i * 16 + mm;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + nn;
+    for (int j = 0; j < WNF; ++j) {
+      const int n = nb + j * 16 + nn;
       const float v[4] = {acc[i][j][0] + bias[j].x, acc[i][j][1] + bias[j].y, acc[i][j][2] + bias[j].z,
                           acc[i][j][3] + bias[j].w};
       acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -218,14 +315,19 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[8][4
   }
 }
 
-template <int EPI, bool CONV = false>
+template <int EPI, bool CONV, int WMF_, int WNF_>
 __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_m, int tiles_n) {
+  using S = PPShape<WMF_, WNF_>;
+  static_assert(!CONV || S::WNF == 4, "implicit convolution: 256 x 256 tiles only");
+  constexpr int WMF = S::WMF, WNF = S::WNF, QM = S::QM, NA = S::NA, NB = S::NB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: LDS-DMA bases in SGPRs
   const int wm = wave >> 2, wn = wave & 3;
   const int frow = lane & 15;
   const int fk = lane >> 4;
+  const int arow = wm * (S::BM / 2);   // this wave's first A row
+  const int wcol = wn * 16 * WNF;      // this wave's first W row (output column)
 
   // this XCD's tiles = a contiguous range; its blocks take them round-robin
   const int nt = tiles_m * tiles_n;
@@ -250,6 +352,12 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   const __amdgpu_buffer_rsrc_t rsB =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, p.bias ? p.N * 4 : 0, 0x00020000);
 
+  // this wave's 8 DMA slots: operand and first row of each (wave-uniform)
+  int grow[8];
+  bool gw[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) grow[i] = pp_group_row<S>(pp_slot_group<S>(wave, i), gw[i]);
+
   // DMA issue cursor: (tile, k) of the next stage to load and this lane's source offsets for
   // that tile.  Past the end it stays on the last stage (re-loaded into the idle buffer), which
   // keeps every wait count uniform.
@@ -260,12 +368,12 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   unsigned cyx[8];
   auto set_tile_ptrs = [&](int ti) {
     int m0, n0;
-    pp_tile_coords(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+    pp_tile_coords<S>(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int row = pp_group_row(wave, i) + (lane >> 3);
+      const int row = grow[i] + (lane >> 3);
       const int chunk = (lane & 7) ^ pp_swz(row);
-      if (pp_slot_is_w(i)) {
+      if (gw[i]) {
         voff[i] = (unsigned)(((size_t)min(n0 + row, p.N - 1) * p.ldw + chunk * 8) * 2);
       } else if constexpr (CONV) {
         const int pix = min(m0 + row, p.M - 1);
@@ -280,9 +388,17 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     }
   };
   set_tile_ptrs(0);
+  // per slot: its buffer resource and LDS offset, resolved once (no selects in the K-loop)
+  __amdgpu_buffer_rsrc_t srs[8];
+  int sdst[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    srs[i] = gw[i] ? rsW : rsA;
+    sdst[i] = (gw[i] ? S::OPA : 0) + grow[i] * 128;
+  }
   auto issue = [&](int i, int slot) {
-    char* dst = smem + slot * PP_STAGE + (pp_slot_is_w(i) ? PP_OP : 0) + pp_group_row(wave, i) * 128;
-    if (CONV && !pp_slot_is_w(i)) {
+    char* dst = smem + slot * PP_STAGE + sdst[i];
+    if (CONV && !gw[i]) {
       // K-step iss_k = tap * (C / 64) + c64: the tap's shifted pixel, channels 64 c64 .. + 63; a pixel
       // outside the image gets an offset past the buffer end, which the DMA turns into zeros (padding)
       const int kpt = p.conv_c >> 6;
@@ -293,7 +409,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
       const unsigned off = (unsigned)((int)voff[i] + (dy * p.conv_w + dx) * p.conv_c + (iss_k - tap * kpt) * 64);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(dst), 16, inside ? off * 2 : 0x80000000u, 0, 0, 0);
     } else {
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(pp_slot_is_w(i) ? rsW : rsA, MQ_LDS_LOCAL(dst), 16, voff[i],
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(srs[i], MQ_LDS_LOCAL(dst), 16, voff[i],
                                                iss_k * PP_BK * 2, 0, 0);
     }
   };
@@ -307,31 +423,47 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     }
   };
 
-  // compute cursor: tile index, K-step in it, its origin, this wave's bias DMA offset
+  // compute cursor: tile index, K-step in it, its origin, this wave's bias DMA offset (dword form:
+  // one column per lane; dwordx4 form: four per lane, lanes past the slice read past the buffer = 0)
   int ct = 0, kt = 0, cm0 = 0, cn0 = 0;
-  pp_tile_coords(lo + xb, tiles_m, tiles_n, cm0, cn0);
-  char* bias_lds = smem + PP_BIAS + wave * 256;
-  unsigned bias_off = (unsigned)((cn0 + wn * 64 + lane) * 4);
+  pp_tile_coords<S>(lo + xb, tiles_m, tiles_n, cm0, cn0);
+  char* bias_lds = smem + PP_BIAS + wave * S::BIAS_SLOT;
+  auto bias_offset = [&](int n0) -> unsigned {
+    if constexpr (S::BIAS_X4)
+      return 4 * lane < 16 * WNF ? (unsigned)((n0 + wcol + 4 * lane) * 4) : 0x80000000u;
+    else
+      return (unsigned)((n0 + wcol + lane) * 4);
+  };
+  unsigned bias_off = bias_offset(cn0);
+  // (literal sizes: a template-dependent size argument makes the host compilation drop the kernel stub)
+  auto issue_bias = [&]() {
+    if constexpr (S::BIAS_X4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 16, bias_off, 0, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
+  };
 
-  f32x4 acc[8][4];
+  f32x4 acc[WMF][WNF];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < WMF; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 a[4][2], b0[2][2], b1[2][2];
+    for (int j = 0; j < WNF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[QM][2], b0[NA][2], b1[NB][2];
 
-  auto mfma_quadrant = [&](int qm, int qn, bf16x8 (&bb)[2][2]) {
+  auto mfma_quadrant = [&](int qm, auto& bb, int jbase, auto nj) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < QM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[qm * 4 + i][qn * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][kk], a[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+        for (int j = 0; j < decltype(nj)::value; ++j)
+          acc[qm * QM + i][jbase + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][kk], a[i][kk], acc[qm * QM + i][jbase + j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  using NAc = std::integral_constant<int, NA>;
+  using NBc = std::integral_constant<int, NB>;
   // barrier that opens an MFMA segment: the segment's fragment reads are complete
   auto bar = [&]() { pp_barrier(); };
   auto open_mfma = [&]() {
@@ -339,84 +471,87 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
-  // prologue: stage 0 into buffer 0; P0 (the 4 oldest DMAs) must land before the first reads
+  // prologue: stage 0 into buffer 0; P0 (the slots of phases 0-1) must land before the first reads
 #pragma unroll
   for (int i = 0; i < 8; ++i) issue(i, 0);
   advance();
-  pp_wait_vm<4>();
+  pp_wait_vm<S::N3>();
   pp_barrier();
   if (wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
 
   // >= this many epilogue stores of a full tile are younger than the DMA the next two waits retire
-  constexpr int EPI_OPS = (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) ? 16 : 32;
+  constexpr int EPI_OPS =
+      (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) ? S::STORES_BF16 : S::STORES_F32;
   bool stores_pending = false;
   for (int g = 0; g < total; ++g) {
     const int slot = g & 1;
     const char* As = smem + slot * PP_STAGE;
-    const char* Ws = As + PP_OP;
-    // ---- phase 0: quadrant (0,0)
+    const char* Ws = As + S::OPA;
+    // ---- phase 0: quadrant (M half 0, N part A)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        b0[j][kk] = pp_frag(Ws, wn * 64 + j * 16 + frow, kk * 4 + fk);
+      for (int j = 0; j < NA; ++j)
+        b0[j][kk] = pp_frag(Ws, wcol + j * 16 + frow, kk * 4 + fk);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[i][kk] = pp_frag(As, wm * 128 + i * 16 + frow, kk * 4 + fk);
+      for (int i = 0; i < QM; ++i)
+        a[i][kk] = pp_frag(As, arow + i * 16 + frow, kk * 4 + fk);
     }
-    issue(0, slot ^ 1);
-    issue(1, slot ^ 1);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < S::C0; ++i) issue(i, slot ^ 1);
+    issue_bias();
+    // retires the DMAs of the previous K-step's phase 2 (younger: its phase 3, this phase + bias)
     if (stores_pending)
-      pp_wait_vm<5 + EPI_OPS>();
+      pp_wait_vm<S::N0 + EPI_OPS>();
     else
-      pp_wait_vm<5>();
+      pp_wait_vm<S::N0>();
     open_mfma();
-    mfma_quadrant(0, 0, b0);
+    mfma_quadrant(0, b0, 0, NAc{});
     bar();
-    // ---- phase 1: quadrant (0,1)
+    // ---- phase 1: quadrant (M half 0, N part B)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        b1[j][kk] = pp_frag(Ws, wn * 64 + 32 + j * 16 + frow, kk * 4 + fk);
-    issue(2, slot ^ 1);
-    issue(3, slot ^ 1);
+      for (int j = 0; j < NB; ++j)
+        b1[j][kk] = pp_frag(Ws, wcol + 16 * NA + j * 16 + frow, kk * 4 + fk);
+#pragma unroll
+    for (int i = S::C0; i < S::C0 + S::C1; ++i) issue(i, slot ^ 1);
+    // retires the previous K-step's phase-3 DMAs (younger: phase 0 + bias, this phase)
     if (stores_pending)
-      pp_wait_vm<5 + EPI_OPS>();
+      pp_wait_vm<S::N1 + EPI_OPS>();
     else
-      pp_wait_vm<5>();
+      pp_wait_vm<S::N1>();
     stores_pending = false;
     open_mfma();
-    mfma_quadrant(0, 1, b1);
+    mfma_quadrant(0, b1, NA, NBc{});
     bar();
-    // ---- phase 2: quadrant (1,0)
+    // ---- phase 2: quadrant (M half 1, N part A)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        a[i][kk] = pp_frag(As, wm * 128 + 64 + i * 16 + frow, kk * 4 + fk);
-    issue(4, slot ^ 1);
-    issue(5, slot ^ 1);
+      for (int i = 0; i < QM; ++i)
+        a[i][kk] = pp_frag(As, arow + 16 * QM + i * 16 + frow, kk * 4 + fk);
+#pragma unroll
+    for (int i = S::C0 + S::C1; i < S::C0 + S::C1 + S::C2; ++i) issue(i, slot ^ 1);
     open_mfma();
-    mfma_quadrant(1, 0, b0);
+    mfma_quadrant(1, b0, 0, NAc{});
     bar();
-    // ---- phase 3: quadrant (1,1)
-    issue(6, slot ^ 1);
-    issue(7, slot ^ 1);
+    // ---- phase 3: quadrant (M half 1, N part B)
+#pragma unroll
+    for (int i = S::C0 + S::C1 + S::C2; i < 8; ++i) issue(i, slot ^ 1);
     advance();
-    pp_wait_vm<4>();
+    pp_wait_vm<S::N3>();  // phases 0-1 of this K-step (P0 of stage g+1) and the bias
     open_mfma();
-    mfma_quadrant(1, 1, b1);
+    mfma_quadrant(1, b1, NA, NBc{});
     bar();
     if (++kt == nk) {
-      pp_epilogue<EPI>(p, acc, reinterpret_cast<const float*>(bias_lds), cm0, cn0, wm, wn, lane);
-      stores_pending = (cm0 + PP_BM <= p.M) && (cn0 + PP_BN <= p.N);
+      pp_epilogue<EPI, S>(p, acc, reinterpret_cast<const float*>(bias_lds), cm0, cn0, wm, wn, lane);
+      stores_pending = (cm0 + S::BM <= p.M) && (cn0 + S::BN <= p.N);
       kt = 0;
       ++ct;
       if (ct < my_tiles) {
-        pp_tile_coords(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
-        bias_off = (unsigned)((cn0 + wn * 64 + lane) * 4);
+        pp_tile_coords<S>(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
+        bias_off = bias_offset(cn0);
       }
     }
   }
@@ -424,15 +559,53 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-template <int EPI, bool CONV = false>
+template <int EPI, bool CONV, class S>
 void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, CONV>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              PP_LDS);
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, CONV, S::WMF, S::WNF>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, CONV>), grid, dim3(PP_T), PP_LDS, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, CONV, S::WMF, S::WNF>), grid, dim3(PP_T), S::LDS, stream, p, tiles_m, tiles_n);
+}
+
+template <class S>
+int tiles_of(const GemmArgs& p, int& tm, int& tn) {
+  tm = (p.M + S::BM - 1) / S::BM;
+  tn = (p.N + S::BN - 1) / S::BN;
+  return tm * tn;
+}
+
+// 192 x 320 tiles where they need fewer CU-rounds of work (persistent rounds x outputs per tile, with
+// a 3 % margin for the wider tile's extra DMA bytes) AND measured faster per MAC: the GELU epilogue
+// (fc1: 1.5 % faster) and the residual at K >= 2048 (fc2: 0.4 %).  Measured slower, so not routed
+// here (profiles/r03b_ab_gemm_wide_tiles.log): the plain bf16 epilogue (qkv -1.5..-6 %) and the
+// short-K residual (proj, 1-10 % behind the interleaved kernel) -- the 18/12/18/12-MFMA phases leave
+// the 12-MFMA segments shorter than the partner's heaviest load segment.
+bool pp_use_wide(const GemmArgs& p, int epi, int num_cus) {
+  if (!g_gemm_pp_wide || !(epi == EPI_GELU_BF16 || (epi == EPI_RESID_F32 && p.K >= 2048))) return false;
+  int tm, tn;
+  const long t256 = tiles_of<Shape256>(p, tm, tn), t320 = tiles_of<Shape320>(p, tm, tn);
+  const long r256 = (t256 + num_cus - 1) / num_cus, r320 = (t320 + num_cus - 1) / num_cus;
+  return r320 * (Shape320::BM * Shape320::BN) * 100 < r256 * (Shape256::BM * Shape256::BN) * 97;
+}
+
+template <class S>
+int launch_shape(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
+  int tiles_m, tiles_n;
+  const int tiles = tiles_of<S>(p, tiles_m, tiles_n);
+  dim3 grid(tiles < num_cus ? tiles : num_cus);
+  switch (epi) {
+    case EPI_BF16: launch_pp<EPI_BF16, false, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16, false, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, false, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RESID_F32: launch_pp<EPI_RESID_F32, false, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_POS_F32: launch_pp<EPI_POS_F32, false, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_F32: launch_pp<EPI_F32, false, S>(grid, stream, p, tiles_m, tiles_n); break;
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
 }
 
 }  // namespace
@@ -447,13 +620,13 @@ int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stre
     return -1;
   // the epilogue stores 8 bf16 / 4 f32 columns per lane: whole groups only
   if (epi == EPI_F32 ? (p.N % 4 || p.ldc % 4) : (p.N % 8 || p.ldc % 8)) return -2;
-  const int tiles_m = (p.M + PP_BM - 1) / PP_BM, tiles_n = (p.N + PP_BN - 1) / PP_BN;
-  const int tiles = tiles_m * tiles_n;
+  int tiles_m, tiles_n;
+  const int tiles = tiles_of<Shape256>(p, tiles_m, tiles_n);
   dim3 grid(tiles < num_cus ? tiles : num_cus);
   switch (epi) {
-    case EPI_BF16: launch_pp<EPI_BF16, true>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, true>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_F32: launch_pp<EPI_F32, true>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_BF16: launch_pp<EPI_BF16, true, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, true, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_F32: launch_pp<EPI_F32, true, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;
@@ -463,25 +636,15 @@ int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stre
 // K (proj, K = 1280: one tile per CU, 20 K-steps), which goes to the interleaved kernel: it measured
 // 8 % faster than the ping-pong there (755 vs 692 TFLOP/s; the residual loads stall both wave
 // groups at the tile end).  At K = 5120 (fc2) the ping-pong wins.
-bool gemm_pingpong_fits(const GemmArgs& p, int epi) {
+bool gemm_pingpong_fits(const GemmArgs& p, int epi, int num_cus) {
+  (void)num_cus;
   return g_gemm_pingpong && epi != EPI_NCHW_F32 && !(epi == EPI_RESID_F32 && p.K < 2048) && p.K > 0 &&
          p.K % PP_BK == 0 && (size_t)p.M * p.lda * 2 < (1ull << 31) && (size_t)p.N * p.ldw * 2 < (1ull << 31);
 }
 
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
-  const int tiles_m = (p.M + PP_BM - 1) / PP_BM, tiles_n = (p.N + PP_BN - 1) / PP_BN;
-  const int tiles = tiles_m * tiles_n;
-  dim3 grid(tiles < num_cus ? tiles : num_cus);
-  switch (epi) {
-    case EPI_BF16: launch_pp<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RESID_F32: launch_pp<EPI_RESID_F32>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_POS_F32: launch_pp<EPI_POS_F32>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_F32: launch_pp<EPI_F32>(grid, stream, p, tiles_m, tiles_n); break;
-    default: return -3;
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -4;
+  return pp_use_wide(p, epi, num_cus) ? launch_shape<Shape320>(p, epi, num_cus, stream)
+                                 : launch_shape<Shape256>(p, epi, num_cus, stream);
 }
 
 }  // namespace mq

@@ -37,7 +37,9 @@ int conv3x3_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 extern bool g_gemm_force_small;  // every GEMM on the 128x128 kernel
 // ping-pong 256x256 kernel (gemm_pp.hip): the two wave groups of a block alternate LDS traffic and MFMA
 extern int g_gemm_pingpong;
-bool gemm_pingpong_fits(const GemmArgs& p, int epi);
+// 192x320 ping-pong tiles where they fill whole CU rounds and measured faster (gemm_pp.hip pp_use_wide)
+extern int g_gemm_pp_wide;
+bool gemm_pingpong_fits(const GemmArgs& p, int epi, int num_cus);
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 

@@ -135,7 +135,7 @@ def test_tuning_knobs_only_select_equivalent_variants(lib):
     for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 99):
         assert lib.mq_set_tuning(key, 1) == -2, key
         assert lib.mq_get_tuning(key) == -2, key
-    for key, default, other in ((2, 0, 1), (12, 1, 0), (17, 1, 0), (4, 20, 10)):
+    for key, default, other in ((2, 0, 1), (12, 1, 0), (17, 1, 0), (18, 1, 0), (19, 1, 0), (4, 20, 10)):
         assert lib.mq_get_tuning(key) == default
         assert lib.mq_set_tuning(key, other) == 0
         assert lib.mq_get_tuning(key) == other

@@ -103,17 +103,21 @@ def _run_pair(M, N, K, epi, aux_rows, seed=0):
     if epi in (0, 1, 6):
         C0 = C0.to(torch.bfloat16)
     outs = []
-    old = ctx.lib.mq_get_tuning(12)
+    old = ctx.lib.mq_get_tuning(12), ctx.lib.mq_get_tuning(19)
     try:
-        for pp in (0, 1):
+        # interleaved kernel; ping-pong with 256x256 tiles only; ping-pong with 192x320 tiles where they
+        # fill whole CU rounds (MQ_TUNE_GEMM_PP_WIDE)
+        for pp, wide in ((0, 0), (1, 0), (1, 1)):
             assert ctx.lib.mq_set_tuning(12, pp) == 0
+            assert ctx.lib.mq_set_tuning(19, wide) == 0
             Cm = C0.clone()
             _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), _lib.ptr(bias),
                                             _lib.ptr(aux), M, N, K, K, K, N, aux_rows, epi, _lib.stream_ptr()),
                        "mq_gemm_bf16")
             outs.append(Cm)
     finally:
-        ctx.lib.mq_set_tuning(12, old)
+        ctx.lib.mq_set_tuning(12, old[0])
+        ctx.lib.mq_set_tuning(19, old[1])
     torch.cuda.synchronize()
     return outs
 
@@ -121,7 +125,8 @@ def _run_pair(M, N, K, epi, aux_rows, seed=0):
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 6])
 @pytest.mark.parametrize("M,N,K", [(12288, 1280, 1280), (700, 512, 320), (4196, 5120, 256), (2048, 3840, 1280),
                                    (1000, 1280, 2048), (3000, 1280, 5120), (4096, 2048, 64), (4196, 2056, 64),
-                                   (4196, 2056, 192)])
+                                   (4196, 2056, 192), (12288, 5120, 1280), (12288, 3840, 1280), (12288, 1280, 5120),
+                                   (6000, 2560, 320)])
 def test_gemm_pingpong_bitwise_equals_interleaved(epi, M, N, K):
     """Both kernels accumulate every output in the same order (32-deep MFMA steps in ascending K,
     then bias, then the epilogue op), so the ping-pong kernel must reproduce the other bit for bit,
@@ -130,6 +135,7 @@ def test_gemm_pingpong_bitwise_equals_interleaved(epi, M, N, K):
     outs = _run_pair(M, N, K, epi, aux_rows=192)
     bits = [o.view(torch.int16) if o.dtype == torch.bfloat16 else o.view(torch.int32) for o in outs]
     assert torch.equal(bits[0], bits[1])
+    assert torch.equal(bits[0], bits[2])
 
 
 def test_gemm_force_small_matches_fp32():
