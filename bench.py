@@ -578,8 +578,7 @@ def main():
                 "traffic_source": "profiles/pmc_fc1_gemm.json: rocprofv3 --pmc 2*FETCH_SIZE + WRITE_SIZE per launch "
                                   "(gfx950 corrections; Infinity-Cache hits included); algorithmic 170,414,080 B",
                 "kernel": "%s (FFN fc1, M=%d N=%d K=%d)" % (
-                    ("gemm_pp_kernel<EPI_GELU_BF16, %s tiles>" % ("192x320" if lib.mq_get_tuning(19) == 1 else "256x256"))
-                    if lib.mq_get_tuning(12) == 1 else "gemm256_kernel<EPI_GELU_BF16>",
+                    "gemm_pp_kernel<EPI_GELU_BF16>" if lib.mq_get_tuning(12) == 1 else "gemm256_kernel<EPI_GELU_BF16>",
                     2 * n * cfg.tokens, cfg.ffn, cfg.embed_dims),
                 "flops_per_launch": fl.value, "avg_launch_ms": round(avg_ms.value, 5), "launches": cnt.value}
 

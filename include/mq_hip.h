@@ -50,9 +50,6 @@ const char* mq_last_error(void);
                                         fits; 0: the global-memory substitution kernel (same preconditioner) */
 #define MQ_TUNE_ATTENTION_V2 17     /* 1 (default): attention on 16x16x32 QK^T + transposed-output PV (vit_ops.hip
                                        attention2_kernel); 0: the first-generation kernel */
-#define MQ_TUNE_GEMM_PP_WIDE 19     /* 1 (default): ping-pong GEMMs with the GELU or long-K residual epilogue whose
-                                       shape fills whole CU rounds with 192x320 tiles take them (fc1, fc2 of
-                                       ViT-H); 0: 256x256 tiles only */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);
@@ -170,6 +167,19 @@ int mq_im2col3x3(mq_ctx* ctx, const float* x, int n_img, int height, int width, 
  * convolutions (neck, SWIN-Mask_R-CNN_bbox_only.py:80-89) and the RPN head convolution (rpn_head, :137). */
 int mq_conv3x3_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch, const uint16_t* w,
                     const float* bias, void* out, int cout, int ldc, int epilogue, void* stream);
+
+/* ConvTranspose2d(k4, s2, p1) + per-channel affine (eval BatchNorm) + ReLU as ONE implicit GEMM: the four
+ * output parity classes are 2x2 convolutions over the input (sub-pixel decomposition), their taps gathered
+ * per K-step and the result stored straight into out, bf16 NHWC (n_img, 2 h, 2 w, cout).  x bf16 NHWC
+ * (n_img, h, w, ch), ch % 64 == 0, cout % 256 == 0; w_packed = mq_deconv_subpixel_pack of the torch weight
+ * [ch][cout][4][4]; shift4 = the BatchNorm shift repeated for the 4 classes (4 * cout floats, may be null).
+ * Replaces the head's second deconvolution + col2im (ViTPose HeatmapHead deconv_layers.3/.4/.5,
+ * model/pose/ViTPose_huge_macaque_256x192.py head). */
+int mq_deconv_subpixel_pack(mq_ctx* ctx, const float* w, const float* scale, uint16_t* w_packed, int ch, int cout,
+                            void* stream);
+int mq_deconv_subpixel_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch,
+                            const uint16_t* w_packed, const float* shift4, uint16_t* out, int cout, int relu,
+                            void* stream);
 
 /* float32 -> bfloat16, round to nearest even (count elements). */
 int mq_f32_to_bf16(mq_ctx* ctx, const float* src, uint16_t* dst, int64_t count, void* stream);

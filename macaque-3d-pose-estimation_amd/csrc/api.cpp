@@ -101,6 +101,10 @@ struct mq_vitpose {
   unsigned short *w_patch, *w_dc1, *w_dc2, *w_fin;
   float *b_patch, *pos, *lnf_g, *lnf_b, *b_fin;
   float *bn1_scale, *bn1_shift, *bn2_scale, *bn2_shift;
+  // deconv 2 as one sub-pixel implicit GEMM (dc % 256 == 0): its f32 weights are kept until finalize,
+  // which packs them with the BatchNorm scale folded in (w_dc2) and replicates the shift per class
+  bool dc2_subpixel = false;
+  float *w_dc2_f32 = nullptr, *bn2_shift4 = nullptr;
   std::vector<float> bn_host[8];  // w1,b1,rm1,rv1,w2,b2,rm2,rv2
   int32_t* flip_idx;
   std::map<std::string, ParamSlot> slots;
@@ -154,9 +158,6 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_OPTIM_PRECOND_LDS:
       mq::g_optim_precond_lds = value != 0;
       break;
-    case MQ_TUNE_GEMM_PP_WIDE:
-      mq::g_gemm_pp_wide = value != 0;
-      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -171,7 +172,6 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_OPTIM_PCG_ITERS: return mq::g_optim_pcg_iters;
     case MQ_TUNE_ATTENTION_V2: return mq::g_attention_v2;
     case MQ_TUNE_OPTIM_PRECOND_LDS: return mq::g_optim_precond_lds;
-    case MQ_TUNE_GEMM_PP_WIDE: return mq::g_gemm_pp_wide;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }
@@ -268,7 +268,15 @@ int mq_vitpose_create(mq_ctx* ctx, int D, int L, int H, int FF, int J, mq_vitpos
   size_t o_lnfg = add("backbone.ln1.weight", 1, D, 4);
   size_t o_lnfb = add("backbone.ln1.bias", 1, D, 4);
   size_t o_dc1 = add("head.deconv_layers.0.weight", 2, (int64_t)D * dc * 16, 2, D, dc);
-  size_t o_dc2 = add("head.deconv_layers.3.weight", 2, (int64_t)dc * dc * 16, 2, dc, dc);
+  m->dc2_subpixel = dc % 256 == 0;
+  size_t o_dc2, o_dc2f = 0, o_shift4 = 0;
+  if (m->dc2_subpixel) {
+    o_dc2f = add("head.deconv_layers.3.weight", 1, (int64_t)dc * dc * 16, 4);
+    o_dc2 = take((size_t)dc * dc * 16 * 2);
+    o_shift4 = take((size_t)4 * dc * 4);
+  } else {
+    o_dc2 = add("head.deconv_layers.3.weight", 2, (int64_t)dc * dc * 16, 2, dc, dc);
+  }
   // final 1x1 conv: pad rows to a multiple of 8 is not needed (N masked in the GEMM)
   size_t o_fin = add("head.final_layer.weight", 0, (int64_t)J * dc, 2);
   size_t o_bfin = add("head.final_layer.bias", 1, J, 4);
@@ -324,6 +332,10 @@ int mq_vitpose_create(mq_ctx* ctx, int D, int L, int H, int FF, int J, mq_vitpos
   m->lnf_b = (float*)(base + o_lnfb);
   m->w_dc1 = (unsigned short*)(base + o_dc1);
   m->w_dc2 = (unsigned short*)(base + o_dc2);
+  if (m->dc2_subpixel) {
+    m->w_dc2_f32 = (float*)(base + o_dc2f);
+    m->bn2_shift4 = (float*)(base + o_shift4);
+  }
   m->w_fin = (unsigned short*)(base + o_fin);
   m->b_fin = (float*)(base + o_bfin);
   m->bn1_scale = (float*)(base + o_bn);
@@ -415,6 +427,14 @@ int mq_vitpose_finalize(mq_vitpose* m) {
   }
   HIP_TRY(hipSetDevice(m->ctx->device));
   HIP_TRY(hipMemcpy(m->bn1_scale, ss.data(), ss.size() * 4, hipMemcpyHostToDevice));
+  if (m->dc2_subpixel) {
+    std::vector<float> sh4(4 * m->dc);
+    for (int c = 0; c < 4; ++c)
+      std::memcpy(sh4.data() + c * m->dc, ss.data() + 3 * m->dc, m->dc * sizeof(float));
+    HIP_TRY(hipMemcpy(m->bn2_shift4, sh4.data(), sh4.size() * 4, hipMemcpyHostToDevice));
+    K_TRY(mq::deconv_subpixel_pack(m->w_dc2_f32, m->bn2_scale, m->w_dc2, m->dc, m->dc, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
+  }
   m->finalized = true;
   if (m->gexec) {
     (void)hipGraphExecDestroy(m->gexec);
@@ -452,7 +472,7 @@ static int ensure_workspace(mq_vitpose* m, int F) {
   size_t big = std::max(rows * FF * 2, rows * 16 * dc * 2);  // G and cols1 share
   size_t oG = take(big);
   size_t oY1 = take((size_t)F * 4 * T * dc * 2);
-  size_t oC2 = take((size_t)F * 4 * T * 16 * dc * 2);
+  size_t oC2 = m->dc2_subpixel ? 0 : take((size_t)F * 4 * T * 16 * dc * 2);
   size_t oY2 = take((size_t)F * 16 * T * dc * 2);
   size_t oHM = take((size_t)F * m->J * 16 * T * 4);
   if (m->ws.ensure(off)) return fail("workspace hipMalloc failed", -5);
@@ -464,7 +484,7 @@ static int ensure_workspace(mq_vitpose* m, int F) {
   m->O = (unsigned short*)(b + oO);
   m->G = (unsigned short*)(b + oG);
   m->Y1 = (unsigned short*)(b + oY1);
-  m->cols2 = (unsigned short*)(b + oC2);
+  m->cols2 = m->dc2_subpixel ? nullptr : (unsigned short*)(b + oC2);
   m->Y2 = (unsigned short*)(b + oY2);
   m->hm_all = (float*)(b + oHM);
   m->ws_F = F;
@@ -519,9 +539,18 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
   K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
   K_TRY(mq::deconv_col2im_bn_relu(cols1, m->bn1_scale, m->bn1_shift, m->Y1, F, m->gh, m->gw, dc, s));
   const int rows2 = F * 4 * T;
-  g = mq::GemmArgs{m->Y1, m->w_dc2, m->cols2, nullptr, nullptr, rows2, 16 * dc, dc, dc, dc, 16 * dc, 0};
-  K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
-  K_TRY(mq::deconv_col2im_bn_relu(m->cols2, m->bn2_scale, m->bn2_shift, m->Y2, F, 2 * m->gh, 2 * m->gw, dc, s));
+  if (m->dc2_subpixel) {
+    // deconv2 + BN + ReLU: four sub-pixel 2x2 convolutions in one implicit GEMM, straight into Y2
+    g = mq::GemmArgs{m->Y1, m->w_dc2, m->Y2, m->bn2_shift4, nullptr, rows2, 4 * dc, 4 * dc, dc, 4 * dc, dc, 0};
+    g.conv_h = 2 * m->gh;
+    g.conv_w = 2 * m->gw;
+    g.conv_c = dc;
+    K_TRY(mq::deconv_subpixel_bf16(g, mq::EPI_RELU_BF16, s));
+  } else {
+    g = mq::GemmArgs{m->Y1, m->w_dc2, m->cols2, nullptr, nullptr, rows2, 16 * dc, dc, dc, dc, 16 * dc, 0};
+    K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+    K_TRY(mq::deconv_col2im_bn_relu(m->cols2, m->bn2_scale, m->bn2_shift, m->Y2, F, 2 * m->gh, 2 * m->gw, dc, s));
+  }
   const int rows3 = F * 16 * T;
   float* hm_dst = flip ? m->hm_all : heatmaps;
   g = mq::GemmArgs{m->Y2, m->w_fin, hm_dst, m->b_fin, nullptr, rows3, m->J, dc, dc, dc, m->J, 16 * T};
@@ -682,6 +711,32 @@ int mq_conv3x3_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int w
   g.conv_w = width;
   g.conv_c = ch;
   if (mq::conv3x3_bf16(g, epilogue, (hipStream_t)stream)) return fail("mq_conv3x3_bf16: launch failed", -6);
+  return 0;
+}
+
+int mq_deconv_subpixel_pack(mq_ctx* ctx, const float* w, const float* scale, uint16_t* w_packed, int ch, int cout,
+                            void* stream) {
+  if (!ctx || !w || !w_packed) return fail("mq_deconv_subpixel_pack: null argument");
+  if (ch <= 0 || cout <= 0) return fail("mq_deconv_subpixel_pack: bad sizes", -2);
+  HIP_TRY(hipSetDevice(ctx->device));
+  K_TRY(mq::deconv_subpixel_pack(w, scale, w_packed, ch, cout, (hipStream_t)stream));
+  return 0;
+}
+
+int mq_deconv_subpixel_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch,
+                            const uint16_t* w_packed, const float* shift4, uint16_t* out, int cout, int relu,
+                            void* stream) {
+  if (!ctx || !x || !w_packed || !out) return fail("mq_deconv_subpixel_bf16: null argument");
+  if (n_img <= 0 || height <= 0 || width <= 0 || ch <= 0 || ch % 64 || cout <= 0 || cout % 256)
+    return fail("mq_deconv_subpixel_bf16: bad sizes (ch % 64 == 0, cout % 256 == 0)", -2);
+  HIP_TRY(hipSetDevice(ctx->device));
+  mq::GemmArgs g{(const unsigned short*)x, (const unsigned short*)w_packed, out, shift4, nullptr,
+                 n_img * height * width, 4 * cout, 4 * ch, ch, 4 * ch, cout, 0};
+  g.conv_h = height;
+  g.conv_w = width;
+  g.conv_c = ch;
+  if (mq::deconv_subpixel_bf16(g, relu ? mq::EPI_RELU_BF16 : mq::EPI_BF16, (hipStream_t)stream))
+    return fail("mq_deconv_subpixel_bf16: launch failed", -6);
   return 0;
 }
 

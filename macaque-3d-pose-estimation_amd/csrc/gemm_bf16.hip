@@ -574,6 +574,16 @@ int conv3x3_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   return gemm_pingpong_conv(p, epi, g_num_cus, stream);
 }
 
+int deconv_subpixel_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
+  if (!g_num_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
+      g_num_cus = 256;
+  }
+  return gemm_pingpong_deconv(p, epi, g_num_cus, stream);
+}
+
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return -1;
   if ((p.lda % 8) || (p.ldw % 8)) return -2;

@@ -35,23 +35,17 @@
 // Accumulation order per output element is the one of gemm256_kernel (K in ascending 32-deep
 // MFMA steps, then + bias, then the epilogue op), so both kernels give bit-identical results.
 //
-// Two tile shapes share the kernel (template PPShape<WMF, WNF>: fragments per wave in M and N):
-//   256 x 256 (8 x 4 fragments per wave, the table above);
-//   192 x 320 (6 x 5 fragments, wave block 96 x 80): 61,440 outputs per tile instead of 65,536, which
-//     fits the ViT-H shapes into whole rounds of the 256 CUs -- fc1 1,024 tiles = 4 rounds (256 x 256:
-//     960 = 3.75 rounds, the last one a quarter idle), fc2 256 = 1 round (240).  Same 64 KiB stage,
-//     LDS reads per MAC within 2 %, DMA bytes per MAC +7 %.  Routed only where measured faster
-//     (pp_use_wide).
-//     Phases: quadrants of 3 x 3 / 3 x 2 / 3 x 3 / 3 x 2 fragments (18 / 12 / 18 / 12 MFMAs); the 64
-//     DMA groups of a stage are issued 3 / 2 / 2 / 1 per wave per phase in first-read order (P0 in
-//     phases 0-1, P1 by phase 2, P2 by phase 3), which keeps every wait a compile-time count.
+// The tile geometry is a template (PPShape<WMF, WNF>: MFMA fragments per wave in M and N, phase split,
+// DMA issue plan and counted waits derived from it); the library instantiates 256 x 256.  A 192 x 320
+// shape (6 x 5 fragments per wave, 18 / 12 / 18 / 12 MFMAs per phase, DMA plan 3 / 2 / 2 / 1) fills whole
+// CU rounds for fc1 / qkv / fc2 / proj but measured 1 % slower end to end in the ViT-H forward
+// (profiles/r03d_vit_probe_wide_tiles.log), so it is not built.
 #include "common.hpp"
 #include "kernels.hpp"
 
 namespace mq {
 
 int g_gemm_pingpong = 1;
-int g_gemm_pp_wide = 1;
 
 constexpr int PP_BK = 64, PP_T = 512;
 constexpr int PP_STAGE = 64 * 1024;   // one BK slice of the A and W tiles (both shapes: (BM + BN) x 128 B)
@@ -88,7 +82,6 @@ struct PPShape {
   static constexpr int STORES_F32 = WMF * WNF;
 };
 using Shape256 = PPShape<8, 4>;
-using Shape320 = PPShape<6, 5>;
 
 namespace {
 
@@ -166,7 +159,10 @@ __device__ __forceinline__ int pp_slot_group(int w, int i) {
 
 // Epilogue of one wave's (16 WMF) x (16 WNF) block: acc[i][j] holds C[m0 + wm*BM/2 + i*16 + (l & 15)]
 // [n0 + wn*16*WNF + j*16 + 4*(l >> 4) + e].  Zeroes the accumulators for the next tile.
-template <int EPI, class S>
+//
+// Sub-pixel deconvolution (DECONV): GEMM row m = input pixel (img, y, x) and column n = class (py, px)
+// x C_out + co store to output pixel (img, 2y + py, 2x + px), channel co, of the NHWC (2H, 2W) image.
+template <int EPI, class S, bool DECONV = false>
 __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::WMF][S::WNF], const float* bias_lds,
                                             int m0, int n0, int wm, int wn, int lane) {
   constexpr int WMF = S::WMF, WNF = S::WNF;
@@ -200,6 +196,23 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
 #pragma unroll
   for (int j = 0; j < WNF; ++j) bias[j] = make_float4(bv[j][0], bv[j][1], bv[j][2], bv[j][3]);
   const bool full = (m0 + S::BM <= p.M) && (n0 + S::BN <= p.N);
+  // C row of GEMM row m, column offset of the tile
+  int dc_cls = 0, dc_col = 0;
+  if constexpr (DECONV) {
+    const int cout = p.N >> 2;
+    dc_cls = n0 / cout;
+    dc_col = dc_cls * cout;
+  }
+  auto crow = [&](int m) -> size_t {
+    if constexpr (DECONV) {
+      const int hw = p.conv_h * p.conv_w;
+      const int img = m / hw, rem = m - img * hw;
+      const int y = rem / p.conv_w, x = rem - y * p.conv_w;
+      return ((size_t)img * 2 * p.conv_h + 2 * y + (dc_cls >> 1)) * (2 * p.conv_w) + 2 * x + (dc_cls & 1);
+    } else {
+      return (size_t)m;
+    }
+  };
   if constexpr (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) {
     auto act = [&](int i, int j, float (&v)[4]) {
       v[0] = acc[i][j][0] + bias[j].x;
@@ -226,6 +239,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
 #pragma unroll
     for (int i = 0; i < WMF; ++i) {
       const int m = mb + i * 16 + mm;
+      bf16_t* crow_p = (bf16_t*)p.C + crow(m < p.M ? m : 0) * p.ldc - dc_col;
 #pragma unroll
       for (int jp = 0; jp + 1 < WNF; jp += 2) {
         unsigned pk[2][2];
@@ -241,14 +255,14 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
         // even lanes: [own tile j | neighbour's tile j]; odd: [neighbour's j+1 | own j+1]
         const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         const int n = nb + (jp + (odd ? 1 : 0)) * 16 + nbase;
-        if (full || (m < p.M && n < p.N)) *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
+        if (full || (m < p.M && n < p.N)) *reinterpret_cast<uint4*>(crow_p + n) = o;
       }
       if constexpr (WNF & 1) {
         float v[4];
         act(i, WNF - 1, v);
         const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         const int n = nb + (WNF - 1) * 16 + nn;
-        if (full || (m < p.M && n < p.N)) *reinterpret_cast<uint2*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
+        if (full || (m < p.M && n < p.N)) *reinterpret_cast<uint2*>(crow_p + n) = o;
       }
     }
     return;
@@ -315,10 +329,15 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
   }
 }
 
-template <int EPI, bool CONV, int WMF_, int WNF_>
+// A-operand modes of the kernel
+enum PPMode { PP_GEMM = 0, PP_CONV3 = 1, PP_DECONV = 2 };
+
+template <int EPI, int MODE, int WMF_, int WNF_>
 __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_m, int tiles_n) {
   using S = PPShape<WMF_, WNF_>;
+  constexpr bool CONV = MODE != PP_GEMM;
   static_assert(!CONV || S::WNF == 4, "implicit convolution: 256 x 256 tiles only");
+  static_assert(MODE != PP_DECONV || EPI == EPI_RELU_BF16 || EPI == EPI_BF16, "deconvolution: bf16 NHWC output");
   constexpr int WMF = S::WMF, WNF = S::WNF, QM = S::QM, NA = S::NA, NB = S::NB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
@@ -366,9 +385,16 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   // implicit convolution: per A slot the output pixel's (y, x) (packed y << 16 | x); voff then holds the
   // element offset of the tap-centre row + this lane's chunk, and the tap shift is added at issue time
   unsigned cyx[8];
+  // sub-pixel deconvolution: output parity class (py, px) of the issue tile (N = 4 classes x C_out)
+  int iss_py = 0, iss_px = 0;
   auto set_tile_ptrs = [&](int ti) {
     int m0, n0;
     pp_tile_coords<S>(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
+    if constexpr (MODE == PP_DECONV) {
+      const int cls = n0 / (p.N >> 2);
+      iss_py = cls >> 1;
+      iss_px = cls & 1;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int row = grow[i] + (lane >> 3);
@@ -400,10 +426,19 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     char* dst = smem + slot * PP_STAGE + sdst[i];
     if (CONV && !gw[i]) {
       // K-step iss_k = tap * (C / 64) + c64: the tap's shifted pixel, channels 64 c64 .. + 63; a pixel
-      // outside the image gets an offset past the buffer end, which the DMA turns into zeros (padding)
+      // outside the image gets an offset past the buffer end, which the DMA turns into zeros (padding).
+      // 3x3: tap = (ky, kx), shift (ky - 1, kx - 1).  Sub-pixel deconvolution: tap = (a, b) of the
+      // class's 2 x 2 kernel taps, input shift (py - a, px - b) (see deconv_subpixel_pack_kernel).
       const int kpt = p.conv_c >> 6;
       const int tap = iss_k / kpt;
-      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+      int dy, dx;
+      if constexpr (MODE == PP_DECONV) {
+        dy = iss_py - (tap >> 1);
+        dx = iss_px - (tap & 1);
+      } else {
+        dy = tap / 3 - 1;
+        dx = tap - (tap / 3) * 3 - 1;
+      }
       const int y = (int)(cyx[i] >> 16) + dy, x = (int)(cyx[i] & 0xffffu) + dx;
       const bool inside = (unsigned)y < (unsigned)p.conv_h && (unsigned)x < (unsigned)p.conv_w;
       const unsigned off = (unsigned)((int)voff[i] + (dy * p.conv_w + dx) * p.conv_c + (iss_k - tap * kpt) * 64);
@@ -545,7 +580,8 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     mfma_quadrant(1, b1, NA, NBc{});
     bar();
     if (++kt == nk) {
-      pp_epilogue<EPI, S>(p, acc, reinterpret_cast<const float*>(bias_lds), cm0, cn0, wm, wn, lane);
+      pp_epilogue<EPI, S, MODE == PP_DECONV>(p, acc, reinterpret_cast<const float*>(bias_lds), cm0, cn0, wm, wn,
+                                             lane);
       stores_pending = (cm0 + S::BM <= p.M) && (cn0 + S::BN <= p.N);
       kt = 0;
       ++ct;
@@ -559,15 +595,15 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-template <int EPI, bool CONV, class S>
+template <int EPI, int MODE, class S>
 void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, CONV, S::WMF, S::WNF>,
+    (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, MODE, S::WMF, S::WNF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm_pp_kernel<EPI, CONV, S::WMF, S::WNF>), grid, dim3(PP_T), S::LDS, stream, p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_pp_kernel<EPI, MODE, S::WMF, S::WNF>), grid, dim3(PP_T), S::LDS, stream, p, tiles_m, tiles_n);
 }
 
 template <class S>
@@ -577,32 +613,18 @@ int tiles_of(const GemmArgs& p, int& tm, int& tn) {
   return tm * tn;
 }
 
-// 192 x 320 tiles where they need fewer CU-rounds of work (persistent rounds x outputs per tile, with
-// a 3 % margin for the wider tile's extra DMA bytes) AND measured faster per MAC: the GELU epilogue
-// (fc1: 1.5 % faster) and the residual at K >= 2048 (fc2: 0.4 %).  Measured slower, so not routed
-// here (profiles/r03b_ab_gemm_wide_tiles.log): the plain bf16 epilogue (qkv -1.5..-6 %) and the
-// short-K residual (proj, 1-10 % behind the interleaved kernel) -- the 18/12/18/12-MFMA phases leave
-// the 12-MFMA segments shorter than the partner's heaviest load segment.
-bool pp_use_wide(const GemmArgs& p, int epi, int num_cus) {
-  if (!g_gemm_pp_wide || !(epi == EPI_GELU_BF16 || (epi == EPI_RESID_F32 && p.K >= 2048))) return false;
-  int tm, tn;
-  const long t256 = tiles_of<Shape256>(p, tm, tn), t320 = tiles_of<Shape320>(p, tm, tn);
-  const long r256 = (t256 + num_cus - 1) / num_cus, r320 = (t320 + num_cus - 1) / num_cus;
-  return r320 * (Shape320::BM * Shape320::BN) * 100 < r256 * (Shape256::BM * Shape256::BN) * 97;
-}
-
 template <class S>
 int launch_shape(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
   int tiles_m, tiles_n;
   const int tiles = tiles_of<S>(p, tiles_m, tiles_n);
   dim3 grid(tiles < num_cus ? tiles : num_cus);
   switch (epi) {
-    case EPI_BF16: launch_pp<EPI_BF16, false, S>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16, false, S>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, false, S>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RESID_F32: launch_pp<EPI_RESID_F32, false, S>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_POS_F32: launch_pp<EPI_POS_F32, false, S>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_F32: launch_pp<EPI_F32, false, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_BF16: launch_pp<EPI_BF16, PP_GEMM, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16, PP_GEMM, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, PP_GEMM, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RESID_F32: launch_pp<EPI_RESID_F32, PP_GEMM, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_POS_F32: launch_pp<EPI_POS_F32, PP_GEMM, S>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_F32: launch_pp<EPI_F32, PP_GEMM, S>(grid, stream, p, tiles_m, tiles_n); break;
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;
@@ -624,9 +646,30 @@ int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stre
   const int tiles = tiles_of<Shape256>(p, tiles_m, tiles_n);
   dim3 grid(tiles < num_cus ? tiles : num_cus);
   switch (epi) {
-    case EPI_BF16: launch_pp<EPI_BF16, true, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, true, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
-    case EPI_F32: launch_pp<EPI_F32, true, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_BF16: launch_pp<EPI_BF16, PP_CONV3, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, PP_CONV3, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_F32: launch_pp<EPI_F32, PP_CONV3, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+// ConvTranspose2d(k4, s2, p1) as four sub-pixel 2x2 convolutions in ONE launch: output parity class
+// (py, px) = N tile / C_out, its 2 x 2 taps gathered like the 3x3 implicit convolution, the result
+// stored straight into the NHWC (2H, 2W) image (no 16-tap column buffer, no col2im pass).
+int gemm_pingpong_deconv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
+  const int cout = p.N / 4;
+  if (p.conv_c <= 0 || p.conv_c % PP_BK || p.K != 4 * p.conv_c || p.lda != p.conv_c || p.N % 4 ||
+      cout % Shape256::BN || p.ldw != p.K || p.ldc != cout || p.conv_h <= 0 || p.conv_w <= 0 ||
+      p.M % (p.conv_h * p.conv_w) || p.conv_w >= 65536 || p.conv_h >= 65536 ||
+      (size_t)p.M * p.lda * 2 >= (1ull << 31) || (size_t)p.N * p.ldw * 2 >= (1ull << 31))
+    return -1;
+  int tiles_m, tiles_n;
+  const int tiles = tiles_of<Shape256>(p, tiles_m, tiles_n);
+  dim3 grid(tiles < num_cus ? tiles : num_cus);
+  switch (epi) {
+    case EPI_BF16: launch_pp<EPI_BF16, PP_DECONV, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
+    case EPI_RELU_BF16: launch_pp<EPI_RELU_BF16, PP_DECONV, Shape256>(grid, stream, p, tiles_m, tiles_n); break;
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;
@@ -643,8 +686,7 @@ bool gemm_pingpong_fits(const GemmArgs& p, int epi, int num_cus) {
 }
 
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
-  return pp_use_wide(p, epi, num_cus) ? launch_shape<Shape320>(p, epi, num_cus, stream)
-                                 : launch_shape<Shape256>(p, epi, num_cus, stream);
+  return launch_shape<Shape256>(p, epi, num_cus, stream);
 }
 
 }  // namespace mq

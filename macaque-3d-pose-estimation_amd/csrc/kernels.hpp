@@ -33,15 +33,18 @@ struct GemmArgs {
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 // implicit-GEMM 3x3 convolution (ping-pong kernel only; conv_c % 64 == 0)
 int conv3x3_bf16(const GemmArgs& p, int epi, hipStream_t stream);
+// ConvTranspose2d(k4, s2, p1) as one sub-pixel implicit GEMM (ping-pong kernel): A = NHWC input
+// (conv_h x conv_w x conv_c), W = deconv_subpixel_pack output [4 classes x C_out][4 taps x conv_c],
+// bias [4 x C_out], C = NHWC (2 conv_h x 2 conv_w x C_out) bf16; C_out % 256 == 0, conv_c % 64 == 0
+int deconv_subpixel_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 // routing knobs (mq_set_tuning): both settings give correct results
 extern bool g_gemm_force_small;  // every GEMM on the 128x128 kernel
 // ping-pong 256x256 kernel (gemm_pp.hip): the two wave groups of a block alternate LDS traffic and MFMA
 extern int g_gemm_pingpong;
-// 192x320 ping-pong tiles where they fill whole CU rounds and measured faster (gemm_pp.hip pp_use_wide)
-extern int g_gemm_pp_wide;
 bool gemm_pingpong_fits(const GemmArgs& p, int epi, int num_cus);
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
+int gemm_pingpong_deconv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
@@ -57,6 +60,8 @@ int deconv_col2im_bn_relu(const unsigned short* cols, const float* scale, const 
                           int n_img, int in_h, int in_w, int ch, hipStream_t s);
 int convert_f32_bf16(const float* src, unsigned short* dst, int64_t n, hipStream_t s);
 int deconv_weight_pack(const float* w, unsigned short* dst, int cin, int cout, hipStream_t s);
+// [cin][cout][4][4] f32 (x scale[co] when scale != null) -> sub-pixel GEMM weights (deconv_subpixel_bf16)
+int deconv_subpixel_pack(const float* w, const float* scale, unsigned short* dst, int cin, int cout, hipStream_t s);
 
 // image ops (imgproc.hip)
 int crop_udp(const uint8_t* frames, int64_t frame_stride, int img_h, int img_w, const float* boxes,

@@ -682,4 +682,32 @@ int deconv_weight_pack(const float* w, unsigned short* dst, int cin, int cout, h
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// torch ConvTranspose2d(k4, s2, p1) weight [cin][cout][4][4] with the eval-BatchNorm scale folded in ->
+// the sub-pixel GEMM operand [(cls * cout + co)][tap * cin + ci].  Output pixel (2y + py, 2x + px) takes
+// input (y + dy, x + dx) through kernel tap (ky, kx) exactly when oy = 2 iy - 1 + ky, i.e. for class py
+// the taps a = 0, 1: ky = (1 - py) + 2a at dy = py - a (py = 0: ky 1, 3 at dy 0, -1; py = 1: ky 0, 2 at
+// dy +1, 0); likewise x.  tap = 2a + b.
+__global__ void deconv_subpixel_pack_kernel(const float* __restrict__ w, const float* __restrict__ scale,
+                                            bf16_t* __restrict__ dst, int cin, int cout) {
+  const int64_t total = (int64_t)16 * cin * cout;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % cin);
+    const int tap = (int)((i / cin) % 4);
+    const int64_t row = i / (4 * (int64_t)cin);
+    const int co = (int)(row % cout);
+    const int cls = (int)(row / cout);
+    const int ky = (1 - (cls >> 1)) + 2 * (tap >> 1), kx = (1 - (cls & 1)) + 2 * (tap & 1);
+    const float v = w[((int64_t)ci * cout + co) * 16 + ky * 4 + kx];
+    dst[i] = f32_to_bf16(scale ? v * scale[co] : v);
+  }
+}
+
+int deconv_subpixel_pack(const float* w, const float* scale, unsigned short* dst, int cin, int cout, hipStream_t s) {
+  const int64_t total = (int64_t)16 * cin * cout;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(deconv_subpixel_pack_kernel, dim3(blocks), dim3(256), 0, s, w, scale, dst, cin, cout);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 }  // namespace mq

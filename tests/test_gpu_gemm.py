@@ -103,21 +103,17 @@ def _run_pair(M, N, K, epi, aux_rows, seed=0):
     if epi in (0, 1, 6):
         C0 = C0.to(torch.bfloat16)
     outs = []
-    old = ctx.lib.mq_get_tuning(12), ctx.lib.mq_get_tuning(19)
+    old = ctx.lib.mq_get_tuning(12)
     try:
-        # interleaved kernel; ping-pong with 256x256 tiles only; ping-pong with 192x320 tiles where they
-        # fill whole CU rounds (MQ_TUNE_GEMM_PP_WIDE)
-        for pp, wide in ((0, 0), (1, 0), (1, 1)):
+        for pp in (0, 1):
             assert ctx.lib.mq_set_tuning(12, pp) == 0
-            assert ctx.lib.mq_set_tuning(19, wide) == 0
             Cm = C0.clone()
             _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), _lib.ptr(bias),
                                             _lib.ptr(aux), M, N, K, K, K, N, aux_rows, epi, _lib.stream_ptr()),
                        "mq_gemm_bf16")
             outs.append(Cm)
     finally:
-        ctx.lib.mq_set_tuning(12, old[0])
-        ctx.lib.mq_set_tuning(19, old[1])
+        ctx.lib.mq_set_tuning(12, old)
     torch.cuda.synchronize()
     return outs
 
@@ -135,7 +131,6 @@ def test_gemm_pingpong_bitwise_equals_interleaved(epi, M, N, K):
     outs = _run_pair(M, N, K, epi, aux_rows=192)
     bits = [o.view(torch.int16) if o.dtype == torch.bfloat16 else o.view(torch.int32) for o in outs]
     assert torch.equal(bits[0], bits[1])
-    assert torch.equal(bits[0], bits[2])
 
 
 def test_gemm_force_small_matches_fp32():

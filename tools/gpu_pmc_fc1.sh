@@ -1,4 +1,4 @@
-# rocprofv3 PMC passes over the fc1 GEMM (gemm_pp_kernel<1, false, 6, 5>: GELU epilogue, 192x320 tiles) of the ViT-H bench shape, one counter
+# rocprofv3 PMC passes over the fc1 GEMM (gemm_pp_kernel<1, 0, 8, 4>: GELU epilogue, GEMM mode, 256x256 tiles) of the ViT-H bench shape, one counter
 # group per pass (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass), then the
 # per-launch summary with the gfx950 corrections -> gpurun_out/$OUT/pmc_fc1_gemm.json.
 set -o pipefail
@@ -13,5 +13,5 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE
   timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/$OUT/p$i -o run -- python3 $GRAFT_REPO_ROOT/tools/gemm_probe.py --iters 5 --shape fc1 --variants pp > gpurun_out/$OUT/p$i.log 2>&1 || { echo "PMC pass $i ($grp) failed"; tail -5 gpurun_out/$OUT/p$i.log; exit 1; }
   echo "PMC pass $i ($grp) ok"
 done
-python3 tools/pmc_summary.py gpurun_out/$OUT "gemm_pp_kernel<1, false, 6, 5>" 170414080 161061273600 > gpurun_out/$OUT/pmc_fc1_gemm.json
+python3 tools/pmc_summary.py gpurun_out/$OUT "gemm_pp_kernel<1, 0, 8, 4>" 170414080 161061273600 > gpurun_out/$OUT/pmc_fc1_gemm.json
 head -40 gpurun_out/$OUT/pmc_fc1_gemm.json

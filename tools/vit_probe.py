@@ -19,9 +19,18 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--knob", default="17=1,0", help="KEY=V1,V2,... (default: attention v2 vs v1)")
     ap.add_argument("--crops", type=int, default=32)
+    ap.add_argument("--lib", default=None, help="another build of libmq_hip.so (A/B across builds)")
     args = ap.parse_args()
     import torch
     from mqhip import _lib
+    if args.lib:
+        # an older build may lack newer entry points: bind only the ones it exports
+        import ctypes
+        probe = ctypes.CDLL(os.path.abspath(args.lib))
+        for name in list(_lib._SIGS):
+            if not hasattr(probe, name):
+                del _lib._SIGS[name]
+        _lib.load(os.path.abspath(args.lib))  # first load wins: every later load() returns this build
     from mqhip.pose import VitPoseHip
     from mqhip.weights import VIT_H, make_random_weights
 
