@@ -50,6 +50,8 @@ const char* mq_last_error(void);
                                         fits; 0: the global-memory substitution kernel (same preconditioner) */
 #define MQ_TUNE_ATTENTION_V2 17     /* 1 (default): attention on 16x16x32 QK^T + transposed-output PV (vit_ops.hip
                                        attention2_kernel); 0: the first-generation kernel */
+#define MQ_TUNE_GEMM_TILE64 19      /* 1 (default): GEMMs whose 128x128 tiles cannot occupy every CU once take the
+                                       64x64-tile kernel (same accumulation order, tested equal); 0: 128x128 */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

@@ -158,6 +158,9 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_OPTIM_PRECOND_LDS:
       mq::g_optim_precond_lds = value != 0;
       break;
+    case MQ_TUNE_GEMM_TILE64:
+      mq::g_gemm_tile64 = value != 0;
+      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -172,6 +175,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_OPTIM_PCG_ITERS: return mq::g_optim_pcg_iters;
     case MQ_TUNE_ATTENTION_V2: return mq::g_attention_v2;
     case MQ_TUNE_OPTIM_PRECOND_LDS: return mq::g_optim_precond_lds;
+    case MQ_TUNE_GEMM_TILE64: return mq::g_gemm_tile64;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }

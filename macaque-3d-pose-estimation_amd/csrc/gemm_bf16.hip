@@ -4,8 +4,11 @@
 // operand order of v_mfma_f32_16x16x32_bf16: lane l reads 16 contiguous bytes of
 // row (l & 15) at k = 8*(l >> 4) for A and of W-row (l & 15) for B.
 //
-// Block tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 = 4x4 MFMA
-// tiles.  Tiles are staged HBM -> LDS with global_load_lds_dwordx4 (no VGPR
+// Block tile (32 WF)^2 x 64, 256 threads = 4 waves (2x2), each wave (16 WF)^2 = WF x WF MFMA tiles:
+// WF = 4 gives 128x128 tiles, WF = 2 gives 64x64 tiles for GEMMs too small to fill the CUs with
+// 128x128 ones (the ID classifier's stage-3/4 convolutions at a frame's dozen boxes, the detector's
+// late Swin stages).  Both accumulate every output in the same order (K ascending, 32 per MFMA), so
+// they agree bit for bit.  Tiles are staged HBM -> LDS with global_load_lds_dwordx4 (no VGPR
 // round trip), double buffered: the next K-tile's DMA is issued before the
 // current tile's MFMAs.  The LDS image is XOR-swizzled on the SOURCE address
 // (16-B chunk c of row r lives at slot c ^ ((r >> 1) & 7)); the ds_read_b128
@@ -19,10 +22,10 @@
 namespace mq {
 
 bool g_gemm_force_small = false;
+int g_gemm_tile64 = 1;
 
 constexpr int BM = 128, BN = 128, BK = 64;
 constexpr int GEMM_THREADS = 256;
-constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand tile
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -30,13 +33,14 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
-// Issue the DMA of one 128x64 bf16 tile (rows [r0, r0+128) of a K-contiguous
-// matrix with leading dimension ld, columns [k0, k0+64)) into LDS.
+// Issue the DMA of one (32 WF)x64 bf16 tile (rows [r0, r0 + 32 WF) of a K-contiguous
+// matrix with leading dimension ld, columns [k0, k0+64)) into LDS: WF 8-row groups per wave.
+template <int WF>
 __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int ld, int r0, int rmax, int k0,
                                            char* lds_tile, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int rbase = (wave * 4 + i) * 8;
+  for (int i = 0; i < WF; ++i) {
+    int rbase = (wave * WF + i) * 8;
     int row = rbase + (lane >> 3);
     int slot = lane & 7;
     int chunk = slot ^ swz(row);
@@ -51,8 +55,11 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds_tile, int row, int c
   return *reinterpret_cast<const bf16x8*>(lds_tile + row * 128 + ((chunk ^ swz(row)) << 4));
 }
 
-template <int EPI>
+template <int EPI, int WF>
 __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) {
+  constexpr int TM = 32 * WF;                // tile rows = tile columns
+  constexpr int TB = TM * BK * 2;            // bytes per operand tile
+  constexpr int WT = 16 * WF;                // wave tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -65,21 +72,21 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
   const int xcd = bid & 7;
   const int q = nwg >> 3, r = nwg & 7;
   const int wid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_m = (p.M + TM - 1) / TM;
   const int tm = wid % tiles_m;
   const int tn = wid / tiles_m;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * TM, n0 = tn * TM;
 
 
-  f32x4 acc[4][4];
+  f32x4 acc[WF][WF];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < WF; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < WF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / BK;
-  stage_tile(p.A, p.lda, m0, p.M, 0, smem, wave, lane);
-  stage_tile(p.W, p.ldw, n0, p.N, 0, smem + TILE_BYTES, wave, lane);
+  stage_tile<WF>(p.A, p.lda, m0, p.M, 0, smem, wave, lane);
+  stage_tile<WF>(p.W, p.ldw, n0, p.N, 0, smem + TB, wave, lane);
   __syncthreads();
 
   const int frow = lane & 15;
@@ -87,23 +94,23 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
   for (int t = 0; t < nk; ++t) {
     const int cur = t & 1;
     if (t + 1 < nk) {
-      char* nxt = smem + (cur ^ 1) * 2 * TILE_BYTES;
-      stage_tile(p.A, p.lda, m0, p.M, (t + 1) * BK, nxt, wave, lane);
-      stage_tile(p.W, p.ldw, n0, p.N, (t + 1) * BK, nxt + TILE_BYTES, wave, lane);
+      char* nxt = smem + (cur ^ 1) * 2 * TB;
+      stage_tile<WF>(p.A, p.lda, m0, p.M, (t + 1) * BK, nxt, wave, lane);
+      stage_tile<WF>(p.W, p.ldw, n0, p.N, (t + 1) * BK, nxt + TB, wave, lane);
     }
-    const char* As = smem + cur * 2 * TILE_BYTES;
-    const char* Bs = As + TILE_BYTES;
+    const char* As = smem + cur * 2 * TB;
+    const char* Bs = As + TB;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 a[4], b[4];
+      bf16x8 a[WF], b[WF];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = read_frag(As, wm * 64 + i * 16 + frow, kk * 4 + fk);
+      for (int i = 0; i < WF; ++i) a[i] = read_frag(As, wm * WT + i * 16 + frow, kk * 4 + fk);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = read_frag(Bs, wn * 64 + j * 16 + frow, kk * 4 + fk);
+      for (int j = 0; j < WF; ++j) b[j] = read_frag(Bs, wn * WT + j * 16 + frow, kk * 4 + fk);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < WF; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < WF; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     __syncthreads();
@@ -113,15 +120,15 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
   const int ccol = lane & 15;
   const int crow = (lane >> 4) * 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wn * 64 + j * 16 + ccol;
+  for (int j = 0; j < WF; ++j) {
+    const int n = n0 + wn * WT + j * 16 + ccol;
     if (n >= p.N) continue;
     const float bias = p.bias ? p.bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < WF; ++i) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int m = m0 + wm * 64 + i * 16 + crow + e;
+        const int m = m0 + wm * WT + i * 16 + crow + e;
         if (m >= p.M) continue;
         float v = acc[i][j][e] + bias;
         if constexpr (EPI == EPI_BF16) {
@@ -584,6 +591,25 @@ int deconv_subpixel_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   return gemm_pingpong_deconv(p, epi, g_num_cus, stream);
 }
 
+template <int WF>
+static int launch_small(const GemmArgs& p, int epi, hipStream_t stream) {
+  constexpr int TM = 32 * WF;
+  const int tiles = ((p.M + TM - 1) / TM) * ((p.N + TM - 1) / TM);
+  dim3 grid(tiles), block(GEMM_THREADS);
+  const size_t lds = 4 * (size_t)TM * BK * 2;
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_BF16, WF>), grid, block, lds, stream, p); break;
+    case EPI_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_GELU_BF16, WF>), grid, block, lds, stream, p); break;
+    case EPI_RELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RELU_BF16, WF>), grid, block, lds, stream, p); break;
+    case EPI_RESID_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RESID_F32, WF>), grid, block, lds, stream, p); break;
+    case EPI_POS_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_POS_F32, WF>), grid, block, lds, stream, p); break;
+    case EPI_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_F32, WF>), grid, block, lds, stream, p); break;
+    case EPI_NCHW_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_NCHW_F32, WF>), grid, block, lds, stream, p); break;
+    default: return -3;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return -1;
   if ((p.lda % 8) || (p.ldw % 8)) return -2;
@@ -601,20 +627,17 @@ int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
     if (p.K % B2K == 0 && epi != EPI_NCHW_F32 && (p.N % 4) == 0 && (p.ldc % 4) == 0) return gemm256(p, epi, stream);
     return -1;
   }
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  dim3 grid(tiles), block(GEMM_THREADS);
-  const size_t lds = 4 * TILE_BYTES;
-  switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_BF16>, grid, block, lds, stream, p); break;
-    case EPI_GELU_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_GELU_BF16>, grid, block, lds, stream, p); break;
-    case EPI_RELU_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_RELU_BF16>, grid, block, lds, stream, p); break;
-    case EPI_RESID_F32: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_RESID_F32>, grid, block, lds, stream, p); break;
-    case EPI_POS_F32: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_POS_F32>, grid, block, lds, stream, p); break;
-    case EPI_F32: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_F32>, grid, block, lds, stream, p); break;
-    case EPI_NCHW_F32: hipLaunchKernelGGL(gemm_bf16_kernel<EPI_NCHW_F32>, grid, block, lds, stream, p); break;
-    default: return -3;
+  if (!g_num_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
+      g_num_cus = 256;
   }
-  return hipGetLastError() == hipSuccess ? 0 : -4;
+  // 64x64 tiles when 128x128 ones cannot occupy every CU once (and K is long enough to be worth it)
+  const int tiles128 = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  if (g_gemm_tile64 && tiles128 < g_num_cus && p.K >= 256) return launch_small<2>(p, epi, stream);
+  return launch_small<4>(p, epi, stream);
 }
+
 
 }  // namespace mq

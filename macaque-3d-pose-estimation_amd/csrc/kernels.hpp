@@ -39,6 +39,7 @@ int conv3x3_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 int deconv_subpixel_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 // routing knobs (mq_set_tuning): both settings give correct results
 extern bool g_gemm_force_small;  // every GEMM on the 128x128 kernel
+extern int g_gemm_tile64;        // 64x64 tiles for GEMMs that cannot fill the CUs with 128x128 ones
 // ping-pong 256x256 kernel (gemm_pp.hip): the two wave groups of a block alternate LDS traffic and MFMA
 extern int g_gemm_pingpong;
 bool gemm_pingpong_fits(const GemmArgs& p, int epi, int num_cus);

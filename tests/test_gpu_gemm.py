@@ -167,3 +167,57 @@ def test_gemm_rejects_bad_k():
     rc = ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), None, None, 64, 64, 40, 40, 40, 64,
                               0, 4, _lib.stream_ptr())
     assert rc != 0
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("M,N,K", [(2548, 256, 2304), (637, 512, 4608), (2548, 1024, 256), (100, 2048, 512),
+                                   (1000, 96, 320), (50, 17, 1024)])
+def test_gemm_tile64_bitwise_equals_tile128(epi, M, N, K):
+    """GEMMs too small to occupy every CU with 128x128 tiles (the ID classifier's stage-3/4 convolutions
+    at a frame's dozen boxes) run on 64x64 tiles: same K order per output, so the bits of the 128x128
+    kernel (MQ_TUNE_GEMM_TILE64 = 0), and within the bf16 tolerance of the fp32 product."""
+    import torch
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(M + N + K)
+    A = torch.randn((M, K), generator=g, device="cuda").to(torch.bfloat16)
+    W = (torch.randn((N, K), generator=g, device="cuda") / K ** 0.5).to(torch.bfloat16)
+    bias = torch.randn((N,), generator=g, device="cuda")
+    aux_rows = 7 if epi == 5 else 3
+    aux = torch.randn((aux_rows, N), generator=g, device="cuda")
+    C0 = torch.randn((M, N), generator=g, device="cuda")
+    if epi in (0, 1, 6):
+        C0 = C0.to(torch.bfloat16)
+    if epi == 5:
+        M = (M // aux_rows) * aux_rows
+        A, C0 = A[:M].contiguous(), torch.zeros((M, N), device="cuda")
+    outs = []
+    old = ctx.lib.mq_get_tuning(19)
+    try:
+        for t64 in (0, 1):
+            assert ctx.lib.mq_set_tuning(19, t64) == 0
+            Cm = C0.clone()
+            _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(A), _lib.ptr(W), _lib.ptr(Cm), _lib.ptr(bias),
+                                            _lib.ptr(aux), M, N, K, K, K, N, aux_rows, epi, _lib.stream_ptr()),
+                       "mq_gemm_bf16")
+            outs.append(Cm)
+    finally:
+        ctx.lib.mq_set_tuning(19, old)
+    torch.cuda.synchronize()
+    bits = [o.view(torch.int16) if o.dtype == torch.bfloat16 else o.view(torch.int32) for o in outs]
+    assert torch.equal(bits[0], bits[1])
+    prod = A.float() @ W.float().t() + bias
+    if epi == 1:
+        prod = torch.nn.functional.gelu(prod)
+    elif epi == 6:
+        prod = prod.clamp_min(0)
+    elif epi == 2:
+        prod = prod + C0
+    elif epi == 3:
+        prod = prod + aux[torch.arange(M, device="cuda") % aux_rows]
+    got = outs[1].float()
+    if epi == 5:  # NCHW: out[img][n][pix]
+        got = got.view(M // aux_rows, N, aux_rows).permute(0, 2, 1).reshape(M, N)
+    tol = 2e-3 * prod.abs().max().item() + (0.01 * prod.abs().max().item() if epi in (0, 1, 6) else 0.0)
+    assert (got - prod).abs().max().item() <= tol

@@ -1,4 +1,8 @@
-"""Time the ResNet-152 ID classifier forward on a frame's 32 boxes (random weights), for rocprof."""
+"""Time the ResNet-152 ID classifier forward (random weights) on n boxes, in one process, under the
+same-result GEMM routing knob MQ_TUNE_GEMM_TILE64 (64x64 tiles for GEMMs that cannot fill the CUs with
+128x128 ones) on and off, and check that both give identical probabilities.
+
+python tools/id_probe.py [n_boxes ...]      (default: 13 32 -- a config-5 frame's tracked boxes, 32)"""
 import os
 import sys
 import time
@@ -9,18 +13,33 @@ sys.path.insert(0, os.path.join(ROOT, "macaque-3d-pose-estimation_amd"))
 
 def main():
     import torch
+    from mqhip import _lib
     from mqhip.resnet_id import ResNetIdHip, make_random_weights
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+    sizes = [int(a) for a in sys.argv[1:]] or [13, 32]
     m = ResNetIdHip(make_random_weights(152, seed=0), depth=152)
-    x = torch.randn((n, 224, 224, 3), device="cuda").to(torch.bfloat16)
-    for _ in range(3):
-        m.forward(x)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(10):
-        m.forward(x)
-    torch.cuda.synchronize()
-    print(f"ResNet-152 ID forward, {n} boxes: {(time.perf_counter() - t0) * 100:.2f} ms", flush=True)
+    lib = m.ctx.lib
+    old = lib.mq_get_tuning(19)
+    try:
+        for n in sizes:
+            x = torch.randn((n, 224, 224, 3), device="cuda").to(torch.bfloat16)
+            ref = None
+            for rnd in range(3):
+                for t64 in (1, 0):
+                    _lib.check(lib.mq_set_tuning(19, t64), "knob")
+                    for _ in range(2):
+                        _, probs = m.forward(x)
+                    torch.cuda.synchronize()
+                    if ref is None:
+                        ref = probs.clone()
+                    same = bool(torch.equal(probs, ref))
+                    t0 = time.perf_counter()
+                    for _ in range(10):
+                        m.forward(x)
+                    torch.cuda.synchronize()
+                    print(f"r={rnd} ResNet-152 ID forward, {n} boxes, tile64={t64}: "
+                          f"{(time.perf_counter() - t0) * 100:.2f} ms  identical={same}", flush=True)
+    finally:
+        lib.mq_set_tuning(19, old)
 
 
 if __name__ == "__main__":
