@@ -123,6 +123,12 @@ int mq_topdown(mq_vitpose* model, const uint8_t* frames, int64_t frame_stride, i
 int mq_gemm_bf16(mq_ctx* ctx, const void* A, const void* W, void* C, const float* bias, const float* aux, int M,
                  int N, int K, int lda, int ldw, int ldc, int aux_rows, int epilogue, void* stream);
 
+/* C f32 (M, ldc) = max(C + A W^T + bias, 0) and out bf16 (M, ldc) = the same values: a ResNet bottleneck's
+ * conv3 + residual add + ReLU in one pass (mmpretrain Bottleneck.forward, the ID classifier
+ * model/id/sn_resnet152_8xb32_in1k_pretrained_optimized_finetuned.py backbone), K % 64 == 0. */
+int mq_gemm_resid_relu_bf16(mq_ctx* ctx, const void* A, const void* W, float* C, const float* bias, uint16_t* out,
+                            int M, int N, int K, int lda, int ldw, int ldc, void* stream);
+
 /* ======================================================================= detector
  * Building blocks of the step-1 detector, Swin-S Mask R-CNN bbox only
  * (model/detection/SWIN-Mask_R-CNN_bbox_only.py:29-226, inference_detector at step1_proc2d.py:226):

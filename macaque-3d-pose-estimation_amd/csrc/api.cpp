@@ -701,6 +701,18 @@ int mq_gemm_bf16(mq_ctx* ctx, const void* A, const void* W, void* C, const float
   return 0;
 }
 
+int mq_gemm_resid_relu_bf16(mq_ctx* ctx, const void* A, const void* W, float* C, const float* bias, uint16_t* out,
+                            int M, int N, int K, int lda, int ldw, int ldc, void* stream) {
+  if (!ctx || !A || !W || !C || !out) return fail("mq_gemm_resid_relu_bf16: null argument");
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64) return fail("mq_gemm_resid_relu_bf16: bad sizes (K % 64 == 0)", -2);
+  HIP_TRY(hipSetDevice(ctx->device));
+  mq::GemmArgs g{(const unsigned short*)A, (const unsigned short*)W, C, bias, nullptr, M, N, K, lda, ldw, ldc, 0};
+  g.C2 = out;
+  if (mq::gemm_bf16(g, mq::EPI_RESID_RELU, (hipStream_t)stream))
+    return fail("mq_gemm_resid_relu_bf16: launch failed / unsupported shape", -6);
+  return 0;
+}
+
 int mq_conv3x3_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch, const uint16_t* w,
                     const float* bias, void* out, int cout, int ldc, int epilogue, void* stream) {
   if (!ctx || !x || !w || !out) return fail("mq_conv3x3_bf16: null argument");

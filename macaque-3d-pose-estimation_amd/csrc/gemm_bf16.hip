@@ -140,6 +140,11 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
         } else if constexpr (EPI == EPI_RESID_F32) {
           float* c = (float*)p.C + (size_t)m * p.ldc + n;
           *c = *c + v;
+        } else if constexpr (EPI == EPI_RESID_RELU) {
+          float* c = (float*)p.C + (size_t)m * p.ldc + n;
+          const float o = fmaxf(*c + v, 0.f);
+          *c = o;
+          ((bf16_t*)p.C2)[(size_t)m * p.ldc + n] = f32_to_bf16(o);
         } else if constexpr (EPI == EPI_POS_F32) {
           ((float*)p.C)[(size_t)m * p.ldc + n] = v + p.aux[(size_t)(m % p.aux_rows) * p.N + n];
         } else if constexpr (EPI == EPI_F32) {
@@ -605,6 +610,7 @@ static int launch_small(const GemmArgs& p, int epi, hipStream_t stream) {
     case EPI_POS_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_POS_F32, WF>), grid, block, lds, stream, p); break;
     case EPI_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_F32, WF>), grid, block, lds, stream, p); break;
     case EPI_NCHW_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_NCHW_F32, WF>), grid, block, lds, stream, p); break;
+    case EPI_RESID_RELU: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RESID_RELU, WF>), grid, block, lds, stream, p); break;
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;
@@ -613,7 +619,9 @@ static int launch_small(const GemmArgs& p, int epi, hipStream_t stream) {
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return -1;
   if ((p.lda % 8) || (p.ldw % 8)) return -2;
-  bool big = epi != EPI_NCHW_F32 && p.N >= 256 && p.M >= 256 && (p.N % 4) == 0 && (p.K % B2K) == 0 &&
+  if (epi == EPI_RESID_RELU && (!p.C2 || p.K % BK)) return -1;
+  // the fused residual + ReLU epilogue exists in the 128x128 / 64x64 kernel only
+  bool big = epi != EPI_NCHW_F32 && epi != EPI_RESID_RELU && p.N >= 256 && p.M >= 256 && (p.N % 4) == 0 && (p.K % B2K) == 0 &&
              (p.ldc % 4) == 0 && !g_gemm_force_small;
   // fewer 256x256 tiles than half the CUs (the detector's late-stage Swin GEMMs): the 128x128 kernel
   // puts 4x as many workgroups on the chip

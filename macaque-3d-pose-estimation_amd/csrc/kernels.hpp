@@ -13,6 +13,7 @@ enum GemmEpilogue {
   EPI_F32 = 4,        // C f32 = acc + bias
   EPI_NCHW_F32 = 5,   // C f32 [m / aux_rows][n][m % aux_rows] = acc + bias (1x1 conv -> NCHW)
   EPI_RELU_BF16 = 6,  // C bf16 = max(acc + bias, 0)   (detector convs / fc layers)
+  EPI_RESID_RELU = 7, // C f32 = max(C + acc + bias, 0), C2 bf16 = the same (ResNet bottleneck output)
 };
 
 struct GemmArgs {
@@ -28,6 +29,7 @@ struct GemmArgs {
   // output pixels, lda = conv_c channels, K = 9 * conv_c in (ky * 3 + kx) * conv_c + c order; the A tile
   // rows of each K-step are gathered from the tap's shifted pixels (zeros outside the image)
   int conv_h = 0, conv_w = 0, conv_c = 0;
+  void* C2 = nullptr;       // EPI_RESID_RELU: bf16 copy of the output, ldc
 };
 
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);

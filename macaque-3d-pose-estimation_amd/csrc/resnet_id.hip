@@ -171,28 +171,47 @@ __global__ __launch_bounds__(256) void relu_bf16_kernel(float* __restrict__ x, b
 
 // GlobalAveragePooling + LinearClsHead.fc + softmax, one block per image: x f32 (n, hw, c) ->
 // logits / probs f32 (n, ncls).  Fixed-order reductions.
-__global__ __launch_bounds__(256) void gap_fc_softmax_kernel(const float* __restrict__ x, int hw, int c,
-                                                             const float* __restrict__ fc_w,
-                                                             const float* __restrict__ fc_b, int ncls,
-                                                             float* __restrict__ logits, float* __restrict__ probs) {
+__global__ __launch_bounds__(1024) void gap_fc_softmax_kernel(const float* __restrict__ x, int hw, int c,
+                                                              const float* __restrict__ fc_w,
+                                                              const float* __restrict__ fc_b, int ncls,
+                                                              float* __restrict__ logits, float* __restrict__ probs) {
   extern __shared__ float sh_id[];
   float* pooled = sh_id;      // [c]
-  float* red = sh_id + c;     // [256]
+  float* red = sh_id + c;     // [1024]
   const int b = blockIdx.x, t = threadIdx.x;
   const float* xb = x + (int64_t)b * hw * c;
-  for (int ch = t; ch < c; ch += 256) {
-    float s = 0.f;
-    for (int p = 0; p < hw; ++p) s += xb[(int64_t)p * c + ch];
-    pooled[ch] = s / (float)hw;
+  // channels t and t + 1024 together, 8 pixels of each per batch of loads (16 loads in flight); every
+  // channel still sums its pixels in ascending order
+  for (int ch0 = t; ch0 < c; ch0 += 2048) {
+    const int ch1 = ch0 + 1024;
+    const bool has1 = ch1 < c;
+    float s0 = 0.f, s1 = 0.f;
+    for (int p0 = 0; p0 < hw; p0 += 8) {
+      float v0[8], v1[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int pp = p0 + u;
+        v0[u] = pp < hw ? xb[(int64_t)pp * c + ch0] : 0.f;
+        v1[u] = (pp < hw && has1) ? xb[(int64_t)pp * c + ch1] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u < hw) {
+          s0 += v0[u];
+          s1 += v1[u];
+        }
+    }
+    pooled[ch0] = s0 / (float)hw;
+    if (has1) pooled[ch1] = s1 / (float)hw;
   }
   __syncthreads();
   float lg[ID_MAX_CLASSES];
   for (int k = 0; k < ncls; ++k) {
     float s = 0.f;
-    for (int ch = t; ch < c; ch += 256) s += fc_w[(int64_t)k * c + ch] * pooled[ch];
+    for (int ch = t; ch < c; ch += 1024) s += fc_w[(int64_t)k * c + ch] * pooled[ch];
     red[t] = s;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
+    for (int o = 512; o > 0; o >>= 1) {
       if (t < o) red[t] += red[t + o];
       __syncthreads();
     }
@@ -252,7 +271,7 @@ int relu_bf16(float* x, bf16_t* y, int64_t count, hipStream_t s) {
 
 int gap_fc_softmax(const float* x, int n, int hw, int c, const float* fc_w, const float* fc_b, int ncls, float* logits,
                    float* probs, hipStream_t s) {
-  hipLaunchKernelGGL(gap_fc_softmax_kernel, dim3(n), dim3(256), (c + 256) * sizeof(float), s, x, hw, c, fc_w, fc_b,
+  hipLaunchKernelGGL(gap_fc_softmax_kernel, dim3(n), dim3(1024), (c + 1024) * sizeof(float), s, x, hw, c, fc_w, fc_b,
                      ncls, logits, probs);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

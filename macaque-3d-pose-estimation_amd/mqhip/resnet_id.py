@@ -23,7 +23,7 @@ import torch
 
 from . import _lib
 
-EPI_RESID, EPI_F32, EPI_RELU = 2, 4, 6
+EPI_F32, EPI_RELU = 4, 6
 ID_CLASSES = ("b", "d", "g", "r", "unknown", "w")
 DEPTH_BLOCKS = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3)}
 STAGE_WIDTHS = (64, 128, 256, 512)
@@ -193,10 +193,12 @@ class ResNetIdHip:
                 src = a if dn["stride"] == 1 else self._im2col(a, n, h, w, dn)[0]
                 xs = torch.empty((Mo, dn["co"]), device=self.dev, dtype=torch.float32)
                 self._gemm(src, dn, xs, Mo, EPI_F32)
-            self._gemm(h2, c3, xs, Mo, EPI_RESID)
+            # conv3 + residual + ReLU in one epilogue: the f32 stream and the next block's bf16 operand
             a = torch.empty((Mo, c3["co"]), device=self.dev, dtype=torch.bfloat16)
-            _lib.check(self.ctx.lib.mq_id_relu_bf16(self.ctx.handle, _lib.ptr(xs), _lib.ptr(a), xs.numel(), self._s()),
-                       "mq_id_relu_bf16")
+            _lib.check(self.ctx.lib.mq_gemm_resid_relu_bf16(self.ctx.handle, _lib.ptr(h2), _lib.ptr(c3["w"]),
+                                                            _lib.ptr(xs), _lib.ptr(c3["b"]), _lib.ptr(a), Mo,
+                                                            c3["co"], c3["kpad"], c3["kpad"], c3["kpad"], c3["co"],
+                                                            self._s()), "mq_gemm_resid_relu_bf16")
             h, w = oh, ow
         logits = torch.empty((n, self.num_classes), device=self.dev, dtype=torch.float32)
         probs = torch.empty_like(logits)
