@@ -641,9 +641,10 @@ int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
     if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
       g_num_cus = 256;
   }
-  // 64x64 tiles when 128x128 ones cannot occupy every CU once (and K is long enough to be worth it)
+  // 64x64 tiles when 128x128 ones cannot occupy every CU once (and K is long enough to be worth it), or
+  // would leave half of every tile's columns empty (N <= 64: the ID classifier's stage-1 convolutions)
   const int tiles128 = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  if (g_gemm_tile64 && tiles128 < g_num_cus && p.K >= 256) return launch_small<2>(p, epi, stream);
+  if (g_gemm_tile64 && ((tiles128 < g_num_cus && p.K >= 256) || p.N <= 64)) return launch_small<2>(p, epi, stream);
   return launch_small<4>(p, epi, stream);
 }
 
