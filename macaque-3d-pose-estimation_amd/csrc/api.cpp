@@ -75,6 +75,7 @@ struct mq_ctx {
   DevBuf optim_ws;
   DevBuf assoc_ws;  // step-2 affinity: rays + pairwise distances
   DevBuf det_ws;    // detector post-processing (sort, NMS masks)
+  DevBuf dlt_ws;    // mq_triangulate_dlt: undistorted points
 };
 
 struct ParamSlot {
@@ -201,6 +202,7 @@ int mq_destroy(mq_ctx* ctx) {
   ctx->decode_work.release();
   ctx->optim_ws.release();
   ctx->assoc_ws.release();
+  ctx->dlt_ws.release();
   ctx->det_ws.release();
   delete ctx;
   return 0;
@@ -1011,6 +1013,15 @@ int mq_triangulate_dlt(mq_ctx* ctx, const double* cams, int C, const double* pts
                        void* stream) {
   int rc = check_geo(ctx, cams, C, n);
   if (rc) return rc;
+  if (undistort && n > 0) {
+    // undistort every (camera, point) in parallel first (20 fixed-point iterations each), then the
+    // per-point DLT on the undistorted coordinates: the same arithmetic as undistorting inside the DLT
+    // kernel, spread over C x n threads instead of n
+    if (ctx->dlt_ws.ensure((size_t)C * n * 2 * sizeof(double))) return fail("DLT workspace alloc failed", -5);
+    K_TRY(mq::omnidir_undistort(cams, C, pts, ctx->dlt_ws.as<double>(), n, (hipStream_t)stream));
+    K_TRY(mq::triangulate_dlt(cams, C, ctx->dlt_ws.as<double>(), n, 0, out, (hipStream_t)stream));
+    return 0;
+  }
   K_TRY(mq::triangulate_dlt(cams, C, pts, n, undistort, out, (hipStream_t)stream));
   return 0;
 }
