@@ -39,7 +39,7 @@
 // DMA issue plan and counted waits derived from it); the library instantiates 256 x 256.  A 192 x 320
 // shape (6 x 5 fragments per wave, 18 / 12 / 18 / 12 MFMAs per phase, DMA plan 3 / 2 / 2 / 1) fills whole
 // CU rounds for fc1 / qkv / fc2 / proj but measured 1 % slower end to end in the ViT-H forward
-// (profiles/r03d_vit_probe_wide_tiles.log), so it is not built.
+// (profiles/r02s3d_vit_probe_wide_tiles.log), so it is not built.
 #include "common.hpp"
 #include "kernels.hpp"
 
