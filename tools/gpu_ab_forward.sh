@@ -1,11 +1,11 @@
-# Deconv sub-pixel + wide-tile check: GPU tests of the touched kernels, the forward A/B (wide tiles on /
-# off in one process; the previous build in a second process on the same box), a short bench.
+# Forward A/B against the previous build: pose / detector / attention GPU tests, the ViT-H forward of this build
+# and of lib_prev (two processes back to back on one box), a short bench.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=${1:-r03d}
+OUT=${1:-ab_fwd}
 mkdir -p gpurun_out/$OUT
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_deconv.py tests/test_gpu_pose.py tests/test_gpu_gemm.py tests/test_gpu_run_demo.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$OUT/pytest.log 2>&1 || { echo PYTEST FAILED; tail -30 gpurun_out/$OUT/pytest.log; exit 1; }
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_pose.py tests/test_gpu_detector.py tests/test_gpu_attention.py tests/test_gpu_run_demo.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/$OUT/pytest.log 2>&1 || { echo PYTEST FAILED; tail -30 gpurun_out/$OUT/pytest.log; exit 1; }
 tail -2 gpurun_out/$OUT/pytest.log
 timeout -k 10 300 python3 -u tools/vit_probe.py --knob 12=1 --iters 10 --rounds 3 > gpurun_out/$OUT/probe_new.log 2>&1 || { echo PROBE FAILED; tail -20 gpurun_out/$OUT/probe_new.log; exit 1; }
 timeout -k 10 300 python3 -u tools/vit_probe.py --lib macaque-3d-pose-estimation_amd/lib_prev/libmq_hip.so --knob 17=1 --iters 10 --rounds 3 > gpurun_out/$OUT/probe_prev.log 2>&1 || { echo PROBE PREV FAILED; tail -20 gpurun_out/$OUT/probe_prev.log; exit 1; }
