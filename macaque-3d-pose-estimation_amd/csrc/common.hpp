@@ -77,10 +77,25 @@ __device__ __forceinline__ float bfly32_sum(float x) {
   return __uint_as_float(p[0]) + __uint_as_float(p[1]);
 }
 
+// Full-wave sum on VALU only (no ds_bpermute LDS round trips): DPP quad_perm xor 1 and xor 2, row_half_mirror
+// (quad <-> quad), row_mirror (half-row <-> half-row), then the row butterflies above.  Every lane ends
+// with the same value; the pairing is fixed, so the result is deterministic.
+__device__ __forceinline__ float dpp_add(float v, int ctrl_sel) {
+  int o;
+  switch (ctrl_sel) {
+    case 0: o = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false); break;   // quad [1,0,3,2]
+    case 1: o = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false); break;   // quad [2,3,0,1]
+    case 2: o = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false); break;  // row_half_mirror
+    default: o = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false); break; // row_mirror
+  }
+  return v + __int_as_float(o);
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = dpp_add(v, 0);
+  v = dpp_add(v, 1);
+  v = dpp_add(v, 2);
+  v = dpp_add(v, 3);
+  return bfly32_sum(bfly16_sum(v));
 }
 
 __device__ __forceinline__ float wave_max(float v) {

@@ -109,6 +109,16 @@ struct AttLayout {
   static constexpr int LDS = KBYTES + VBYTES;
 };
 
+// XCD-aware (image, head) of a workgroup: blocks b and b + 8 share an XCD (round-robin dispatch), so
+// the bijective remap gives every XCD a contiguous range of (image, head) items, all heads of an image on
+// one XCD.  A head's Q / K / V rows are 160 B of a 7,680-B QKV row: neighbouring heads share their
+// boundary 128-B lines, which then hit in that XCD's L2 instead of being fetched once per XCD.
+__device__ __forceinline__ int att_item(int H) {
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
 // TT: compile-time token count (192 = the ViT-H 256x192 grid) so every per-block guard
 // folds away; 0 = runtime T (other grids / tests).
 template <int DH, int TT = 0>
@@ -124,7 +134,8 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t*
   char* Kimg = smem;
   char* Vimg = smem + L::KBYTES;
 
-  const int img = blockIdx.x / H, h = blockIdx.x % H;
+  const int item = att_item(H);
+  const int img = item / H, h = item % H;
   const size_t row0 = (size_t)img * T;
   const int ld = 3 * D;
   const int lane = threadIdx.x & 63;
@@ -302,7 +313,8 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
   char* Kimg = smem;
   char* Vimg = smem + KBYTES;
 
-  const int img = blockIdx.x / H, h = blockIdx.x % H;
+  const int item = att_item(H);
+  const int img = item / H, h = item % H;
   const size_t row0 = (size_t)img * T;
   const int ld = 3 * D;
   const int lane = threadIdx.x & 63;
