@@ -52,6 +52,8 @@ const char* mq_last_error(void);
                                        attention2_kernel); 0: the first-generation kernel */
 #define MQ_TUNE_GEMM_TILE64 19      /* 1 (default): GEMMs whose 128x128 tiles cannot occupy every CU once take the
                                        64x64-tile kernel (same accumulation order, tested equal); 0: 128x128 */
+#define MQ_TUNE_QKV_HEAD_MAJOR 20   /* 1 (default): the ViT qkv GEMM writes Q / K / V head-major (each head's rows
+                                       contiguous) for the attention's loads; 0: row-major (same results) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

@@ -24,6 +24,8 @@
 namespace {
 
 thread_local std::string g_err;
+// ViT qkv GEMM output head-major for the attention (MQ_TUNE_QKV_HEAD_MAJOR; 0: row-major, same bits)
+int g_qkv_head_major = 1;
 int g_tuning_gen = 0;  // bumped by mq_set_tuning
 
 int fail(const std::string& msg, int code = -1) {
@@ -162,6 +164,9 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_GEMM_TILE64:
       mq::g_gemm_tile64 = value != 0;
       break;
+    case MQ_TUNE_QKV_HEAD_MAJOR:
+      g_qkv_head_major = value != 0;
+      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -177,6 +182,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_ATTENTION_V2: return mq::g_attention_v2;
     case MQ_TUNE_OPTIM_PRECOND_LDS: return mq::g_optim_precond_lds;
     case MQ_TUNE_GEMM_TILE64: return mq::g_gemm_tile64;
+    case MQ_TUNE_QKV_HEAD_MAJOR: return g_qkv_head_major;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }
@@ -514,9 +520,11 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
   for (int l = 0; l < m->L; ++l) {
     const Layer& ly = m->layers[l];
     K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
+    // qkv written head-major (each head's Q / K / V rows contiguous) for the attention's loads
     g = mq::GemmArgs{m->Hn, ly.wqkv, m->QKV, ly.bqkv, nullptr, rows, 3 * D, D, D, D, 3 * D, 0};
+    g.head_dim = g_qkv_head_major ? D / m->H : 0;
     K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
-    K_TRY(mq::attention_bf16(m->QKV, m->O, F, T, D, m->H, s));
+    K_TRY(mq::attention_bf16(m->QKV, m->O, F, T, D, m->H, s, g_qkv_head_major != 0));
     g = mq::GemmArgs{m->O, ly.wproj, m->X, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
     K_TRY(mq::gemm_bf16(g, mq::EPI_RESID_F32, s));
     K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));

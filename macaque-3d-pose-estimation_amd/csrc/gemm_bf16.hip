@@ -132,7 +132,7 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
         if (m >= p.M) continue;
         float v = acc[i][j][e] + bias;
         if constexpr (EPI == EPI_BF16) {
-          ((bf16_t*)p.C)[(size_t)m * p.ldc + n] = f32_to_bf16(v);
+          *gemm_out_bf16(p, m, n) = f32_to_bf16(v);
         } else if constexpr (EPI == EPI_GELU_BF16) {
           ((bf16_t*)p.C)[(size_t)m * p.ldc + n] = f32_to_bf16(gelu_erf(v));
         } else if constexpr (EPI == EPI_RELU_BF16) {
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
           const int j = jp + (odd ? 1 : 0);
           const int n = n0 + wn * 64 + j * 16 + nbase;
           if (m < p.M && n < p.N)
-            *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)m * p.ldc + n) = o;
+            *reinterpret_cast<uint4*>(gemm_out_bf16(p, m, n)) = o;
         }
       }
       return;
@@ -620,6 +620,7 @@ int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0) return -1;
   if ((p.lda % 8) || (p.ldw % 8)) return -2;
   if (epi == EPI_RESID_RELU && (!p.C2 || p.K % BK)) return -1;
+  if (p.head_dim && (epi != EPI_BF16 || p.head_dim % 8 || p.N % p.head_dim)) return -1;
   // the fused residual + ReLU epilogue exists in the 128x128 / 64x64 kernel only
   bool big = epi != EPI_NCHW_F32 && epi != EPI_RESID_RELU && p.N >= 256 && p.M >= 256 && (p.N % 4) == 0 && (p.K % B2K) == 0 &&
              (p.ldc % 4) == 0 && !g_gemm_force_small;

@@ -255,14 +255,16 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
         // even lanes: [own tile j | neighbour's tile j]; odd: [neighbour's j+1 | own j+1]
         const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         const int n = nb + (jp + (odd ? 1 : 0)) * 16 + nbase;
-        if (full || (m < p.M && n < p.N)) *reinterpret_cast<uint4*>(crow_p + n) = o;
+        if (full || (m < p.M && n < p.N))
+          *reinterpret_cast<uint4*>(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n) : crow_p + n) = o;
       }
       if constexpr (WNF & 1) {
         float v[4];
         act(i, WNF - 1, v);
         const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
         const int n = nb + (WNF - 1) * 16 + nn;
-        if (full || (m < p.M && n < p.N)) *reinterpret_cast<uint2*>(crow_p + n) = o;
+        if (full || (m < p.M && n < p.N))
+          *reinterpret_cast<uint2*>(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n) : crow_p + n) = o;
       }
     }
     return;

@@ -30,7 +30,17 @@ struct GemmArgs {
   // rows of each K-step are gathered from the tap's shifted pixels (zeros outside the image)
   int conv_h = 0, conv_w = 0, conv_c = 0;
   void* C2 = nullptr;       // EPI_RESID_RELU: bf16 copy of the output, ldc
+  // EPI_BF16 with head_dim > 0: head-major output, column n of row m at
+  // C[((n / head_dim) * M + m) * head_dim + n % head_dim] (the ViT qkv GEMM -> attention; ldc unused)
+  int head_dim = 0;
 };
+
+// bf16 output address of element (m, n) of a GEMM (row-major, or head-major blocks)
+__device__ __forceinline__ unsigned short* gemm_out_bf16(const GemmArgs& p, int m, int n) {
+  if (p.head_dim)
+    return (unsigned short*)p.C + ((size_t)(n / p.head_dim) * p.M + m) * p.head_dim + (n - (n / p.head_dim) * p.head_dim);
+  return (unsigned short*)p.C + (size_t)m * p.ldc + n;
+}
 
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 // implicit-GEMM 3x3 convolution (ping-pong kernel only; conv_c % 64 == 0)
@@ -55,8 +65,9 @@ int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, un
 int layernorm_f32_f32(const float* x, const float* gamma, const float* beta, float* y, int rows, int dim, float eps,
                       hipStream_t s);
 extern int g_attention_v2;  // 1 (default): attention2_kernel; 0: the first-generation kernel
+// head_major: qkv holds the head-major blocks of the qkv GEMM's head_dim output (GemmArgs::head_dim)
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
-                   hipStream_t s);
+                   hipStream_t s, bool head_major = false);
 int patch_im2col(const float* crops, unsigned short* A, int n_crops, int flip_copies, int img_h, int img_w,
                  int patch, int pad, hipStream_t s);
 int deconv_col2im_bn_relu(const unsigned short* cols, const float* scale, const float* shift, unsigned short* out,

@@ -109,6 +109,24 @@ struct AttLayout {
   static constexpr int LDS = KBYTES + VBYTES;
 };
 
+// Q / K / V rows of (image, head): row-major QKV (ld = 3 D; sections at columns 0, D, 2 D, the head at
+// h DH) or, with nt_hm = images x tokens > 0, the head-major blocks the ViT qkv GEMM writes (GemmArgs
+// head_dim): block s H + h of nt_hm x DH, ld = DH -- each head's 192 x 160-B rows contiguous.
+template <int DH>
+__device__ __forceinline__ int att_bases(const bf16_t* qkv, int D, int H, int h, size_t row0, int nt_hm,
+                                         const bf16_t*& qb, const bf16_t*& kb, const bf16_t*& vb) {
+  if (nt_hm) {
+    qb = qkv + ((size_t)h * nt_hm + row0) * DH;
+    kb = qkv + ((size_t)(H + h) * nt_hm + row0) * DH;
+    vb = qkv + ((size_t)(2 * H + h) * nt_hm + row0) * DH;
+    return DH;
+  }
+  qb = qkv + row0 * 3 * D + h * DH;
+  kb = qb + D;
+  vb = kb + D;
+  return 3 * D;
+}
+
 // XCD-aware (image, head) of a workgroup: blocks b and b + 8 share an XCD (round-robin dispatch), so
 // the bijective remap gives every XCD a contiguous range of (image, head) items, all heads of an image on
 // one XCD.  A head's Q / K / V rows are 160 B of a 7,680-B QKV row: neighbouring heads share their
@@ -124,7 +142,7 @@ __device__ __forceinline__ int att_item(int H) {
 template <int DH, int TT = 0>
 __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t* __restrict__ qkv,
                                                                     bf16_t* __restrict__ out, int T_rt, int D,
-                                                                    int H, float scale_log2) {
+                                                                    int H, float scale_log2, int nt_hm) {
   using L = AttLayout<DH>;
   const int T = TT ? TT : T_rt;
   constexpr int NKS = DH / 16;  // k-steps of QK^T
@@ -137,7 +155,8 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t*
   const int item = att_item(H);
   const int img = item / H, h = item % H;
   const size_t row0 = (size_t)img * T;
-  const int ld = 3 * D;
+  const bf16_t *qbase, *kbase, *vbase;
+  const int ld = att_bases<DH>(qkv, D, H, h, row0, nt_hm, qbase, kbase, vbase);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, g = lane >> 4;
@@ -145,8 +164,6 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t*
 
   // K / V images by LDS-DMA: instruction i of the image writes chunks 64 i .. 64 i + 63
   // (lane-linear); a chunk is (token, 16-B piece); pad / tail lanes re-load chunk 0.
-  const bf16_t* kbase = qkv + row0 * ld + D + h * DH;
-  const bf16_t* vbase = kbase + D;
   const int nk_ins = (T * L::KCH + 63) / 64, nv_ins = (T * L::VCH + 63) / 64;
   for (int ins = wave; ins < nk_ins; ins += ATT_WAVES) {
     const int q = ins * 64 + lane;
@@ -172,7 +189,7 @@ __global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t*
     const int q = qb * 16 + l16;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks)
-      qf[u][ks] = *reinterpret_cast<const short4v*>(qkv + (row0 + q) * ld + h * DH + ks * 16 + 4 * g);
+      qf[u][ks] = *reinterpret_cast<const short4v*>(qbase + (size_t)q * ld + ks * 16 + 4 * g);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -298,7 +315,7 @@ constexpr int ATT2_KCH = 10;  // K image row stride in 16-B chunks (DH <= 80)
 template <int DH, int TT = 0>
 __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t* __restrict__ qkv,
                                                                      bf16_t* __restrict__ out, int T_rt, int D,
-                                                                     int H, float scale_log2) {
+                                                                     int H, float scale_log2, int nt_hm) {
   using L = AttLayout<DH>;
   const int T = TT ? TT : T_rt;
   constexpr int NKS = (DH + 31) / 32;   // 16x16x32 k-steps of QK^T
@@ -316,14 +333,13 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
   const int item = att_item(H);
   const int img = item / H, h = item % H;
   const size_t row0 = (size_t)img * T;
-  const int ld = 3 * D;
+  const bf16_t *qbase, *kbase, *vbase;
+  const int ld = att_bases<DH>(qkv, D, H, h, row0, nt_hm, qbase, kbase, vbase);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l16 = lane & 15, g = lane >> 4;
   const int ntb = T / 16;
 
-  const bf16_t* kbase = qkv + row0 * ld + D + h * DH;
-  const bf16_t* vbase = kbase + D;
   const int nk_ins = (T * KCH + 63) / 64, nv_ins = (T * L::VCH + 63) / 64;
   for (int ins = wave; ins < nk_ins; ins += ATT_WAVES) {
     const int q = ins * 64 + lane;
@@ -344,7 +360,7 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int qb = min(wave + u * ATT_WAVES, ntb - 1);
-    const bf16_t* qrow = qkv + (row0 + qb * 16 + l16) * ld + h * DH;
+    const bf16_t* qrow = qbase + (size_t)(qb * 16 + l16) * ld;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       if (HALF && ks == NKS - 1 && g >= 2)
@@ -514,33 +530,36 @@ int g_attention_v2 = 1;
 
 template <int DH>
 static void launch_attention(dim3 grid, dim3 block, hipStream_t s, const unsigned short* qkv, unsigned short* out,
-                             int tokens, int dim, int heads, float scale_log2) {
+                             int tokens, int dim, int heads, float scale_log2, int nt_hm) {
   constexpr int lds = AttLayout<DH>::LDS;
   if (g_attention_v2) {
     constexpr int lds2 = (ATT_MAXT * ATT2_KCH + 63) / 64 * 1024 + AttLayout<DH>::VBYTES;
     if (tokens == ATT_MAXT)
       hipLaunchKernelGGL((attention2_kernel<DH, ATT_MAXT>), grid, block, lds2, s, qkv, out, tokens, dim, heads,
-                         scale_log2);
+                         scale_log2, nt_hm);
     else
-      hipLaunchKernelGGL((attention2_kernel<DH, 0>), grid, block, lds2, s, qkv, out, tokens, dim, heads, scale_log2);
+      hipLaunchKernelGGL((attention2_kernel<DH, 0>), grid, block, lds2, s, qkv, out, tokens, dim, heads, scale_log2,
+                         nt_hm);
     return;
   }
   if (tokens == ATT_MAXT)
-    hipLaunchKernelGGL((attention_kernel<DH, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+    hipLaunchKernelGGL((attention_kernel<DH, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2,
+                       nt_hm);
   else
-    hipLaunchKernelGGL((attention_kernel<DH, 0>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2);
+    hipLaunchKernelGGL((attention_kernel<DH, 0>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2,
+                       nt_hm);
 }
 
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
-                   hipStream_t s) {
+                   hipStream_t s, bool head_major) {
   const int dh = dim / heads;
   if (tokens % 32 || tokens > ATT_MAXT || tokens <= 0 || dh * heads != dim) return -1;
   const float scale_log2 = (1.0f / sqrtf((float)dh)) * 1.4426950408889634f;
   dim3 grid(n_img * heads), block(ATT_THREADS);
   if (dh == 80)
-    launch_attention<80>(grid, block, s, qkv, out, tokens, dim, heads, scale_log2);
+    launch_attention<80>(grid, block, s, qkv, out, tokens, dim, heads, scale_log2, head_major ? n_img * tokens : 0);
   else if (dh == 64)
-    launch_attention<64>(grid, block, s, qkv, out, tokens, dim, heads, scale_log2);
+    launch_attention<64>(grid, block, s, qkv, out, tokens, dim, heads, scale_log2, head_major ? n_img * tokens : 0);
   else
     return -2;
   return hipGetLastError() == hipSuccess ? 0 : -3;

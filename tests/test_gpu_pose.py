@@ -121,6 +121,33 @@ def test_vitpose_graph_replay_matches_eager():
     assert torch.equal(out, eager)
 
 
+@pytest.mark.parametrize("cfg_name,n", [("tiny", 3), ("huge", 32)])
+def test_vitpose_qkv_head_major_matches_row_major(cfg_name, n):
+    """The qkv GEMM writing Q / K / V head-major (MQ_TUNE_QKV_HEAD_MAJOR = 1, the attention then reads each
+    head's rows contiguously) gives the heatmaps of the row-major layout bit for bit; n = 32 takes the ViT-H
+    qkv GEMM through the ping-pong kernel, n = 3 through the small-tile kernel."""
+    import torch
+    from mqhip import _lib
+    from mqhip.pose import VitPoseHip
+    from mqhip.weights import CONFIGS, make_random_weights
+    cfg = CONFIGS[cfg_name]
+    w = make_random_weights(cfg, seed=5, device="cuda")
+    crops = torch.randn((n, 3, 256, 192), device="cuda")
+    model = VitPoseHip(cfg, w, graph=False)
+    ctx = _lib.Context.get(0)
+    old = ctx.lib.mq_get_tuning(20)
+    outs = []
+    try:
+        for hm in (0, 1):
+            assert ctx.lib.mq_set_tuning(20, hm) == 0
+            outs.append(model.forward(crops).clone())
+    finally:
+        ctx.lib.mq_set_tuning(20, old)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_topdown_end_to_end_vs_oracle():
     """crop -> ViT-tiny (flip) -> decode; argmax exact wherever the top-2 margin is clear."""
     import torch
