@@ -125,6 +125,13 @@ int mq_topdown(mq_vitpose* model, const uint8_t* frames, int64_t frame_stride, i
 int mq_gemm_bf16(mq_ctx* ctx, const void* A, const void* W, void* C, const float* bias, const float* aux, int M,
                  int N, int K, int lda, int ldw, int ldc, int aux_rows, int epilogue, void* stream);
 
+/* k x k / stride / pad convolution as an implicit GEMM (no im2col buffer): x bf16 NHWC (n_img, height, width,
+ * ch), ch % 64 == 0; w bf16 (cout, k * k * ch) in the mq_id_im2col order ((ky * k + kx) * ch + c); out
+ * (n_img * OH * OW, cout) with epilogue 0 (bf16), 4 (f32) or 6 (ReLU bf16) of mq_gemm_bf16, plus bias.  The
+ * same bits as mq_id_im2col + mq_gemm_bf16: the ID classifier's 3x3 and strided 1x1 convolutions. */
+int mq_id_conv_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch, int k, int stride,
+                    int pad, const uint16_t* w, const float* bias, void* out, int cout, int epilogue, void* stream);
+
 /* C f32 (M, ldc) = max(C + A W^T + bias, 0) and out bf16 (M, ldc) = the same values: a ResNet bottleneck's
  * conv3 + residual add + ReLU in one pass (mmpretrain Bottleneck.forward, the ID classifier
  * model/id/sn_resnet152_8xb32_in1k_pretrained_optimized_finetuned.py backbone), K % 64 == 0. */

@@ -723,6 +723,29 @@ int mq_gemm_resid_relu_bf16(mq_ctx* ctx, const void* A, const void* W, float* C,
   return 0;
 }
 
+int mq_id_conv_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch, int k, int stride,
+                    int pad, const uint16_t* w, const float* bias, void* out, int cout, int epilogue, void* stream) {
+  if (!ctx || !x || !w || !out) return fail("mq_id_conv_bf16: null argument");
+  if (n_img <= 0 || height <= 0 || width <= 0 || ch <= 0 || ch % 64 || k <= 0 || stride <= 0 || pad < 0 || cout <= 0 ||
+      cout % 8)
+    return fail("mq_id_conv_bf16: bad sizes (ch % 64 == 0, cout % 8 == 0)", -2);
+  if (epilogue != mq::EPI_BF16 && epilogue != mq::EPI_F32 && epilogue != mq::EPI_RELU_BF16)
+    return fail("mq_id_conv_bf16: epilogue must be 0 (bf16), 4 (f32) or 6 (ReLU bf16)", -2);
+  const int oh = (height + 2 * pad - k) / stride + 1, ow = (width + 2 * pad - k) / stride + 1;
+  if (oh <= 0 || ow <= 0) return fail("mq_id_conv_bf16: empty output", -2);
+  HIP_TRY(hipSetDevice(ctx->device));
+  mq::GemmArgs g{(const unsigned short*)x, (const unsigned short*)w, out, bias, nullptr, n_img * oh * ow, cout,
+                 k * k * ch, ch, k * k * ch, cout, 0};
+  g.conv_h = height;
+  g.conv_w = width;
+  g.conv_c = ch;
+  g.conv_k = k;
+  g.conv_s = stride;
+  g.conv_p = pad;
+  if (mq::conv_small_bf16(g, epilogue, (hipStream_t)stream)) return fail("mq_id_conv_bf16: launch failed", -6);
+  return 0;
+}
+
 int mq_conv3x3_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch, const uint16_t* w,
                     const float* bias, void* out, int cout, int ldc, int epilogue, void* stream) {
   if (!ctx || !x || !w || !out) return fail("mq_conv3x3_bf16: null argument");

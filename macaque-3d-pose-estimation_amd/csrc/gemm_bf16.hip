@@ -51,11 +51,35 @@ __device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ g, int ld,
   }
 }
 
+// Implicit convolution: the A tile of K-step t is tap t / (C / 64), channels 64 (t % (C / 64)) .. + 63 of
+// the tap-shifted input pixels of this tile's output rows; a pixel outside the image gets an offset past
+// the buffer end, which the DMA turns into zeros (padding).  cbase / cy / cx: per A slot the row's image
+// base offset (elements) and its top-left input coordinate (oy s - p, ox s - p).
+template <int WF>
+__device__ __forceinline__ void stage_conv_a(__amdgpu_buffer_rsrc_t rsA, const GemmArgs& p, const int (&cbase)[WF],
+                                             const int (&cy)[WF], const int (&cx)[WF], int t, char* lds_tile,
+                                             int wave, int lane) {
+  const int kpt = p.conv_c >> 6;
+  const int tap = t / kpt, c0 = (t - tap * kpt) * 64;
+  const int ky = tap / p.conv_k, kx = tap - ky * p.conv_k;
+#pragma unroll
+  for (int i = 0; i < WF; ++i) {
+    const int rbase = (wave * WF + i) * 8;
+    const int row = rbase + (lane >> 3);
+    const int chunk = (lane & 7) ^ swz(row);
+    const int iy = cy[i] + ky, ix = cx[i] + kx;
+    const bool inside = (unsigned)iy < (unsigned)p.conv_h && (unsigned)ix < (unsigned)p.conv_w;
+    const unsigned off = (unsigned)(cbase[i] + (iy * p.conv_w + ix) * p.conv_c + c0 + chunk * 8) * 2u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsA, MQ_LDS_LOCAL(lds_tile + rbase * 128), 16, inside ? off : 0x80000000u,
+                                             0, 0, 0);
+  }
+}
+
 __device__ __forceinline__ bf16x8 read_frag(const char* lds_tile, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds_tile + row * 128 + ((chunk ^ swz(row)) << 4));
 }
 
-template <int EPI, int WF>
+template <int EPI, int WF, bool CONV = false>
 __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) {
   constexpr int TM = 32 * WF;                // tile rows = tile columns
   constexpr int TB = TM * BK * 2;            // bytes per operand tile
@@ -85,8 +109,28 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
     for (int j = 0; j < WF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / BK;
-  stage_tile<WF>(p.A, p.lda, m0, p.M, 0, smem, wave, lane);
+  // implicit convolution: per A slot (this lane's row of each of the wave's 8-row groups) the output
+  // pixel's image base and top-left input coordinate
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, 0x7fffffff, 0x00020000);
+  int cbase[WF], cy[WF], cx[WF];
+  if constexpr (CONV) {
+    const int oh = (p.conv_h + 2 * p.conv_p - p.conv_k) / p.conv_s + 1;
+    const int ow = (p.conv_w + 2 * p.conv_p - p.conv_k) / p.conv_s + 1;
+#pragma unroll
+    for (int i = 0; i < WF; ++i) {
+      const int pix = min(m0 + (wave * WF + i) * 8 + (lane >> 3), p.M - 1);
+      const int img = pix / (oh * ow), rem = pix - img * (oh * ow);
+      const int oy = rem / ow, ox = rem - oy * ow;
+      cbase[i] = img * p.conv_h * p.conv_w * p.conv_c;
+      cy[i] = oy * p.conv_s - p.conv_p;
+      cx[i] = ox * p.conv_s - p.conv_p;
+    }
+    stage_conv_a<WF>(rsA, p, cbase, cy, cx, 0, smem, wave, lane);
+  } else {
+    stage_tile<WF>(p.A, p.lda, m0, p.M, 0, smem, wave, lane);
+  }
   stage_tile<WF>(p.W, p.ldw, n0, p.N, 0, smem + TB, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int frow = lane & 15;
@@ -95,7 +139,10 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
     const int cur = t & 1;
     if (t + 1 < nk) {
       char* nxt = smem + (cur ^ 1) * 2 * TB;
-      stage_tile<WF>(p.A, p.lda, m0, p.M, (t + 1) * BK, nxt, wave, lane);
+      if constexpr (CONV)
+        stage_conv_a<WF>(rsA, p, cbase, cy, cx, t + 1, nxt, wave, lane);
+      else
+        stage_tile<WF>(p.A, p.lda, m0, p.M, (t + 1) * BK, nxt, wave, lane);
       stage_tile<WF>(p.W, p.ldw, n0, p.N, (t + 1) * BK, nxt + TB, wave, lane);
     }
     const char* As = smem + cur * 2 * TB;
@@ -596,12 +643,23 @@ int deconv_subpixel_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   return gemm_pingpong_deconv(p, epi, g_num_cus, stream);
 }
 
-template <int WF>
+template <int WF, bool CONV = false>
 static int launch_small(const GemmArgs& p, int epi, hipStream_t stream) {
   constexpr int TM = 32 * WF;
   const int tiles = ((p.M + TM - 1) / TM) * ((p.N + TM - 1) / TM);
   dim3 grid(tiles), block(GEMM_THREADS);
   const size_t lds = 4 * (size_t)TM * BK * 2;
+  if constexpr (CONV) {
+    switch (epi) {
+      case EPI_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_BF16, WF, true>), grid, block, lds, stream, p); break;
+      case EPI_RELU_BF16:
+        hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RELU_BF16, WF, true>), grid, block, lds, stream, p);
+        break;
+      case EPI_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_F32, WF, true>), grid, block, lds, stream, p); break;
+      default: return -3;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -4;
+  }
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_BF16, WF>), grid, block, lds, stream, p); break;
     case EPI_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_GELU_BF16, WF>), grid, block, lds, stream, p); break;
@@ -614,6 +672,31 @@ static int launch_small(const GemmArgs& p, int epi, hipStream_t stream) {
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+// small-kernel tile choice: 64x64 when 128x128 tiles cannot occupy every CU once (and K is long enough to
+// be worth it), or would leave half of every tile's columns empty (N <= 64: the ID stage-1 convolutions)
+static bool use_tile64(const GemmArgs& p) {
+  if (!g_num_cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
+      g_num_cus = 256;
+  }
+  const int tiles128 = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  return g_gemm_tile64 && ((tiles128 < g_num_cus && p.K >= 256) || p.N <= 64);
+}
+
+int conv_small_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
+  if (p.conv_c <= 0 || p.conv_c % 64 || p.conv_k <= 0 || p.conv_s <= 0 || p.conv_p < 0 || p.conv_h <= 0 ||
+      p.conv_w <= 0 || p.K != p.conv_k * p.conv_k * p.conv_c || p.ldw % 8 || p.M <= 0 || p.N <= 0)
+    return -1;
+  const int oh = (p.conv_h + 2 * p.conv_p - p.conv_k) / p.conv_s + 1;
+  const int ow = (p.conv_w + 2 * p.conv_p - p.conv_k) / p.conv_s + 1;
+  if (oh <= 0 || ow <= 0 || p.M % (oh * ow)) return -1;
+  const int64_t in_bytes = (int64_t)(p.M / (oh * ow)) * p.conv_h * p.conv_w * p.conv_c * 2;
+  if (in_bytes >= (1ll << 31)) return -1;
+  return use_tile64(p) ? launch_small<2, true>(p, epi, stream) : launch_small<4, true>(p, epi, stream);
 }
 
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
@@ -636,17 +719,7 @@ int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
     if (p.K % B2K == 0 && epi != EPI_NCHW_F32 && (p.N % 4) == 0 && (p.ldc % 4) == 0) return gemm256(p, epi, stream);
     return -1;
   }
-  if (!g_num_cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
-      g_num_cus = 256;
-  }
-  // 64x64 tiles when 128x128 ones cannot occupy every CU once (and K is long enough to be worth it), or
-  // would leave half of every tile's columns empty (N <= 64: the ID classifier's stage-1 convolutions)
-  const int tiles128 = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  if (g_gemm_tile64 && ((tiles128 < g_num_cus && p.K >= 256) || p.N <= 64)) return launch_small<2>(p, epi, stream);
-  return launch_small<4>(p, epi, stream);
+  return use_tile64(p) ? launch_small<2>(p, epi, stream) : launch_small<4>(p, epi, stream);
 }
 
 

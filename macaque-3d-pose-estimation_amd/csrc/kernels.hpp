@@ -29,6 +29,10 @@ struct GemmArgs {
   // output pixels, lda = conv_c channels, K = 9 * conv_c in (ky * 3 + kx) * conv_c + c order; the A tile
   // rows of each K-step are gathered from the tap's shifted pixels (zeros outside the image)
   int conv_h = 0, conv_w = 0, conv_c = 0;
+  // implicit k x k / stride / pad convolution in the 128x128 / 64x64 kernel (conv_c % 64 == 0): conv_h /
+  // conv_w are the INPUT size, M = n * OH * OW output pixels, K = k * k * conv_c in (ky * k + kx) * C + c
+  // order (the ID classifier's mq_id_im2col order); the ping-pong conv path takes 3 / 1 / 1 only
+  int conv_k = 3, conv_s = 1, conv_p = 1;
   void* C2 = nullptr;       // EPI_RESID_RELU: bf16 copy of the output, ldc
   // EPI_BF16 with head_dim > 0: head-major output, column n of row m at
   // C[((n / head_dim) * M + m) * head_dim + n % head_dim] (the ViT qkv GEMM -> attention; ldc unused)
@@ -45,6 +49,9 @@ __device__ __forceinline__ unsigned short* gemm_out_bf16(const GemmArgs& p, int 
 int gemm_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 // implicit-GEMM 3x3 convolution (ping-pong kernel only; conv_c % 64 == 0)
 int conv3x3_bf16(const GemmArgs& p, int epi, hipStream_t stream);
+// k x k / stride / pad convolution as an implicit GEMM on the 128x128 / 64x64 kernel (same bits as
+// mq_id_im2col + gemm_bf16 on those tiles); conv_c % 64 == 0
+int conv_small_bf16(const GemmArgs& p, int epi, hipStream_t stream);
 // ConvTranspose2d(k4, s2, p1) as one sub-pixel implicit GEMM (ping-pong kernel): A = NHWC input
 // (conv_h x conv_w x conv_c), W = deconv_subpixel_pack output [4 classes x C_out][4 taps x conv_c],
 // bias [4 x C_out], C = NHWC (2 conv_h x 2 conv_w x C_out) bf16; C_out % 256 == 0, conv_c % 64 == 0

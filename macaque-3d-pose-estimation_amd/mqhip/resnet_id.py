@@ -126,6 +126,7 @@ class ResNetIdHip:
                 if bi == 0:
                     blk["down"] = fold(p + ".downsample.0.weight", p + ".downsample.1", stride, 0)
                 self.blocks.append(blk)
+        self.implicit_conv = True  # 3x3 / strided 1x1 convolutions as implicit GEMMs (False: im2col + GEMM)
         self.fc_w = weights["head.fc.weight"].detach().float().contiguous().to(d)
         self.fc_b = weights["head.fc.bias"].detach().float().contiguous().to(d)
 
@@ -137,6 +138,22 @@ class ResNetIdHip:
         _lib.check(self.ctx.lib.mq_gemm_bf16(self.ctx.handle, _lib.ptr(A), _lib.ptr(cv["w"]), _lib.ptr(C),
                                              _lib.ptr(cv["b"]), None, M, cv["co"], cv["kpad"], cv["kpad"],
                                              cv["kpad"], cv["co"], 0, epi, self._s()), "mq_gemm_bf16")
+
+    def _conv(self, x, n, h, w, cv, epi, dtype=torch.bfloat16):
+        """k x k / stride convolution of the NHWC bf16 map x: an implicit GEMM when the input channels are a
+        multiple of 64 (every 3x3 and strided 1x1 of the bottlenecks), else im2col + GEMM (the stem);
+        both give the same bits.  Returns (y (n*oh*ow, co), oh, ow)."""
+        oh = (h + 2 * cv["pad"] - cv["kh"]) // cv["stride"] + 1
+        ow = (w + 2 * cv["pad"] - cv["kw"]) // cv["stride"] + 1
+        y = torch.empty((n * oh * ow, cv["co"]), device=self.dev, dtype=dtype)
+        if self.implicit_conv and cv["ci"] % 64 == 0 and cv["kh"] == cv["kw"] and cv["kpad"] == cv["kh"] ** 2 * cv["ci"]:
+            _lib.check(self.ctx.lib.mq_id_conv_bf16(self.ctx.handle, _lib.ptr(x), n, h, w, cv["ci"], cv["kh"],
+                                                    cv["stride"], cv["pad"], _lib.ptr(cv["w"]), _lib.ptr(cv["b"]),
+                                                    _lib.ptr(y), cv["co"], epi, self._s()), "mq_id_conv_bf16")
+        else:
+            cols, _, _ = self._im2col(x, n, h, w, cv)
+            self._gemm(cols, cv, y, n * oh * ow, epi)
+        return y, oh, ow
 
     def _im2col(self, x, n, h, w, cv):
         oh = (h + 2 * cv["pad"] - cv["kh"]) // cv["stride"] + 1
@@ -184,15 +201,15 @@ class ResNetIdHip:
             M = n * h * w
             h1 = torch.empty((M, c1["co"]), device=self.dev, dtype=torch.bfloat16)
             self._gemm(a, c1, h1, M, EPI_RELU)
-            cols, oh, ow = self._im2col(h1, n, h, w, c2)
+            h2, oh, ow = self._conv(h1, n, h, w, c2, EPI_RELU)
             Mo = n * oh * ow
-            h2 = torch.empty((Mo, c2["co"]), device=self.dev, dtype=torch.bfloat16)
-            self._gemm(cols, c2, h2, Mo, EPI_RELU)
             if "down" in blk:
                 dn = blk["down"]
-                src = a if dn["stride"] == 1 else self._im2col(a, n, h, w, dn)[0]
-                xs = torch.empty((Mo, dn["co"]), device=self.dev, dtype=torch.float32)
-                self._gemm(src, dn, xs, Mo, EPI_F32)
+                if dn["stride"] == 1:
+                    xs = torch.empty((Mo, dn["co"]), device=self.dev, dtype=torch.float32)
+                    self._gemm(a, dn, xs, Mo, EPI_F32)
+                else:
+                    xs = self._conv(a, n, h, w, dn, EPI_F32, dtype=torch.float32)[0]
             # conv3 + residual + ReLU in one epilogue: the f32 stream and the next block's bf16 operand
             a = torch.empty((Mo, c3["co"]), device=self.dev, dtype=torch.bfloat16)
             _lib.check(self.ctx.lib.mq_gemm_resid_relu_bf16(self.ctx.handle, _lib.ptr(h2), _lib.ptr(c3["w"]),

@@ -154,3 +154,52 @@ def test_step1_classify_patches_and_process_frame(frames, monkeypatch):
             assert abs(row[7] - r["pred_score"]) <= 2e-2
             if abs(r["pred_score"] - s1.ID_CONF_THR) > 2e-2:
                 assert row[6] == (r["pred_label"] if r["pred_score"] >= s1.ID_CONF_THR else -1)
+
+
+@pytest.mark.parametrize("n,h,w,c,k,s,p,cout,epi", [(13, 56, 56, 64, 3, 1, 1, 64, 6), (13, 56, 56, 256, 1, 2, 0, 512, 4),
+                                                    (13, 56, 56, 128, 3, 2, 1, 128, 6), (13, 14, 14, 256, 3, 1, 1, 256, 6),
+                                                    (3, 7, 7, 512, 3, 1, 1, 512, 0), (2, 15, 12, 64, 3, 2, 1, 24, 4)])
+def test_implicit_conv_equals_im2col_gemm(n, h, w, c, k, s, p, cout, epi):
+    """mq_id_conv_bf16 (the A tile of each K-step gathered from the tap-shifted input pixels, zero padding from
+    out-of-range DMA offsets) gives the bits of mq_id_im2col + mq_gemm_bf16: same K order, same tiles."""
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    g = torch.Generator(device="cuda").manual_seed(n + h + c + k + s)
+    x = torch.randn((n, h, w, c), generator=g, device="cuda").to(torch.bfloat16)
+    wt = (torch.randn((cout, k * k * c), generator=g, device="cuda") / (k * c ** 0.5)).to(torch.bfloat16)
+    bias = torch.randn((cout,), generator=g, device="cuda")
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    M = n * oh * ow
+    dt = torch.float32 if epi == 4 else torch.bfloat16
+    got = torch.empty((M, cout), device="cuda", dtype=dt)
+    _lib.check(ctx.lib.mq_id_conv_bf16(ctx.handle, _lib.ptr(x), n, h, w, c, k, s, p, _lib.ptr(wt), _lib.ptr(bias),
+                                       _lib.ptr(got), cout, epi, _lib.stream_ptr()), "mq_id_conv_bf16")
+    cols = torch.empty((M, k * k * c), device="cuda", dtype=torch.bfloat16)
+    _lib.check(ctx.lib.mq_id_im2col(ctx.handle, _lib.ptr(x), n, h, w, c, k, k, s, p, k * k * c, _lib.ptr(cols),
+                                    _lib.stream_ptr()), "mq_id_im2col")
+    ref = torch.empty_like(got)
+    # the explicit GEMM takes the 256x256 kernels at large M x N; the implicit one always the 128 / 64 tiles
+    big = ((M + 255) // 256) * ((cout + 255) // 256) >= 128 and cout >= 256
+    old = ctx.lib.mq_get_tuning(2)
+    try:
+        assert ctx.lib.mq_set_tuning(2, 1) == 0   # the explicit GEMM on the same small-tile kernel
+        _lib.check(ctx.lib.mq_gemm_bf16(ctx.handle, _lib.ptr(cols), _lib.ptr(wt), _lib.ptr(ref), _lib.ptr(bias), None,
+                                        M, cout, k * k * c, k * k * c, k * k * c, cout, 0, epi, _lib.stream_ptr()),
+                   "gemm")
+    finally:
+        ctx.lib.mq_set_tuning(2, old)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), (big, (got.float() - ref.float()).abs().max().item())
+
+
+def test_classifier_implicit_conv_matches_im2col(frames):
+    """The whole ResNet-152 forward with the implicit convolutions equals the im2col path bit for bit."""
+    _, m = _model(152, seed=1)
+    dev = torch.as_tensor(frames).cuda()
+    x, _ = m.preprocess(dev, BOXES)
+    outs = []
+    for implicit in (False, True):
+        m.implicit_conv = implicit
+        outs.append([t.clone() for t in m.forward(x)])
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])

@@ -1,6 +1,7 @@
 """Time the ResNet-152 ID classifier forward (random weights) on n boxes, in one process, under the
 same-result GEMM routing knob MQ_TUNE_GEMM_TILE64 (64x64 tiles for GEMMs that cannot fill the CUs with
-128x128 ones) on and off, and check that both give identical probabilities.
+128x128 ones) on and off and the implicit-GEMM convolutions on and off, and check that every variant
+gives identical probabilities.
 
 python tools/id_probe.py [n_boxes ...]      (default: 13 32 -- a config-5 frame's tracked boxes, 32)"""
 import os
@@ -24,7 +25,8 @@ def main():
             x = torch.randn((n, 224, 224, 3), device="cuda").to(torch.bfloat16)
             ref = None
             for rnd in range(3):
-                for t64 in (1, 0):
+                for t64, implicit in ((1, True), (1, False), (0, True)):
+                    m.implicit_conv = implicit
                     _lib.check(lib.mq_set_tuning(19, t64), "knob")
                     for _ in range(2):
                         _, probs = m.forward(x)
@@ -36,7 +38,7 @@ def main():
                     for _ in range(10):
                         m.forward(x)
                     torch.cuda.synchronize()
-                    print(f"r={rnd} ResNet-152 ID forward, {n} boxes, tile64={t64}: "
+                    print(f"r={rnd} ResNet-152 ID forward, {n} boxes, tile64={t64} implicit_conv={implicit}: "
                           f"{(time.perf_counter() - t0) * 100:.2f} ms  identical={same}", flush=True)
     finally:
         lib.mq_set_tuning(19, old)
