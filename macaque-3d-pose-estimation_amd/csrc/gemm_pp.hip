@@ -35,11 +35,12 @@
 // Accumulation order per output element is the one of gemm256_kernel (K in ascending 32-deep
 // MFMA steps, then + bias, then the epilogue op), so both kernels give bit-identical results.
 //
-// The tile geometry is a template (PPShape<WMF, WNF>: MFMA fragments per wave in M and N, phase split,
-// DMA issue plan and counted waits derived from it); the library instantiates 256 x 256.  A 192 x 320
-// shape (6 x 5 fragments per wave, 18 / 12 / 18 / 12 MFMAs per phase, DMA plan 3 / 2 / 2 / 1) fills whole
-// CU rounds for fc1 / qkv / fc2 / proj but measured 1 % slower end to end in the ViT-H forward
-// (profiles/r02s3d_vit_probe_wide_tiles.log), so it is not built.
+// The tile geometry is a template (PPShape<WMF, WNF>: MFMA fragments per wave in M and N; phase split,
+// DMA issue plan and counted waits derived from it); the epilogue is written for WNF = 4 and the library
+// instantiates 256 x 256.  A 192 x 320 shape (6 x 5 fragments per wave, 18 / 12 / 18 / 12 MFMAs per
+// phase, DMA plan 3 / 2 / 2 / 1, odd-fragment stores, dwordx4 bias DMA) fills whole CU rounds for fc1 /
+// qkv / fc2 / proj but measured 1 % slower end to end in the ViT-H forward
+// (profiles/r02s3d_vit_probe_wide_tiles.log); its epilogue branches were removed again.
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -60,9 +61,9 @@ struct PPShape {
   static constexpr int NB = WNF - NA;         // second N part (phases 1, 3)
   static constexpr int BM = 2 * 16 * WMF, BN = 4 * 16 * WNF;
   static constexpr int OPA = BM * PP_BK * 2;  // A slice bytes; the W slice follows it
-  // bias slice per wave: 16 WNF floats; one dword LDS-DMA covers 64 (256 B), else one dwordx4 (1 KiB)
-  static constexpr bool BIAS_X4 = WNF > 4;
-  static constexpr int BIAS_SLOT = BIAS_X4 ? 1024 : 256;
+  // bias slice per wave: 16 WNF = 64 floats, one dword LDS-DMA (256 B)
+  static_assert(WNF == 4, "the epilogue's bias read, paired stores and bias DMA are written for 4 fragments");
+  static constexpr int BIAS_SLOT = 256;
   static constexpr int LDS = PP_BIAS + 8 * BIAS_SLOT;
   // DMA groups (8 rows x 128 B = one 1-KiB wave instruction) in first-read order: P0 A, P0 W, P1 W, P2 A
   static constexpr int GA0 = BM / 16;         // P0 A groups (M half 0 of both wave groups)
@@ -78,7 +79,7 @@ struct PPShape {
   // counted waits (vector memory ops younger than the ones retired): see the kernel
   static constexpr int N0 = C3 + C0 + 1, N1 = C0 + 1 + C1, N3 = C2 + C3;
   // epilogue stores per wave of a full tile (bf16: pairs of fragments as 16-B rows + an 8-B tail)
-  static constexpr int STORES_BF16 = WMF * (WNF / 2 + (WNF & 1));
+  static constexpr int STORES_BF16 = WMF * (WNF / 2);
   static constexpr int STORES_F32 = WMF * WNF;
 };
 using Shape256 = PPShape<8, 4>;
@@ -175,22 +176,12 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
   f32x4 bv[WNF];
   {
     const unsigned addr = (unsigned)(uintptr_t)MQ_LDS_LOCAL(bias_lds + nn);
-    if constexpr (WNF == 4) {
-      asm volatile(
-          "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
-          "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
-          : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
-          : "v"(addr)
-          : "memory");
-    } else {
-      static_assert(WNF == 5, "bias read for 4 or 5 fragments");
-      asm volatile(
-          "ds_read_b128 %0, %5\n\tds_read_b128 %1, %5 offset:64\n\tds_read_b128 %2, %5 offset:128\n\t"
-          "ds_read_b128 %3, %5 offset:192\n\tds_read_b128 %4, %5 offset:256\n\ts_waitcnt lgkmcnt(0)"
-          : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3]), "=&v"(bv[4])
-          : "v"(addr)
-          : "memory");
-    }
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
+        "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
+        : "v"(addr)
+        : "memory");
   }
   float4 bias[WNF];
 #pragma unroll
@@ -258,14 +249,6 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
         if (full || (m < p.M && n < p.N))
           *reinterpret_cast<uint4*>(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n) : crow_p + n) = o;
       }
-      if constexpr (WNF & 1) {
-        float v[4];
-        act(i, WNF - 1, v);
-        const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-        const int n = nb + (WNF - 1) * 16 + nn;
-        if (full || (m < p.M && n < p.N))
-          *reinterpret_cast<uint2*>(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n) : crow_p + n) = o;
-      }
     }
     return;
   }
@@ -273,7 +256,8 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
     if (full) {
       // RG fragment rows (RG x WNF independent 16-B loads) in flight per round trip: the A/W
       // fragment registers are dead here and hold them
-      constexpr int RG = WMF % 4 == 0 ? 4 : 3;
+      constexpr int RG = 4;
+      static_assert(WMF % RG == 0, "row groups");
 #pragma unroll
       for (int i0 = 0; i0 < WMF; i0 += RG) {
         float4 x[RG][WNF];
@@ -460,24 +444,14 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     }
   };
 
-  // compute cursor: tile index, K-step in it, its origin, this wave's bias DMA offset (dword form:
-  // one column per lane; dwordx4 form: four per lane, lanes past the slice read past the buffer = 0)
+  // compute cursor: tile index, K-step in it, its origin, this wave's bias DMA offset (one column per lane)
   int ct = 0, kt = 0, cm0 = 0, cn0 = 0;
   pp_tile_coords<S>(lo + xb, tiles_m, tiles_n, cm0, cn0);
   char* bias_lds = smem + PP_BIAS + wave * S::BIAS_SLOT;
-  auto bias_offset = [&](int n0) -> unsigned {
-    if constexpr (S::BIAS_X4)
-      return 4 * lane < 16 * WNF ? (unsigned)((n0 + wcol + 4 * lane) * 4) : 0x80000000u;
-    else
-      return (unsigned)((n0 + wcol + lane) * 4);
-  };
+  auto bias_offset = [&](int n0) -> unsigned { return (unsigned)((n0 + wcol + lane) * 4); };
   unsigned bias_off = bias_offset(cn0);
-  // (literal sizes: a template-dependent size argument makes the host compilation drop the kernel stub)
   auto issue_bias = [&]() {
-    if constexpr (S::BIAS_X4)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 16, bias_off, 0, 0, 0);
-    else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
   };
 
   f32x4 acc[WMF][WNF];
