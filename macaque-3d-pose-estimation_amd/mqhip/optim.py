@@ -42,19 +42,36 @@ def median_filter_series(values, size=7):
     return np.median(win, axis=-1)[pad:-pad]
 
 
+def median_filter_columns(values, size=7):
+    """median_filter_series on every column of values (F, n) at once: the same padding, windows and
+    medians (np.median of the same 7 values), so the same numbers."""
+    pad = size + 5
+    v = np.pad(values, ((pad, pad), (0, 0)), mode="reflect")
+    h = size // 2
+    vz = np.pad(v, ((h, h), (0, 0)), mode="constant")
+    win = np.lib.stride_tricks.sliding_window_view(vz, size, axis=0)[pad:-pad]   # (F, n, size)
+    if size % 2 and not np.isnan(vz).any():
+        # odd window without NaN: np.median is the middle order statistic, exactly
+        return np.sort(win, axis=-1)[..., size // 2]
+    return np.median(win, axis=-1)
+
+
 def smooth_scale(p3ds_intp, scale_smooth):
     """scale_smooth_full = scale_smooth / mean|diff(medfilt7(interp p3d))| (cameras.py:1133-1137)."""
     F = p3ds_intp.shape[0]
-    flat = p3ds_intp.reshape(F, -1)
-    med = np.stack([median_filter_series(flat[:, i], 7) for i in range(flat.shape[1])], axis=1)
+    med = median_filter_columns(p3ds_intp.reshape(F, -1), 7)
     return scale_smooth * (1.0 / np.mean(np.abs(np.diff(med, axis=0))))
 
 
 def initial_lengths(p3ds_intp, constraints, constraints_weak):
     """_initialize_params_triangulation (cameras.py:1670-1697): median limb lengths, 0 / outlier -> median."""
     def med_len(pairs):
-        return np.array([np.median(np.linalg.norm(p3ds_intp[:, a] - p3ds_intp[:, b], axis=1)) for a, b in pairs],
-                        dtype=np.float64)
+        pairs = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+        if len(pairs) == 0:
+            return np.zeros(0, dtype=np.float64)
+        # every pair's per-frame length at once (F, P), then each column's median
+        d = np.linalg.norm(p3ds_intp[:, pairs[:, 0]] - p3ds_intp[:, pairs[:, 1]], axis=2)
+        return np.median(d, axis=0).astype(np.float64)
     jl, jlw = med_len(constraints), med_len(constraints_weak)
     alll = np.hstack([jl, jlw])
     if alll.size == 0:
@@ -73,7 +90,10 @@ def prepare(p3ds, constraints, constraints_weak, scale_smooth):
     """x0 and scale_smooth_full for one animal, exactly as the reference builds them."""
     p3ds = np.asarray(p3ds, dtype=np.float64)
     F, J, _ = p3ds.shape
-    intp = np.apply_along_axis(interpolate_series, 0, p3ds)
+    intp = p3ds.copy()
+    flat = intp.reshape(F, -1)
+    for i in np.flatnonzero(np.isnan(flat).any(axis=0)):   # only the series with gaps (others unchanged)
+        flat[:, i] = interpolate_series(flat[:, i])
     ssf = smooth_scale(intp, scale_smooth)
     jl, jlw = initial_lengths(intp, constraints, constraints_weak)
     x0 = np.hstack([intp.ravel(), jl, jlw])

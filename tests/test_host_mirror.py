@@ -1,15 +1,21 @@
 """CPU: host-side pieces of the drop-in mirror against the oracle (no GPU needed)."""
 import numpy as np
+import pytest
 
 
-def test_optim_prepare_matches_oracle_init():
-    """x0 and scale_smooth_full (cameras.py:1125-1150) are bit-identical to the oracle's."""
+@pytest.mark.parametrize("F,ties", [(50, False), (300, False), (300, True)])
+def test_optim_prepare_matches_oracle_init(F, ties):
+    """x0 and scale_smooth_full (cameras.py:1125-1150) are bit-identical to the oracle's (the mirror
+    vectorises the median filter and the limb-length medians over all series; ties exercise the
+    order-statistic median)."""
     from mqhip import synth
     from mqhip.optim import prepare
     from oracle.geometry import initialize_params_triangulation, interpolate_data, medfilt_data
-    rng = np.random.default_rng(0)
-    p3 = synth.make_skeletons(1, 50)[0] + rng.normal(0, 3, (50, 17, 3))
-    p3[rng.random((50, 17)) < 0.2] = np.nan
+    rng = np.random.default_rng(F)
+    p3 = synth.make_skeletons(1, F)[0] + rng.normal(0, 3, (F, 17, 3))
+    if ties:
+        p3 = np.round(p3 / 4) * 4
+    p3[rng.random((F, 17)) < 0.2] = np.nan
     p3[:, 4] = np.nan                                 # a joint never triangulated
     cons = synth.constraint_indices(synth.CONSTRAINTS)
     weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
