@@ -59,7 +59,8 @@ def median_filter_columns(values, size=7):
 def smooth_scale(p3ds_intp, scale_smooth):
     """scale_smooth_full = scale_smooth / mean|diff(medfilt7(interp p3d))| (cameras.py:1133-1137)."""
     F = p3ds_intp.shape[0]
-    med = median_filter_columns(p3ds_intp.reshape(F, -1), 7)
+    # the mean over the reference's (F, J, 3) shape: np.mean's pairwise summation order depends on it
+    med = median_filter_columns(p3ds_intp.reshape(F, -1), 7).reshape(p3ds_intp.shape)
     return scale_smooth * (1.0 / np.mean(np.abs(np.diff(med, axis=0))))
 
 
