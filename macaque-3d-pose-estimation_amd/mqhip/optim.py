@@ -59,8 +59,12 @@ def median_filter_columns(values, size=7):
 def smooth_scale(p3ds_intp, scale_smooth):
     """scale_smooth_full = scale_smooth / mean|diff(medfilt7(interp p3d))| (cameras.py:1133-1137)."""
     F = p3ds_intp.shape[0]
-    # the mean over the reference's (F, J, 3) shape: np.mean's pairwise summation order depends on it
     med = median_filter_columns(p3ds_intp.reshape(F, -1), 7).reshape(p3ds_intp.shape)
+    # np.mean's summation order follows the memory layout: lay med out as the reference's
+    # np.apply_along_axis(medfilt_data, 0, ...) result is laid out (frames fastest)
+    buf = np.empty(p3ds_intp.shape[1:] + (F,), dtype=np.float64)
+    buf[...] = np.moveaxis(med, 0, -1)
+    med = np.moveaxis(buf, -1, 0)
     return scale_smooth * (1.0 / np.mean(np.abs(np.diff(med, axis=0))))
 
 
