@@ -29,7 +29,13 @@
 extern "C" {
 #endif
 
-#define MQ_ABI_VERSION 1
+/* ABI history:
+ *   1 -- rounds 1-2.
+ *   2 -- mq_viterbi_filter accepts n_back in [1, 3] only (was [1, 8]); the timing-ablation tuning keys and
+ *        MQ_TUNE_ATTENTION_V2 (key 17, the first-generation attention kernel) were removed and now return -2;
+ *        MQ_TUNE_OPTIM_PCG_ITERS defaults to 20 (was 40; optim_points results stay within their tolerance);
+ *        mq_det_topk_boxes added (config-5 capturable box selection). */
+#define MQ_ABI_VERSION 2
 
 typedef struct mq_ctx mq_ctx;
 typedef struct mq_vitpose mq_vitpose;
@@ -41,15 +47,14 @@ const char* mq_last_error(void);
  * same results (tested equal); the PCG cap changes only the inner-solve accuracy of optim_points,
  * whose results stay within that stage's tolerance.  No knob can select a variant that computes
  * something else.  Changing one makes the next mq_vitpose_forward re-capture its graph. */
-#define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 kernel (default 0) */
+#define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 / 64x64 kernel (default 0; the reference
+                                       route of the bitwise implicit-convolution tests) */
 #define MQ_TUNE_OPTIM_PCG_ITERS 4   /* cap on the conjugate-gradient iterations per Levenberg-Marquardt step (default 20;
                                        results stay within the optim_points tolerance) */
 #define MQ_TUNE_GEMM_PINGPONG 12    /* 1 (default): 256x256 GEMMs with K % 64 == 0 on the ping-pong kernel (wave groups
                                        alternate LDS traffic and MFMA, gemm_pp.hip); 0: the interleaved-K-step kernel */
 #define MQ_TUNE_OPTIM_PRECOND_LDS 18 /* 1 (default): optim_points' preconditioner on the series staged in LDS when it
                                         fits; 0: the global-memory substitution kernel (same preconditioner) */
-#define MQ_TUNE_ATTENTION_V2 17     /* 1 (default): attention on 16x16x32 QK^T + transposed-output PV (vit_ops.hip
-                                       attention2_kernel); 0: the first-generation kernel */
 #define MQ_TUNE_GEMM_TILE64 19      /* 1 (default): GEMMs whose 128x128 tiles cannot occupy every CU once take the
                                        64x64-tile kernel (same accumulation order, tested equal); 0: 128x128 */
 #define MQ_TUNE_QKV_HEAD_MAJOR 20   /* 1 (default): the ViT qkv GEMM writes Q / K / V head-major (each head's rows

@@ -155,9 +155,6 @@ int mq_set_tuning(int key, int value) {
       if (value < 1 || value > 128) return fail("mq_set_tuning: PCG iterations must be in [1, 128]", -2);
       mq::g_optim_pcg_iters = value;
       break;
-    case MQ_TUNE_ATTENTION_V2:
-      mq::g_attention_v2 = value != 0;
-      break;
     case MQ_TUNE_OPTIM_PRECOND_LDS:
       mq::g_optim_precond_lds = value != 0;
       break;
@@ -179,7 +176,6 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_GEMM_FORCE_SMALL: return mq::g_gemm_force_small ? 1 : 0;
     case MQ_TUNE_GEMM_PINGPONG: return mq::g_gemm_pingpong;
     case MQ_TUNE_OPTIM_PCG_ITERS: return mq::g_optim_pcg_iters;
-    case MQ_TUNE_ATTENTION_V2: return mq::g_attention_v2;
     case MQ_TUNE_OPTIM_PRECOND_LDS: return mq::g_optim_precond_lds;
     case MQ_TUNE_GEMM_TILE64: return mq::g_gemm_tile64;
     case MQ_TUNE_QKV_HEAD_MAJOR: return g_qkv_head_major;

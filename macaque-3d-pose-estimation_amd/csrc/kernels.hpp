@@ -71,7 +71,6 @@ int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, un
                        float eps, hipStream_t s);
 int layernorm_f32_f32(const float* x, const float* gamma, const float* beta, float* y, int rows, int dim, float eps,
                       hipStream_t s);
-extern int g_attention_v2;  // 1 (default): attention2_kernel; 0: the first-generation kernel
 // head_major: qkv holds the head-major blocks of the qkv GEMM's head_dim output (GemmArgs::head_dim)
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s, bool head_major = false);

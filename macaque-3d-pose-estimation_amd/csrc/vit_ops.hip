@@ -86,27 +86,16 @@ int layernorm_f32_f32(const float* x, const float* gamma, const float* beta, flo
 }
 
 // ---------------------------------------------------------------- attention
-// One workgroup (6 waves) per (image, head).  K and V are staged ROW-MAJOR in LDS by LDS-DMA
-// (global_load_lds_dwordx4: no VGPR round trip, no packing VALU, conflict-free lane-linear
-// writes); Q fragments go straight to registers.  Each wave owns two 16-query blocks and runs
-// them together:
-//   S^T = K Q^T   v_mfma_f32_16x16x16_bf16 (query on the lane, tokens in registers), K read by
-//                 rows (ds_read_b64) from an image with 11 x 16-B chunks per row (conflict-free);
-//   softmax       in registers + 2 cross-lane steps, P packed to bf16 in PV operand order;
-//   O = P V       v_mfma_f32_16x16x32_bf16 with the V operand gathered by ds_read_b64_tr_b16
-//                 (hardware transpose) from a row-major image whose row stride (40 dwords) makes
-//                 the transposed reads conflict-free.
+// One workgroup (6 waves) per (image, head); K and V staged whole in LDS by LDS-DMA; each wave owns
+// two 16-query blocks (attention2_kernel below).
 constexpr int ATT_WAVES = 6;  // 12 query blocks of 16 at T = 192: two per wave
 constexpr int ATT_THREADS = 64 * ATT_WAVES;
 constexpr int ATT_MAXT = 192;
 
 template <int DH>
 struct AttLayout {
-  static constexpr int KCH = DH / 8 + 1;           // K row: DH/8 data chunks + 1 pad chunk
   static constexpr int VCH = DH == 64 ? 10 : DH / 8;  // V row stride in 16-B chunks (= 8 * odd dwords mod 64)
-  static constexpr int KBYTES = (ATT_MAXT * KCH + 63) / 64 * 1024;
   static constexpr int VBYTES = (ATT_MAXT * VCH + 63) / 64 * 1024;
-  static constexpr int LDS = KBYTES + VBYTES;
 };
 
 // Q / K / V rows of (image, head): row-major QKV (ld = 3 D; sections at columns 0, D, 2 D, the head at
@@ -137,169 +126,9 @@ __device__ __forceinline__ int att_item(int H) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-// TT: compile-time token count (192 = the ViT-H 256x192 grid) so every per-block guard
-// folds away; 0 = runtime T (other grids / tests).
-template <int DH, int TT = 0>
-__global__ __launch_bounds__(ATT_THREADS, 3) void attention_kernel(const bf16_t* __restrict__ qkv,
-                                                                    bf16_t* __restrict__ out, int T_rt, int D,
-                                                                    int H, float scale_log2, int nt_hm) {
-  using L = AttLayout<DH>;
-  const int T = TT ? TT : T_rt;
-  constexpr int NKS = DH / 16;  // k-steps of QK^T
-  constexpr int DCH = DH / 8;   // data chunks per row
-  constexpr int MAXT = ATT_MAXT;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Kimg = smem;
-  char* Vimg = smem + L::KBYTES;
-
-  const int item = att_item(H);
-  const int img = item / H, h = item % H;
-  const size_t row0 = (size_t)img * T;
-  const bf16_t *qbase, *kbase, *vbase;
-  const int ld = att_bases<DH>(qkv, D, H, h, row0, nt_hm, qbase, kbase, vbase);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int l16 = lane & 15, g = lane >> 4;
-  const int ntb = T / 16;
-
-  // K / V images by LDS-DMA: instruction i of the image writes chunks 64 i .. 64 i + 63
-  // (lane-linear); a chunk is (token, 16-B piece); pad / tail lanes re-load chunk 0.
-  const int nk_ins = (T * L::KCH + 63) / 64, nv_ins = (T * L::VCH + 63) / 64;
-  for (int ins = wave; ins < nk_ins; ins += ATT_WAVES) {
-    const int q = ins * 64 + lane;
-    int t = q / L::KCH, ch = q - (q / L::KCH) * L::KCH;
-    if (t >= T || ch >= DCH) t = 0, ch = 0;
-    __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(kbase + (size_t)t * ld + ch * 8), MQ_LDS_LOCAL(Kimg + ins * 1024),
-                                     16, 0, 0);
-  }
-  for (int ins = wave; ins < nv_ins; ins += ATT_WAVES) {
-    const int q = ins * 64 + lane;
-    int t = q / L::VCH, ch = q - (q / L::VCH) * L::VCH;
-    if (t >= T || ch >= DCH) t = 0, ch = 0;
-    __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(vbase + (size_t)t * ld + ch * 8), MQ_LDS_LOCAL(Vimg + ins * 1024),
-                                     16, 0, 0);
-  }
-  // this wave's query blocks (wave, wave + ATT_WAVES): Q fragments straight to registers
-  constexpr int QB_PER_WAVE = (MAXT / 16 + ATT_WAVES - 1) / ATT_WAVES;
-  static_assert(QB_PER_WAVE == 2, "two query blocks per wave");
-  short4v qf[2][NKS];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int qb = min(wave + u * ATT_WAVES, ntb - 1);
-    const int q = qb * 16 + l16;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-      qf[u][ks] = *reinterpret_cast<const short4v*>(qbase + (size_t)q * ld + ks * 16 + 4 * g);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (wave >= ntb) return;
-  const bool has1 = (TT == MAXT) ? true : (wave + ATT_WAVES < ntb);
-
-  f32x4 S[2][MAXT / 16];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int tb = 0; tb < MAXT / 16; ++tb) S[u][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-#pragma unroll
-    for (int tb = 0; tb < MAXT / 16; ++tb) {
-      if (tb < ntb) {
-        const short4v kf =
-            *reinterpret_cast<const short4v*>(Kimg + (tb * 16 + l16) * (L::KCH * 16) + (ks * 16 + 4 * g) * 2);
-        S[0][tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[0][ks], S[0][tb], 0, 0, 0);
-        if (has1) S[1][tb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(kf, qf[1][ks], S[1][tb], 0, 0, 0);
-      }
-    }
-  }
-  // softmax over tokens for query (column l16): values spread over registers and lane groups g;
-  // P is packed to bf16 in the PV operand order (tokens tb0*16+4g+0..3, (tb0+1)*16+4g+0..3)
-  bf16x8 P[2][MAXT / 32];
-  float lsum[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    float m = -INFINITY;
-#pragma unroll
-    for (int tb = 0; tb < MAXT / 16; ++tb)
-      if (tb < ntb) m = fmaxf(m, fmaxf(fmaxf(S[u][tb][0], S[u][tb][1]), fmaxf(S[u][tb][2], S[u][tb][3])));
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    const float mb = m * scale_log2;
-    float ls = 0.f;
-#pragma unroll
-    for (int tb = 0; tb < MAXT / 16; ++tb) {
-      if (tb < ntb) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float pv = __builtin_amdgcn_exp2f(S[u][tb][e] * scale_log2 - mb);
-          S[u][tb][e] = pv;
-          ls += pv;
-        }
-      }
-    }
-    ls += __shfl_xor(ls, 16, 64);
-    ls += __shfl_xor(ls, 32, 64);
-    lsum[u] = ls;
-#pragma unroll
-    for (int kst = 0; kst < MAXT / 32; ++kst) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        P[u][kst][e] = (__bf16)S[u][2 * kst][e];
-        P[u][kst][4 + e] = (__bf16)S[u][2 * kst + 1][e];
-      }
-    }
-  }
-
-  f32x4 O[2][NKS];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int dt = 0; dt < NKS; ++dt) O[u][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // transposed read: lane 4q+p of each 16-lane group addresses row r0+q, columns c0+4p..+3 and
-  // receives column c0 + (lane & 15) of those 4 rows
-  const int trq = l16 >> 2, trp = l16 & 3;
-#pragma unroll
-  for (int kst = 0; kst < MAXT / 32; ++kst) {
-    if (kst < T / 32) {
-#pragma unroll
-      for (int dt = 0; dt < NKS; ++dt) {
-        const int ra = 2 * kst * 16 + 4 * g + trq;
-        const char* pa = Vimg + ra * (L::VCH * 16) + (dt * 16 + 4 * trp) * 2;
-        const short4v v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa));
-        const short4v v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) short4v*)MQ_LDS_LOCAL(pa + 16 * (L::VCH * 16)));
-        bf16x8 vb;
-        const short4v* pv0 = &v0;
-        const short4v* pv1 = &v1;
-        __builtin_memcpy(&vb, pv0, 8);
-        __builtin_memcpy(reinterpret_cast<char*>(&vb) + 8, pv1, 8);
-        O[0][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[0][kst], vb, O[0][dt], 0, 0, 0);
-        if (has1) O[1][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(P[1][kst], vb, O[1][dt], 0, 0, 0);
-      }
-    }
-  }
-  // O C-layout: col = l16 -> d, row = 4g + e -> query; normaliser lives in lane (4g + e)
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    if (u == 1 && !has1) break;
-    const int qb = wave + u * ATT_WAVES;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float inv = 1.0f / __shfl(lsum[u], 4 * g + e, 64);
-      const int qq = qb * 16 + 4 * g + e;
-      bf16_t* orow = out + (row0 + qq) * D + h * DH;
-#pragma unroll
-      for (int dt = 0; dt < NKS; ++dt) orow[dt * 16 + l16] = __builtin_bit_cast(bf16_t, (__bf16)(O[u][dt][e] * inv));
-    }
-  }
-}
-
-// ---------------------------------------------------------------- attention, version 2
-// Same work split (one 6-wave workgroup per (image, head), two 16-query blocks per wave, K/V
-// staged whole in LDS by LDS-DMA, Q fragments straight to registers), rebuilt around the gfx950
-// MFMA forms and the output path:
+// ---------------------------------------------------------------- attention kernel
+// One 6-wave workgroup per (image, head), two 16-query blocks per wave, K/V staged whole in LDS by
+// LDS-DMA, Q fragments straight to registers:
 //   S^T = K Q^T   v_mfma_f32_16x16x32_bf16: ceil(DH/32) k-steps of 32 (the last one half
 //                 zero-padded on the Q side when DH % 32 == 16) instead of DH/16 steps of the
 //                 half-rate 16x16x16 form.  K image rows of 10 x 16-B chunks (80 d = 160 B, no
@@ -526,27 +355,15 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
   }
 }
 
-int g_attention_v2 = 1;
-
 template <int DH>
 static void launch_attention(dim3 grid, dim3 block, hipStream_t s, const unsigned short* qkv, unsigned short* out,
                              int tokens, int dim, int heads, float scale_log2, int nt_hm) {
-  constexpr int lds = AttLayout<DH>::LDS;
-  if (g_attention_v2) {
-    constexpr int lds2 = (ATT_MAXT * ATT2_KCH + 63) / 64 * 1024 + AttLayout<DH>::VBYTES;
-    if (tokens == ATT_MAXT)
-      hipLaunchKernelGGL((attention2_kernel<DH, ATT_MAXT>), grid, block, lds2, s, qkv, out, tokens, dim, heads,
-                         scale_log2, nt_hm);
-    else
-      hipLaunchKernelGGL((attention2_kernel<DH, 0>), grid, block, lds2, s, qkv, out, tokens, dim, heads, scale_log2,
-                         nt_hm);
-    return;
-  }
+  constexpr int lds2 = (ATT_MAXT * ATT2_KCH + 63) / 64 * 1024 + AttLayout<DH>::VBYTES;
   if (tokens == ATT_MAXT)
-    hipLaunchKernelGGL((attention_kernel<DH, ATT_MAXT>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2,
-                       nt_hm);
+    hipLaunchKernelGGL((attention2_kernel<DH, ATT_MAXT>), grid, block, lds2, s, qkv, out, tokens, dim, heads,
+                       scale_log2, nt_hm);
   else
-    hipLaunchKernelGGL((attention_kernel<DH, 0>), grid, block, lds, s, qkv, out, tokens, dim, heads, scale_log2,
+    hipLaunchKernelGGL((attention2_kernel<DH, 0>), grid, block, lds2, s, qkv, out, tokens, dim, heads, scale_log2,
                        nt_hm);
 }
 

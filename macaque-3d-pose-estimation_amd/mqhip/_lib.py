@@ -13,6 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmq_hip.so"))
+ABI_VERSION = 2  # include/mq_hip.h MQ_ABI_VERSION
 
 EXPORTED = [
     "mq_abi_version", "mq_last_error", "mq_set_tuning", "mq_get_tuning", "mq_create", "mq_destroy",
@@ -110,7 +111,7 @@ def load(path: str = LIB_PATH):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.mq_abi_version() != 1:
+        if lib.mq_abi_version() != ABI_VERSION:
             raise MqError("libmq_hip ABI version mismatch")
         _lib = lib
         return lib

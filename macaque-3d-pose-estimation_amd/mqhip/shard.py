@@ -37,6 +37,16 @@ def gather_keypoints(kp_local: torch.Tensor, n_frames: int, world: int, group=No
     return torch.cat(out, dim=0)
 
 
+def n_joints_of(pose_model, default=17):
+    """Keypoints per instance of a pose model (PoseModelHip / VitPoseHip: cfg.n_joints; an mmpose-style
+    model: dataset_meta['num_keypoints'])."""
+    cfg = getattr(pose_model, "cfg", None)
+    if cfg is not None and getattr(cfg, "n_joints", None):
+        return int(cfg.n_joints)
+    meta = getattr(pose_model, "dataset_meta", None) or {}
+    return int(meta.get("num_keypoints", default))
+
+
 def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, steps_per_batch=8,
                       kp_params=None, device=None):
     """BASELINE config 3: the step-1 pose slice of a clip, time steps sharded across ranks.
@@ -56,10 +66,9 @@ def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, 
     n_steps, C = len(T), len(stores)
     s0, e0 = frame_block(n_steps, world, rank)
     raw = s1.run_pose(pose_model, stores, jobs, range(s0, e0), steps_per_batch)
-    J = 17
-    for kp, _ in raw.values():
-        J = kp.shape[1]
-        break
+    # the buffer shape must agree on every rank, also on a rank whose block holds no pose job:
+    # take J from the model, never from this rank's results
+    J = n_joints_of(pose_model)
     nb = max([len(j[2]) for js in jobs.values() for j in js] or [1])
     block = frame_block(n_steps, world, 0)[1]
     buf = torch.full((block, C, nb, J, 3), float("nan"), dtype=torch.float64)

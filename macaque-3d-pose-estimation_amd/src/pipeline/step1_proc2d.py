@@ -107,10 +107,14 @@ def detect_stores(detector, stores, T, score_thr=SCORE_THR):
         cams = [i for i, p in enumerate(plans) if not p[k][1]]
         if not cams:
             continue
-        imgs = [stores[i].image(plans[i][k][0]) for i in cams]
-        for i, (b, sc) in zip(cams, inference_detector(detector, imgs)):
-            keep = sc > score_thr
-            out[i].append((plans[i][k][0], b[keep], sc[keep]))
+        by_shape = {}
+        for i in cams:  # one detector batch per image size (cameras may differ in resolution)
+            img = stores[i].image(plans[i][k][0])
+            by_shape.setdefault(img.shape, []).append((i, img))
+        for items in by_shape.values():
+            for (i, _), (b, sc) in zip(items, inference_detector(detector, [im for _, im in items])):
+                keep = sc > score_thr
+                out[i].append((plans[i][k][0], b[keep], sc[keep]))
     return out
 
 
@@ -128,8 +132,8 @@ def init_id_model(device: str = "cuda:0", id_variant: str = "normal", weights=No
             import torch
             sd = torch.load(ck, map_location="cpu", weights_only=True)
             weights = {k: v.float() for k, v in sd.get("state_dict", sd).items()}
-        else:
-            weights = make_random_weights(152, seed=0)
+        else:  # one seed per variant, so a camera's variant shows in its (random-weight) predictions
+            weights = make_random_weights(152, seed={"normal": 0, "mff1y": 1}[id_variant])
     return ResNetIdHip(weights, depth=152, device=dev)
 
 
@@ -374,20 +378,52 @@ def run_pose(pose_model, stores, jobs, steps, steps_per_batch=8):
     return raw
 
 
+def id_variant_of(store):
+    """step1:425-426: the ID checkpoint of a camera -- 'mff1y' when its store folder name contains it."""
+    return "mff1y" if "mff1y" in os.path.basename(str(store.filename)).lower() else "normal"
+
+
+def resolve_id_models(stores, id_model, device_str="cuda:0"):
+    """One ID model (or None) per store.  ``id_model``: None (no classification: the stores' own ID
+    predictions, if any); ``"auto"`` -- the reference's rule, ``init_id_model(device, id_variant_of(store))``
+    per camera (step1:424-427), each variant built once; a dict {variant: model}; or one model for every
+    camera."""
+    if id_model is None:
+        return None
+    if isinstance(id_model, str):
+        if id_model != "auto":
+            raise ValueError(f"id_model must be None, 'auto', a dict or a model, not {id_model!r}")
+        cache = {}
+        for st in stores:
+            v = id_variant_of(st)
+            if v not in cache:
+                cache[v] = init_id_model(device_str, v)
+        return [cache[id_variant_of(st)] for st in stores]
+    if isinstance(id_model, dict):
+        return [id_model.get(id_variant_of(st)) for st in stores]
+    return [id_model] * len(stores)
+
+
 def run_id(id_model, stores, jobs, steps, steps_per_batch=8):
     """The ID classification of the given time steps' tracked boxes (step1:301-302): every job of
     ``steps_per_batch`` consecutive steps (all cameras) in ONE batched patch -> ResNet launch sequence
-    per image size.  Returns {(step, cam): [{pred_label, pred_score}] per box}."""
+    per (ID model, image size).  ``id_model``: one model, or a list with one model (or None) per store
+    (``resolve_id_models``).  Returns {(step, cam): [{pred_label, pred_score}] per box}; cameras without a
+    model get the reference's "not classified" value (label -1, score 0)."""
+    models = id_model if isinstance(id_model, (list, tuple)) else [id_model] * len(stores)
     steps = [k for k in steps if k in jobs]
     out = {}
     for b0 in range(0, len(steps), steps_per_batch):
-        by_shape = {}
+        by_key = {}
         for k in steps[b0:b0 + steps_per_batch]:
             for (c, fn, boxes, _, _) in jobs[k]:
+                if models[c] is None:
+                    out[(k, c)] = [{"pred_label": -1, "pred_score": 0.0} for _ in boxes]
+                    continue
                 img = stores[c].image(fn)
-                by_shape.setdefault(img.shape, []).append(((k, c), img, boxes))
-        for items in by_shape.values():
-            preds = id_model.classify(np.stack([im for _, im, _ in items]), [bx for _, _, bx in items])
+                by_key.setdefault((id(models[c]), img.shape), (models[c], []))[1].append(((k, c), img, boxes))
+        for model, items in by_key.values():
+            preds = model.classify(np.stack([im for _, im, _ in items]), [bx for _, _, bx in items])
             for (key, _, _), p in zip(items, preds):
                 out[key] = p
     return out
@@ -445,7 +481,8 @@ def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8
 def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None, redo=False, pose_model=None,
                         device_str="cuda:0", steps_per_batch=8, id_model=None, detector=None):
     """step1_proc2d.py:389-447 with the frame stores of ``mqhip.io.FrameStore`` and the tracker
-    rows they carry (detector / tracker / ID classifier run upstream).  Writes
+    rows they carry (or, with ``detector``, the detector -> tracker chain).  ``id_model``: see
+    ``resolve_id_models`` ("auto" = the reference's per-camera variant).  Writes
     <results_root>/<data_name>/<cam>/alldata.json and frame_num.npy."""
     import glob
     from mqhip.io import FrameStore
@@ -472,7 +509,8 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
         pose_model = init_pose_model(device=device_str)
     sel = [stores[i] for i in todo]
     tracks = None if detector is None else track_stores(detector, sel, T)
-    res = process_stores(pose_model, sel, T, steps_per_batch=steps_per_batch, id_model=id_model, tracks=tracks)
+    id_models = resolve_id_models(sel, id_model, device_str)
+    res = process_stores(pose_model, sel, T, steps_per_batch=steps_per_batch, id_model=id_models, tracks=tracks)
     for i, (rows, fn) in zip(todo, res):
         os.makedirs(out_dirs[i], exist_ok=True)
         np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))
@@ -481,9 +519,11 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
 
 
 def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0, pose_model=None, detector=None,
-         id_model=None):
-    """step1.proc (step1_proc2d.py:450) over every camera's frame store: pose (and ID with ``id_model``) on
-    the stores' tracker rows, or the full detector -> tracker -> pose -> ID chain with ``detector``.  Unlike
-    the reference (which hard-codes cuda:1, step1:50,421) the device argument is honoured."""
+         id_model="auto"):
+    """step1.proc (step1_proc2d.py:450) over every camera's frame store: pose and ID on the stores' tracker
+    rows, or the full detector -> tracker -> pose -> ID chain with ``detector``.  ``id_model="auto"`` is the
+    reference's rule (every camera classified by the ID model of its variant, step1:424-427); None keeps
+    the stores' own ID predictions (``resolve_id_models``).  Unlike the reference (which hard-codes cuda:1,
+    step1:50,421) the device argument is honoured."""
     step1_proc2d_custom(data_name, results_root, raw_root, fps=fps, pose_model=pose_model, device_str=device_str,
                         detector=detector, id_model=id_model)

@@ -43,14 +43,23 @@ def load_alldata(result_dir, cam_ids):
     return T
 
 
+def default_track_map(T, n_animal):
+    """{track id -> individual} for the smallest ``n_animal`` track ids present in the alldata rows, in
+    ascending order (synthetic stores number tracks from 0, the BoT-SORT tracker from 1)."""
+    tids = sorted({int(row[0]) for cam in T for frame in cam for row in frame})
+    if not tids:  # nothing tracked: every individual stays zero-filled
+        return {a: a for a in range(n_animal)}
+    return {t: a for a, t in enumerate(tids[:n_animal])}
+
+
 def known_assignment(T, n_animal, track_to_animal=None):
     """Trk[k] (F, C) box id of track k in each camera (-1 = absent) and Cid[k] (F,) its individual,
-    for a known {track id -> individual} map shared by all cameras (default: identity on
-    0..n_animal-1)."""
+    for a known {track id -> individual} map shared by all cameras (default: ``default_track_map``, the
+    ``n_animal`` smallest track ids present -> 0..n_animal-1)."""
     n_cam = len(T)
     n_frame = len(T[0])
     if track_to_animal is None:
-        track_to_animal = {a: a for a in range(n_animal)}
+        track_to_animal = default_track_map(T, n_animal)
     Trk, Cid = {}, {}
     for tid, a in track_to_animal.items():
         trk = np.full((n_frame, n_cam), -1, dtype=np.int64)

@@ -19,20 +19,9 @@ def _ref(qkv, n, T, D, H):
     return (a @ v).permute(0, 2, 1, 3).reshape(n * T, D)
 
 
-@pytest.fixture(params=[1, 0], ids=["v2", "v1"])
-def version(request):
-    """MQ_TUNE_ATTENTION_V2 (key 17): the shipped kernel (v2) and the first-generation one (v1)."""
-    from mqhip import _lib
-    ctx = _lib.Context.get(0)
-    old = ctx.lib.mq_get_tuning(17)
-    assert ctx.lib.mq_set_tuning(17, request.param) == 0
-    yield request.param
-    ctx.lib.mq_set_tuning(17, old)
-
-
 @pytest.mark.parametrize("n,T,D,H", [(3, 192, 1280, 16), (2, 192, 768, 12), (2, 64, 320, 4), (1, 96, 1280, 16),
                                      (64, 192, 1280, 16)])
-def test_attention_matches_fp32(n, T, D, H, version):
+def test_attention_matches_fp32(n, T, D, H):
     import torch
     from mqhip import _lib
     ctx = _lib.Context.get(0)
@@ -59,7 +48,7 @@ def test_attention_rejects_bad_shapes():
     assert ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), 1, 96, 1280, 10, None) != 0
 
 
-def test_attention_spiky_scores_match_fp32(version):
+def test_attention_spiky_scores_match_fp32():
     """A few very large keys per query: the row max dominates and most P underflow -- the softmax
     must still be normalised per query (checks the lane-local 1/l of the transposed output)."""
     import torch
