@@ -239,6 +239,17 @@ int mq_rcnn_post(mq_ctx* ctx, const float* rois, const float* head, const int32_
                  float img_h, float img_w, float inv_scale_w, float inv_scale_h, float score_thr, float iou_thr,
                  int max_det, float* det_boxes, float* det_scores, int32_t* det_counts, void* stream);
 
+/* Static top-k crop boxes per image from mq_rcnn_post's output, the capturable stand-in for the tracker's
+ * box list in the config-5 per-frame graph: per image the first k detections (score order) with score >
+ * score_thr whose int()-truncated box has positive extent (step1_proc2d.py:229-240, 255-268), expanded by
+ * step 1's dynamic margin + aspect fix in float64 (step1:270-292; margins / aspect as there: 0.2, 0.5,
+ * 0.75).  Out (n_img * k slots): boxes f32 (., 4) expanded xyxy, tight f32 (., 4) the truncated box,
+ * img_of int32 (.) = image index, valid int32 (.) = 1 for a filled slot (0: placeholder box
+ * (0, 0, 192, 256) so the crop stays in bounds). */
+int mq_det_topk_boxes(mq_ctx* ctx, const float* det_boxes, const float* det_scores, const int32_t* det_counts,
+                      int n_img, int max_det, int k, float score_thr, double min_margin, double max_margin,
+                      double desired_ar, float* boxes, float* tight, int32_t* img_of, int32_t* valid, void* stream);
+
 /* ======================================================================= ID classifier
  * Step-1 collar-ID classifier, ResNet-152 + GlobalAveragePooling + LinearClsHead (6 classes)
  * (model/id/sn_resnet152_8xb32_in1k_pretrained_optimized_finetuned.py:41-73), replacing

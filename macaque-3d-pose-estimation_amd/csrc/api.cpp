@@ -1011,6 +1011,19 @@ int mq_rcnn_post(mq_ctx* ctx, const float* rois, const float* head, const int32_
   return 0;
 }
 
+int mq_det_topk_boxes(mq_ctx* ctx, const float* det_boxes, const float* det_scores, const int32_t* det_counts,
+                      int n_img, int max_det, int k, float score_thr, double min_margin, double max_margin,
+                      double desired_ar, float* boxes, float* tight, int32_t* img_of, int32_t* valid, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!det_boxes || !det_scores || !det_counts || !boxes || !tight || !img_of || !valid)
+    return fail("mq_det_topk_boxes: null argument");
+  if (n_img <= 0 || max_det <= 0 || k <= 0 || k > max_det) return fail("mq_det_topk_boxes: bad sizes", -2);
+  if (!(desired_ar > 0) || !(max_margin >= min_margin)) return fail("mq_det_topk_boxes: bad margins", -2);
+  K_TRY(mq::det_topk_boxes(det_boxes, det_scores, det_counts, n_img, max_det, k, score_thr, min_margin, max_margin,
+                           desired_ar, boxes, tight, img_of, valid, (hipStream_t)stream));
+  return 0;
+}
+
 // ----------------------------------------------------------------------------- geometry
 static int check_geo(mq_ctx* ctx, const void* cams, int C, int n) {
   if (!ctx) return fail("null ctx");

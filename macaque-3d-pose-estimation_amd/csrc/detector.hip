@@ -666,6 +666,65 @@ __global__ void rcnn_decode_kernel(const float* __restrict__ rois, const float* 
   valid[idx] = (idx % max_rois < n_rois[img]) && (s > score_thr);
 }
 
+
+// ------------------------------------------------------------------ static top-k crop boxes (config 5 graph)
+// One thread per image.  The detections (score-ordered, det_counts[i] valid) that score above thr and
+// are non-degenerate after step 1's int() truncation (filter_tracks, step1_proc2d.py:255-268) fill the
+// first k slots in score order; each gets the dynamic-margin expansion + aspect fix of step1:270-292
+// in float64 with numpy's operation order (expand_boxes), rounded to float32.  Empty slots: valid 0 and
+// a placeholder box (the crop stays in bounds, the caller masks the keypoints).
+__global__ void det_topk_boxes_kernel(const float* __restrict__ dboxes, const float* __restrict__ dscores,
+                                      const int32_t* __restrict__ dcount, int n_img, int max_det, int k, float thr,
+                                      double mn, double mx, double ar_t, float* __restrict__ out,
+                                      float* __restrict__ tight, int32_t* __restrict__ img_of,
+                                      int32_t* __restrict__ valid) {
+  const int img = blockIdx.x * blockDim.x + threadIdx.x;
+  if (img >= n_img) return;
+  const int cnt = min(dcount[img], max_det);
+  int slot = 0;
+  for (int d = 0; d < cnt && slot < k; ++d) {
+    if (!(dscores[(size_t)img * max_det + d] > thr)) continue;
+    const float* b = dboxes + ((size_t)img * max_det + d) * 4;
+    const long long x1 = (long long)b[0], y1 = (long long)b[1], x2 = (long long)b[2], y2 = (long long)b[3];
+    if (!(x2 > x1 && y2 > y1)) continue;
+    const double w = (double)(x2 - x1), h = (double)(y2 - y1);
+    const double cx = (double)x1 + 0.5 * w, cy = (double)y1 + 0.5 * h;
+    double frac = (h - 50.0) / (200.0 - 50.0);
+    frac = frac < 0.0 ? 0.0 : (frac > 1.0 ? 1.0 : frac);
+    const double m = mx - (mx - mn) * frac;
+    double wn = w * (1.0 + m), hn = h * (1.0 + m);
+    const double ar = wn / hn;
+    const bool fix = fabs(ar - ar_t) > 0.20, wide = ar >= ar_t;
+    if (fix && !wide) wn = hn * ar_t;
+    if (fix && wide) hn = wn / ar_t;
+    const double fcx = (double)(float)cx, fcy = (double)(float)cy;
+    const double hw = 0.5 * (double)(float)wn, hh = 0.5 * (double)(float)hn;
+    const int o = img * k + slot;
+    out[4 * o + 0] = (float)(fcx - hw);
+    out[4 * o + 1] = (float)(fcy - hh);
+    out[4 * o + 2] = (float)(fcx + hw);
+    out[4 * o + 3] = (float)(fcy + hh);
+    tight[4 * o + 0] = (float)x1;
+    tight[4 * o + 1] = (float)y1;
+    tight[4 * o + 2] = (float)x2;
+    tight[4 * o + 3] = (float)y2;
+    img_of[o] = img;
+    valid[o] = 1;
+    ++slot;
+  }
+  for (; slot < k; ++slot) {
+    const int o = img * k + slot;
+    out[4 * o + 0] = 0.f;
+    out[4 * o + 1] = 0.f;
+    out[4 * o + 2] = 192.f;
+    out[4 * o + 3] = 256.f;
+    tight[4 * o + 0] = tight[4 * o + 1] = tight[4 * o + 2] = tight[4 * o + 3] = 0.f;
+    img_of[o] = img;
+    valid[o] = 0;
+  }
+}
+
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -825,6 +884,14 @@ int rcnn_post(const float* rois, const float* head, const int32_t* n_rois, int n
   if (rc) return rc;
   hipLaunchKernelGGL(gather_boxes_kernel, blocks_for((int64_t)n_img * max_det), dim3(256), 0, s, boxes, scores,
                      keep_buf, n_img, max_rois, max_det, det_boxes, det_scores);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int det_topk_boxes(const float* dboxes, const float* dscores, const int32_t* dcount, int n_img, int max_det, int k,
+                   float thr, double min_margin, double max_margin, double desired_ar, float* boxes, float* tight,
+                   int32_t* img_of, int32_t* valid, hipStream_t s) {
+  hipLaunchKernelGGL(det_topk_boxes_kernel, dim3((n_img + 63) / 64), dim3(64), 0, s, dboxes, dscores, dcount, n_img,
+                     max_det, k, thr, min_margin, max_margin, desired_ar, boxes, tight, img_of, valid);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -65,5 +65,8 @@ size_t rcnn_workspace_bytes(int n_img, int max_rois);
 int rcnn_post(const float* rois, const float* head, const int32_t* n_rois, int n_img, int max_rois, float img_h,
               float img_w, float inv_sw, float inv_sh, float score_thr, float iou_thr, int max_det, void* ws,
               float* det_boxes, float* det_scores, int32_t* n_det, int32_t* keep_buf, hipStream_t s);
+int det_topk_boxes(const float* dboxes, const float* dscores, const int32_t* dcount, int n_img, int max_det, int k,
+                   float thr, double min_margin, double max_margin, double desired_ar, float* boxes, float* tight,
+                   int32_t* img_of, int32_t* valid, hipStream_t s);
 
 }  // namespace mq

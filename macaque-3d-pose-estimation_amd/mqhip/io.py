@@ -116,6 +116,9 @@ class FrameStore:
                         out-of-scope Swin detector + BoT-SORT produce (step1_proc2d.py:226-252)
       id_preds.json     optional: per stored frame, per row {"pred_label", "pred_score"} of the
                         ResNet-152 ID classifier (step1_proc2d.py:140-163)
+      frame_index.npy   optional int64 (N,): frame i is frames.npy[frame_index[i]] -- synthetic clips
+                        reuse a small pool of rendered images so a 300-frame x 8-view clip at the
+                        cameras' 2048x1536 stays a few hundred MB on disk
     """
 
     def __init__(self, directory):
@@ -133,7 +136,11 @@ class FrameStore:
         if os.path.exists(idp):
             with open(idp) as f:
                 self.id_preds = json.load(f)
-        if not (len(self.frames) == len(self.frame_time) == len(self.frame_number) == len(self.tracks)):
+        fi = os.path.join(directory, "frame_index.npy")
+        self.frame_index = np.load(fi) if os.path.exists(fi) else np.arange(len(self.frames))
+        if len(self.frame_index) and (self.frame_index.min() < 0 or self.frame_index.max() >= len(self.frames)):
+            raise ValueError(f"{directory}: frame_index out of range")
+        if not (len(self.frame_index) == len(self.frame_time) == len(self.frame_number) == len(self.tracks)):
             raise ValueError(f"{directory}: frames, times, numbers and tracks differ in length")
         self._pos = {int(n): i for i, n in enumerate(self.frame_number)}
 
@@ -144,7 +151,7 @@ class FrameStore:
         return self._pos[int(frame_number)]
 
     def image(self, frame_number):
-        return np.asarray(self.frames[self.index_of(frame_number)])
+        return np.asarray(self.frames[self.frame_index[self.index_of(frame_number)]])
 
     def tracks_of(self, frame_number):
         return self.tracks[self.index_of(frame_number)]
@@ -153,8 +160,10 @@ class FrameStore:
         return None if self.id_preds is None else self.id_preds[self.index_of(frame_number)]
 
 
-def write_frame_store(directory, frames, frame_time, frame_number, tracks, camera_id, id_preds=None):
-    """Write a FrameStore directory (used by tests and synthetic runs)."""
+def write_frame_store(directory, frames, frame_time, frame_number, tracks, camera_id, id_preds=None,
+                      frame_index=None):
+    """Write a FrameStore directory (used by tests and synthetic runs).  With ``frame_index`` the
+    ``frames`` are a pool of images and frame i shows ``frames[frame_index[i]]``."""
     import yaml
     os.makedirs(directory, exist_ok=True)
     frames = np.asarray(frames, dtype=np.uint8)
@@ -169,3 +178,5 @@ def write_frame_store(directory, frames, frame_time, frame_number, tracks, camer
     if id_preds is not None:
         with open(os.path.join(directory, "id_preds.json"), "w") as f:
             json.dump(id_preds, f)
+    if frame_index is not None:
+        np.save(os.path.join(directory, "frame_index.npy"), np.asarray(frame_index, dtype=np.int64))

@@ -47,44 +47,61 @@ def n_joints_of(pose_model, default=17):
     return int(meta.get("num_keypoints", default))
 
 
+def _all_gather(buf, world, group=None):
+    import torch.distributed as dist
+    if world == 1:
+        return [buf]
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return parts
+
+
 def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, steps_per_batch=8,
-                      kp_params=None, device=None):
+                      kp_params=None, device=None, id_model=None, tracks=None):
     """BASELINE config 3: the step-1 pose slice of a clip, time steps sharded across ranks.
 
     Every rank walks the same per-camera time grid (``step1_proc2d.plan_jobs``); rank r runs the
-    ViTPose jobs of its contiguous block of time steps (``frame_block``); one all-gather moves
-    every rank's raw keypoints and scores ([steps, C, boxes, J, 3] float64, padded to the largest
-    block and box count) to every rank, which then runs the sequential KP_THR / EMA / alldata
-    post-process over the whole clip -- the EMA is recursive in time per track, so it runs after
-    the gather and the result equals the single-GPU ``process_stores`` exactly.  Returns what
-    ``process_stores`` returns (per camera: rows per kept frame, frame numbers)."""
+    ViTPose jobs (and, with ``id_model``, the ID classification) of its contiguous block of time steps
+    (``frame_block``); one all-gather moves every rank's raw keypoints and scores ([steps, C, boxes, J, 3]
+    float64, padded to the largest block and box count; + [steps, C, boxes, 2] ID label / score) to every
+    rank, which then runs the sequential KP_THR / EMA / alldata post-process over the whole clip -- the EMA
+    is recursive in time per track, so it runs after the gather and the result equals the single-GPU
+    ``process_stores`` exactly.  ``device``: where the gathered buffers live (a CUDA device for RCCL;
+    None = host tensors, gloo).  ``world == 1`` needs no process group.  Returns what ``process_stores``
+    returns (per camera: rows per kept frame, frame numbers)."""
     import numpy as np
-    import torch.distributed as dist
     from src.pipeline import step1_proc2d as s1
     kp_params = s1.KP_PARAMS if kp_params is None else kp_params
-    plans, jobs = s1.plan_jobs(stores, T, kp_params)
+    plans, jobs = s1.plan_jobs(stores, T, kp_params, tracks)
     n_steps, C = len(T), len(stores)
     s0, e0 = frame_block(n_steps, world, rank)
     raw = s1.run_pose(pose_model, stores, jobs, range(s0, e0), steps_per_batch)
+    id_raw = None if id_model is None else s1.run_id(id_model, stores, jobs, range(s0, e0), steps_per_batch)
     # the buffer shape must agree on every rank, also on a rank whose block holds no pose job:
     # take J from the model, never from this rank's results
     J = n_joints_of(pose_model)
     nb = max([len(j[2]) for js in jobs.values() for j in js] or [1])
     block = frame_block(n_steps, world, 0)[1]
-    buf = torch.full((block, C, nb, J, 3), float("nan"), dtype=torch.float64)
+    buf = torch.full((block, C, nb, J * 3 + 2), float("nan"), dtype=torch.float64)
     for (k, c), (kp, sc) in raw.items():
-        buf[k - s0, c, :len(kp), :, :2] = torch.from_numpy(kp)
-        buf[k - s0, c, :len(kp), :, 2] = torch.from_numpy(sc.astype(np.float64))
+        n = len(kp)
+        buf[k - s0, c, :n, :J * 3] = torch.from_numpy(
+            np.concatenate([kp, sc.astype(np.float64)[..., None]], axis=-1).reshape(n, J * 3))
+        if id_raw is not None:
+            buf[k - s0, c, :n, J * 3:] = torch.tensor([[p["pred_label"], p["pred_score"]] for p in id_raw[(k, c)]],
+                                                      dtype=torch.float64)
     if device is not None:
         buf = buf.to(device)
-    parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
-    allraw = {}
+    parts = _all_gather(buf, world, group)
+    allraw, allid = {}, ({} if id_model is not None else None)
     for r in range(world):
         s, e = frame_block(n_steps, world, r)
         part = parts[r].cpu().numpy()
         for k in range(s, e):
             for (c, _, boxes, _, _) in jobs.get(k, []):
                 v = part[k - s, c, :len(boxes)]
-                allraw[(k, c)] = (v[..., :2].copy(), v[..., 2].astype(np.float32))
-    return s1.assemble_rows(stores, T, plans, jobs, allraw, kp_params)
+                kp = v[:, :J * 3].reshape(len(boxes), J, 3)
+                allraw[(k, c)] = (kp[..., :2].copy(), kp[..., 2].astype(np.float32))
+                if allid is not None:
+                    allid[(k, c)] = [{"pred_label": int(lab), "pred_score": float(scr)} for lab, scr in v[:, J * 3:]]
+    return s1.assemble_rows(stores, T, plans, jobs, allraw, kp_params, allid)

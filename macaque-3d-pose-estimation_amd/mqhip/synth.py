@@ -360,3 +360,58 @@ def make_alldata(cams, skel, noise_px=2.0, p_seen=0.9, p_dup=0.1, id_score=0.95,
             rows_cam.append(rows)
         T.append(rows_cam)
     return T
+
+
+# ----------------------------------------------------------------------------- clips on disk
+
+def write_clip(root, data_name="clip", n_frames=300, n_views=8, n_animals=4, pool=4, height=IMG_H, width=IMG_W,
+               fps=24.0, seed=2):
+    """A synchronized multi-view clip on disk in the layout ``run_demo.proc`` reads (BASELINE config 3):
+    per camera a FrameStore ``<root>/videos/<data_name>.<cam>`` (frames of ``pool`` rendered images reused
+    through ``frame_index``, tracker rows = the tight boxes of the projected skeletons with track id =
+    individual), ``<root>/results3D/<data_name>/calibration.toml`` and ``<root>/calib/config.yaml``.
+    Camera 0's frame times are exactly 1/fps apart and the others jitter by +-2 ms, so step 1's time grid
+    has ``n_frames`` steps.  Returns (cams, raw_dir, results_root, config_path, kp2d truth)."""
+    import os
+
+    import yaml
+
+    from . import io as mqio
+    cams = make_cameras(n_views)
+    skel = make_skeletons(n_animals, n_frames + 1, seed=seed)
+    truth = make_kp2d(cams, skel, noise_px=0.0, drop=0.0, seed=seed + 1)          # (A, F+1, C, J, 3)
+    raw = os.path.join(root, "videos")
+    rng = np.random.default_rng(seed + 2)
+    t0 = 1000.0
+    boxes = [boxes_from_kp2d(truth[:, f].transpose(1, 0, 2, 3)) for f in range(n_frames + 1)]  # (C, A, 4) each
+    for c, cam in enumerate(cams):
+        imgs = np.stack([make_frames(1, truth[:, j, c][None], seed=100 * c + j, height=height, width=width)[0]
+                         for j in range(pool)])
+        tracks = []
+        for f in range(n_frames + 1):
+            b = boxes[f][c]
+            rows = [[float(x1), float(y1), float(x2), float(y2), float(a), 0.95]
+                    for a, (x1, y1, x2, y2) in enumerate(b) if x2 > x1 and y2 > y1]
+            tracks.append(rows)
+        times = t0 + np.arange(n_frames + 1) / fps
+        if c:
+            times = times + rng.uniform(-2e-3, 2e-3, n_frames + 1)
+        mqio.write_frame_store(os.path.join(raw, f"{data_name}.{cam['name']}"), imgs, times,
+                               np.arange(n_frames + 1), tracks, cam["name"], frame_index=np.arange(n_frames + 1) % pool)
+    res = os.path.join(root, "results3D")
+    os.makedirs(os.path.join(res, data_name), exist_ok=True)
+    write_calibration_toml(cams, os.path.join(res, data_name, "calibration.toml"))
+    os.makedirs(os.path.join(root, "calib"), exist_ok=True)
+    cfg = os.path.join(root, "calib", "config.yaml")
+    with open(cfg, "w") as f:
+        yaml.safe_dump({"camera_id": [int(c["name"]) for c in cams]}, f)
+    return cams, raw, res, cfg, truth[:, :n_frames]
+
+
+def confident_head(weights, gain=20.0, shift=0.5):
+    """Random ViTPose weights with the 1x1 head scaled and shifted so that heatmap peaks score above
+    step 1's KP_THR / step 4's score threshold (seeded random weights otherwise give scores near 0 and
+    an empty 3D stage).  In place; returns ``weights``."""
+    weights["head.final_layer.weight"] = weights["head.final_layer.weight"] * gain
+    weights["head.final_layer.bias"] = weights["head.final_layer.bias"] + shift
+    return weights

@@ -6,28 +6,91 @@ and imports the Cython ``pictorial`` module (run_demo.py:3-11) that no step call
 
 This build runs the same chain on MI355X with the parts outside its scope replaced by data:
 
-* step 1 (``src.pipeline.step1_proc2d.proc``): the pose slice over every camera's frame store;
-  the detector / tracker / ID classifier output arrives as the stores' tracker rows;
+* step 1 (``src.pipeline.step1_proc2d.proc``): the pose slice over every camera's frame store
+  and the ID classifier of each camera's variant; the detector / tracker output arrives as the
+  stores' tracker rows;
 * steps 2-3: association is bypassed -- ``kp2d.pickle`` is written by step 3's own
   ``create_kp2dfile`` from a known track -> individual map
   (``src.pipeline.step3_crossframematching.proc_known_assignment``);
 * step 4 (``src.pipeline.step4_aniposefiltering.proc``): unchanged drop-in;
 * visualisation (video rendering) is out of scope and the ``pictorial`` import is not needed.
+
+Multi-GPU (BASELINE config 3): run one process per GPU under ``torch.distributed.run``; every rank
+calls ``proc(..., world=W, rank=r, group=g)``.  Step 1's time steps are sharded over the ranks with
+one all-gather of the 2D keypoints (RCCL over xGMI), and rank 0 runs steps 3-4 on the gathered clip
+(``step4`` couples all frames of an animal, so it is not sharded).  The files and kp3d equal the
+single-process run bit for bit (tests/test_gpu_config3.py).
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29500 \\
+        run_demo.py --data example --raw ./videos --results ./results3D --config ./calib/config.yaml
 """
+import argparse
+import os
+
 from src.pipeline import step1_proc2d as step1
 from src.pipeline import step3_crossframematching as step3
 from src.pipeline import step4_aniposefiltering as step4
 
 
 def proc(data_name, fps, results_dir_root, device_str, config_path, raw_data_dir, n_kp, vidfile_prefix='',
-         n_animal=4, track_to_animal=None, pose_model=None):
-    """run_demo.py:21-30: step 1 -> (known assignment) -> step 4; returns step 4's kp3d dict."""
+         n_animal=4, track_to_animal=None, pose_model=None, id_model="auto", world=1, rank=0, group=None,
+         sharded=False, gather_device=None, timings=None):
+    """run_demo.py:21-30: step 1 -> (known assignment) -> step 4; returns step 4's kp3d dict (on rank 0;
+    None on the other ranks of a sharded run).  ``timings``: optional dict filled with wall seconds per
+    stage."""
+    import time
     device = int(device_str.split(':')[1]) if ':' in device_str else 0
-    step1.proc(data_name, results_dir_root, raw_data_dir, device_str, fps, pose_model=pose_model)
+    t0 = time.perf_counter()
+    step1.proc(data_name, results_dir_root, raw_data_dir, device_str, fps, pose_model=pose_model, id_model=id_model,
+               world=world, rank=rank, group=group, sharded=sharded, gather_device=gather_device)
+    t1 = time.perf_counter()
+    if rank != 0:
+        return None
     step3.proc_known_assignment(data_name, results_dir_root, config_path, n_animal=n_animal, n_kp=n_kp,
                                 track_to_animal=track_to_animal)
-    return step4.proc(data_name, results_dir_root, config_path, n_kp, redo=True, device=device)
+    t2 = time.perf_counter()
+    out = step4.proc(data_name, results_dir_root, config_path, n_kp, redo=True, device=device)
+    t3 = time.perf_counter()
+    if timings is not None:
+        timings.update(step1_s=t1 - t0, step3_s=t2 - t1, step4_s=t3 - t2)
+    return out
+
+
+def _dist_from_env(backend=None):
+    """torch.distributed.run environment -> (world, rank, local_rank, group, gather_device).  Backend
+    "nccl" (RCCL over xGMI, one GPU per rank) unless MQ_DIST_BACKEND=gloo (host tensors: a rehearsal
+    of several ranks on one GPU, MQ_SHARE_GPU=1)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = backend or os.environ.get("MQ_DIST_BACKEND", "nccl")
+    if os.environ.get("MQ_SHARE_GPU") == "1":
+        local = local % torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    if world == 1:
+        return 1, 0, local, None, None
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return world, rank, local, None, torch.device("cuda", local)
+    dist.init_process_group(backend)
+    return world, rank, local, None, None
 
 
 if __name__ == '__main__':
-    proc('example', 24, './results3D', 'cuda:0', './calib/config.yaml', './videos', 17)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--data", default="example")
+    ap.add_argument("--fps", type=float, default=24)
+    ap.add_argument("--results", default="./results3D")
+    ap.add_argument("--config", default="./calib/config.yaml")
+    ap.add_argument("--raw", default="./videos")
+    ap.add_argument("--n-kp", type=int, default=17)
+    a = ap.parse_args()
+    W, R, L, G, dev = _dist_from_env()
+    proc(a.data, a.fps, a.results, f"cuda:{L}", a.config, a.raw, a.n_kp, world=W, rank=R, group=G,
+         gather_device=dev)
+    if W > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()

@@ -479,11 +479,17 @@ def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8
 
 
 def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None, redo=False, pose_model=None,
-                        device_str="cuda:0", steps_per_batch=8, id_model=None, detector=None):
+                        device_str="cuda:0", steps_per_batch=8, id_model=None, detector=None, world=1, rank=0,
+                        group=None, sharded=False, gather_device=None):
     """step1_proc2d.py:389-447 with the frame stores of ``mqhip.io.FrameStore`` and the tracker
     rows they carry (or, with ``detector``, the detector -> tracker chain).  ``id_model``: see
     ``resolve_id_models`` ("auto" = the reference's per-camera variant).  Writes
-    <results_root>/<data_name>/<cam>/alldata.json and frame_num.npy."""
+    <results_root>/<data_name>/<cam>/alldata.json and frame_num.npy.
+
+    Multi-GPU (BASELINE config 3; ``world`` > 1, or ``sharded`` at world 1): every rank calls this with
+    its ``rank``; the clip's time steps are sharded over the ranks (``mqhip.shard.pose_clip_sharded``:
+    one all-gather of the raw keypoints over ``group``, buffers on ``gather_device`` -- the rank's GPU for
+    RCCL, None for gloo) and rank 0 writes the files, which equal the single-process ones bit for bit."""
     import glob
     from mqhip.io import FrameStore
     meta_paths = sorted(glob.glob(os.path.join(raw_root, f"{data_name}.*", "metadata.yaml")))
@@ -510,7 +516,14 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
     sel = [stores[i] for i in todo]
     tracks = None if detector is None else track_stores(detector, sel, T)
     id_models = resolve_id_models(sel, id_model, device_str)
-    res = process_stores(pose_model, sel, T, steps_per_batch=steps_per_batch, id_model=id_models, tracks=tracks)
+    if world > 1 or sharded:
+        from mqhip.shard import pose_clip_sharded
+        res = pose_clip_sharded(pose_model, sel, T, world, rank, group=group, steps_per_batch=steps_per_batch,
+                                device=gather_device, id_model=id_models, tracks=tracks)
+        if rank != 0:
+            return
+    else:
+        res = process_stores(pose_model, sel, T, steps_per_batch=steps_per_batch, id_model=id_models, tracks=tracks)
     for i, (rows, fn) in zip(todo, res):
         os.makedirs(out_dirs[i], exist_ok=True)
         np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))
@@ -519,11 +532,11 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
 
 
 def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0, pose_model=None, detector=None,
-         id_model="auto"):
+         id_model="auto", **shard):
     """step1.proc (step1_proc2d.py:450) over every camera's frame store: pose and ID on the stores' tracker
     rows, or the full detector -> tracker -> pose -> ID chain with ``detector``.  ``id_model="auto"`` is the
     reference's rule (every camera classified by the ID model of its variant, step1:424-427); None keeps
     the stores' own ID predictions (``resolve_id_models``).  Unlike the reference (which hard-codes cuda:1,
     step1:50,421) the device argument is honoured."""
     step1_proc2d_custom(data_name, results_root, raw_root, fps=fps, pose_model=pose_model, device_str=device_str,
-                        detector=detector, id_model=id_model)
+                        detector=detector, id_model=id_model, **shard)

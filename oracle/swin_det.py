@@ -229,7 +229,7 @@ def swin_block(x, H, W, w, k, heads, ws, shift):
     Hp, Wp = H + pad_b, W + pad_r
     if shift > 0:
         q = torch.roll(q, shifts=(-shift, -shift), dims=(1, 2))
-        mask = shift_mask(Hp, Wp, ws, shift)
+        mask = shift_mask(Hp, Wp, ws, shift).to(q.device)
     else:
         mask = None
     win = window_partition(q, ws).view(-1, ws * ws, C)
@@ -241,7 +241,7 @@ def swin_block(x, H, W, w, k, heads, ws, shift):
     qq = qq * (hd ** -0.5)
     attn = qq @ kk.transpose(-2, -1)
     table = w[k + "attn.w_msa.relative_position_bias_table"]
-    bias = table[relative_position_index(ws).view(-1)].view(N, N, -1).permute(2, 0, 1)
+    bias = table[relative_position_index(ws).view(-1).to(table.device)].view(N, N, -1).permute(2, 0, 1)
     attn = attn + bias[None]
     if mask is not None:
         nW = mask.shape[0]

@@ -179,3 +179,49 @@ def test_topdown_end_to_end_vs_oracle():
     clear = margin > 5e-2
     assert clear.sum() > 0
     np.testing.assert_array_equal(am[clear], ram[clear])
+
+
+def test_vitpose_h_config2_batch_vs_fp32_oracle():
+    """BASELINE config 2 at the bench's own batch: one frame of 8 views at 2048x1536 x 4 individuals =
+    32 crops through ``VitPoseHip.topdown`` (UDP crop -> ViT-H flip test = 64 forwards -> decode), the
+    shapes that route every ViT-H GEMM through the 256x256 ping-pong kernel, the head-major qkv, the
+    64-image attention and the sub-pixel deconv.  All 32 flip-averaged heatmaps vs the fp32 oracle
+    (oracle/vitpose.py, run on the GPU with TF32 off) on the same crops: max|dH| <= 2e-2 max|H| per crop;
+    the decoded argmax equals the oracle's wherever the oracle's top-2 margin exceeds 5e-2 max|H|
+    (model/pose/...macaque.py:54-110, step1_proc2d.py:294-298)."""
+    import torch
+    from mqhip import synth
+    from mqhip.pose import VitPoseHip
+    from mqhip.weights import VIT_H, make_random_weights
+    from oracle.decode import decode_batch
+    from oracle.vitpose import forward_flip_test
+    cams = synth.make_cameras(8)
+    kp2d = synth.make_kp2d(cams, synth.make_skeletons(4, 1, seed=7), noise_px=0.0, drop=0.0)   # (A, 1, C, J, 3)
+    frames = synth.make_frames(8, kp2d[:, 0].transpose(1, 0, 2, 3), seed=8)
+    boxes = synth.expand_boxes(synth.boxes_from_kp2d(kp2d[:, 0].transpose(1, 0, 2, 3)).reshape(-1, 4))
+    fidx = np.repeat(np.arange(8, dtype=np.int32), 4)
+    w = make_random_weights(VIT_H, seed=11, device="cuda")
+    model = VitPoseHip(VIT_H, w, graph=True)
+    fr = torch.from_numpy(frames).cuda()
+    crops, center, scale = model.crop(fr, torch.from_numpy(boxes).cuda(), torch.from_numpy(fidx).cuda())
+    hm = model.forward(crops, flip_test=True)
+    kp, score, am, _ = model.decode(hm, center, scale)
+    kp_t, score_t, am_t = model.topdown(fr, torch.from_numpy(boxes).cuda(), torch.from_numpy(fidx).cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(am, am_t) and torch.equal(score, score_t) and torch.equal(kp, kp_t)
+    with torch.no_grad():
+        torch.backends.cuda.matmul.allow_tf32 = False
+        torch.backends.cudnn.allow_tf32 = False
+        ref, _, _ = forward_flip_test(crops, w, VIT_H)
+    got, ref = hm.float().cpu().numpy(), ref.float().cpu().numpy()
+    assert got.shape == (32, 17, 64, 48)
+    for i in range(32):
+        s = np.abs(ref[i]).max()
+        err = np.abs(got[i] - ref[i]).max()
+        assert err <= HM_TOL * s, f"crop {i}: max|d|={err:.3e} vs {HM_TOL}*{s:.3e}"
+    rkp, rsc, ram = decode_batch(ref, center.cpu().numpy(), scale.cpu().numpy())
+    flat = ref.reshape(32, 17, -1)
+    top2 = np.sort(flat, axis=-1)[..., -2:]
+    clear = (top2[..., 1] - top2[..., 0]) / np.abs(flat).max(axis=-1) > 5e-2
+    assert clear.sum() > 0
+    np.testing.assert_array_equal(am.cpu().numpy()[clear], ram[clear])

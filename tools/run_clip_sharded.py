@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""BASELINE config 3 end to end: a synthetic 300-frame x 8-view x 4-individual clip through
+``run_demo.proc`` -- step 1 (ViTPose-H flip test + ID classifier per camera variant) with the clip's
+time steps sharded over the ranks and one all-gather of the 2D keypoints, then steps 3-4 (Viterbi,
+DLT or RANSAC, optim_points) on rank 0.  One process per GPU:
+
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \\
+        tools/run_clip_sharded.py --root /tmp/clip
+
+Rank 0 writes the clip (frame stores, calibration, config.yaml) when --root does not hold one yet,
+and prints one JSON line with the stage wall times.  MQ_DIST_BACKEND=gloo MQ_SHARE_GPU=1 rehearses
+several ranks on one GPU (keypoints exchanged through host tensors); the default is RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "macaque-3d-pose-estimation_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--root", required=True)
+    ap.add_argument("--data", default="clip")
+    ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--views", type=int, default=8)
+    ap.add_argument("--animals", type=int, default=4)
+    ap.add_argument("--pool", type=int, default=4)
+    ap.add_argument("--model", default="huge", choices=["huge", "base", "tiny"])
+    ap.add_argument("--results", default=None, help="results root (default <root>/results3D)")
+    ap.add_argument("--no-id", action="store_true", help="skip the ID classifier")
+    ap.add_argument("--sharded", action="store_true", help="use the sharded step 1 also at world size 1")
+    a = ap.parse_args()
+
+    import shutil
+
+    import torch
+    import torch.distributed as dist
+
+    import run_demo
+    from mqhip import synth
+    from mqhip.apis import PoseModelHip
+    from mqhip.weights import CONFIGS, make_random_weights
+
+    world, rank, local, group, gdev = run_demo._dist_from_env()
+    cfg_path = os.path.join(a.root, "calib", "config.yaml")
+    if rank == 0 and not os.path.exists(cfg_path):
+        t0 = time.perf_counter()
+        synth.write_clip(a.root, a.data, n_frames=a.frames, n_views=a.views, n_animals=a.animals, pool=a.pool)
+        print(f"[clip] wrote {a.frames} frames x {a.views} views in {time.perf_counter() - t0:.1f} s",
+              file=sys.stderr, flush=True)
+    if world > 1:
+        dist.barrier()
+    res = a.results or os.path.join(a.root, "results3D")
+    if rank == 0 and res != os.path.join(a.root, "results3D"):
+        os.makedirs(os.path.join(res, a.data), exist_ok=True)
+        shutil.copy(os.path.join(a.root, "results3D", a.data, "calibration.toml"), os.path.join(res, a.data))
+    if world > 1:
+        dist.barrier()
+    cfg = CONFIGS[a.model]
+    w = synth.confident_head(make_random_weights(cfg, seed=0, device=torch.device("cuda", local)))
+    pose = PoseModelHip(cfg, w, local)
+    del w
+    id_model = None if a.no_id else "auto"
+    times = {}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_demo.proc(a.data, 24, res, f"cuda:{local}", cfg_path, os.path.join(a.root, "videos"), 17,
+                  n_animal=a.animals, pose_model=pose, id_model=id_model, world=world, rank=rank, group=group,
+                  sharded=a.sharded, gather_device=gdev, timings=times)
+    torch.cuda.synchronize()
+    total = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([total], dtype=torch.float64, device=gdev or "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        total = float(t.item())
+    if rank == 0:
+        print(json.dumps({"config": "BASELINE config 3 (+ step 4 of config 4's path: Viterbi, DLT, optim_points)",
+                          "frames": a.frames, "views": a.views, "individuals": a.animals, "model": a.model,
+                          "world": world, "backend": os.environ.get("MQ_DIST_BACKEND", "nccl") if world > 1 else None,
+                          "id_classifier": not a.no_id, "seconds": {k: round(v, 4) for k, v in times.items()},
+                          "total_s": round(total, 4),
+                          "individuals_frames_per_s": round(a.animals * a.frames / total, 2)}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
