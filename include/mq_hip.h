@@ -34,7 +34,7 @@ extern "C" {
  *   2 -- mq_viterbi_filter accepts n_back in [1, 3] only (was [1, 8]); the timing-ablation tuning keys and
  *        MQ_TUNE_ATTENTION_V2 (key 17, the first-generation attention kernel) were removed and now return -2;
  *        MQ_TUNE_OPTIM_PCG_ITERS defaults to 20 (was 40; optim_points results stay within their tolerance);
- *        mq_det_topk_boxes added (config-5 capturable box selection). */
+ *        mq_det_topk_boxes (config-5 capturable box selection) and mq_optim_prepare (host initialisation) added. */
 #define MQ_ABI_VERSION 2
 
 typedef struct mq_ctx mq_ctx;
@@ -351,6 +351,16 @@ int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int n_animals, int n_frames
  *   tokens % 32 == 0 and <= 192; head_dim = dim / heads in {64, 80}. */
 int mq_attention_bf16(mq_ctx* ctx, const uint16_t* qkv, uint16_t* out, int n_img, int tokens, int dim, int heads,
                       void* stream);
+
+/* optim_points' parameter initialisation on the HOST (no HIP call; host pointers): per animal b of
+ * p3ds (B, F, J, 3) float64 (NaN = missing) -> x0 (B, F*J*3 + n_strong + n_weak) = [p3d with every NaN gap
+ * of a series linearly interpolated over frames (np.interp; an all-NaN series -> 0), median limb lengths
+ * (strong then weak; 0 or > median + 5 MAD -> the median of all)], non-finite -> 0, and scale_smooth_full
+ * (B) = scale_smooth / mean |diff(medfilt7(series))|: bit for bit the numpy arithmetic of cameras.py:
+ * 1116-1150 / 1670-1697 (np.interp, medfilt_data's padding, np.median, np.linalg.norm and np.mean's
+ * summation orders).  constraints: int32 (n_strong + n_weak, 2) joint pairs.  One host thread per animal. */
+int mq_optim_prepare(const double* p3ds, int B, int F, int J, const int32_t* constraints, int n_strong, int n_weak,
+                     double scale_smooth, double* x0, double* scale_smooth_full);
 
 /* CameraGroup.optim_points (cameras.py:1116-1190) and optim_points_jointlenfix (:1192-1415) for
  * B animals at once.  Replaces scipy least_squares(trf, 2-point sparse Jacobian) with

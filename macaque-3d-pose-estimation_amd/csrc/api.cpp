@@ -1174,3 +1174,6 @@ int mq_attention_bf16(mq_ctx* ctx, const uint16_t* qkv, uint16_t* out, int n_img
 }
 
 }  // extern "C"
+
+// error reporting for the host-only translation units (optim_host.cpp)
+int mq_fail_host(const std::string& msg, int code) { return fail(msg, code); }

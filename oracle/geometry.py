@@ -466,6 +466,17 @@ def jac_sparsity_triangulation(p2ds, constraints, constraints_weak, n_deriv_smoo
     return A
 
 
+def optim_init(p3ds, constraints, constraints_weak, scale_smooth):
+    """cameras.py:1146-1150: x0 (interpolated p3d + limb lengths, non-finite -> 0) and scale_smooth_full."""
+    p3ds_intp = np.apply_along_axis(interpolate_data, 0, p3ds)
+    p3ds_med = np.apply_along_axis(medfilt_data, 0, p3ds_intp, size=7)
+    default_smooth = 1.0 / np.mean(np.abs(np.diff(p3ds_med, axis=0)))
+    scale_smooth_full = scale_smooth * default_smooth
+    x0 = initialize_params_triangulation(p3ds_intp, constraints, constraints_weak)
+    x0[~np.isfinite(x0)] = 0
+    return x0, scale_smooth_full
+
+
 def optim_points(cgroup, points, p3ds, constraints=(), constraints_weak=(), scale_smooth=4,
                  scale_length=2, scale_length_weak=0.5, reproj_error_threshold=15,
                  reproj_loss='soft_l1', n_deriv_smooth=1, ftol=1e-3, return_result=False):
@@ -474,12 +485,7 @@ def optim_points(cgroup, points, p3ds, constraints=(), constraints_weak=(), scal
     assert n_cams == len(cgroup.cameras)
     constraints = np.array(constraints)
     constraints_weak = np.array(constraints_weak)
-    p3ds_intp = np.apply_along_axis(interpolate_data, 0, p3ds)
-    p3ds_med = np.apply_along_axis(medfilt_data, 0, p3ds_intp, size=7)
-    default_smooth = 1.0 / np.mean(np.abs(np.diff(p3ds_med, axis=0)))
-    scale_smooth_full = scale_smooth * default_smooth
-    x0 = initialize_params_triangulation(p3ds_intp, constraints, constraints_weak)
-    x0[~np.isfinite(x0)] = 0
+    x0, scale_smooth_full = optim_init(p3ds, constraints, constraints_weak, scale_smooth)
     jac = jac_sparsity_triangulation(points, constraints, constraints_weak, n_deriv_smooth)
     res = optimize.least_squares(
         cgroup._error_fun_triangulation, x0=x0, jac_sparsity=jac, loss='linear', ftol=ftol,

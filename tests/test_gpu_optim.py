@@ -101,13 +101,14 @@ def test_optim_batch_equals_single_and_is_deterministic():
 
 def test_optim_points_jointlenfix_keeps_lengths_and_lowers_cost():
     from mqhip.geometry import CameraGroup
-    from mqhip.optim import optim_points_batch, prepare
+    from mqhip.optim import optim_points_batch, prepare_batch
     cams, o, p2, init, cons, weak, truth = _problem(30)
     g = CameraGroup.from_dicts(cams)
     jl_fixed = np.linspace(60, 300, len(cons) + len(weak))
     p3, jl = g.optim_points_jointlenfix(p2, init, jl_fixed, constraints=cons, constraints_weak=weak, **ARGS)
     np.testing.assert_array_equal(jl, jl_fixed)
-    x0, ssf = prepare(init, cons, weak, ARGS["scale_smooth"])
+    x0, ssf = prepare_batch(init[None], cons, weak, ARGS["scale_smooth"])
+    x0, ssf = x0[0], ssf[0]
     x0[-len(jl_fixed):] = jl_fixed
     c0 = _oracle_cost(o, x0, p2, cons, weak, ssf, ARGS)
     c1 = _oracle_cost(o, np.hstack([p3.ravel(), jl_fixed]), p2, cons, weak, ssf, ARGS)

@@ -5,11 +5,11 @@ import pytest
 
 @pytest.mark.parametrize("F,ties", [(50, False), (300, False), (300, True)])
 def test_optim_prepare_matches_oracle_init(F, ties):
-    """x0 and scale_smooth_full (cameras.py:1125-1150) are bit-identical to the oracle's (the mirror
-    vectorises the median filter and the limb-length medians over all series; ties exercise the
-    order-statistic median)."""
+    """x0 and scale_smooth_full (cameras.py:1125-1150) from libmq_hip's host initialisation
+    (mq_optim_prepare through mqhip.optim.prepare_batch) are bit-identical to the oracle's; ties
+    exercise the order-statistic median."""
     from mqhip import synth
-    from mqhip.optim import prepare
+    from mqhip.optim import prepare_batch
     from oracle.geometry import initialize_params_triangulation, interpolate_data, medfilt_data
     rng = np.random.default_rng(F)
     p3 = synth.make_skeletons(1, F)[0] + rng.normal(0, 3, (F, 17, 3))
@@ -19,7 +19,8 @@ def test_optim_prepare_matches_oracle_init(F, ties):
     p3[:, 4] = np.nan                                 # a joint never triangulated
     cons = synth.constraint_indices(synth.CONSTRAINTS)
     weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
-    x0, ssf = prepare(p3, cons, weak, 3)
+    x0, ssf = prepare_batch(p3[None], cons, weak, 3)
+    x0, ssf = x0[0], ssf[0]
     intp = np.apply_along_axis(interpolate_data, 0, p3)
     med = np.apply_along_axis(medfilt_data, 0, intp, size=7)
     ref_ssf = 3 * (1.0 / np.mean(np.abs(np.diff(med, axis=0))))
