@@ -390,7 +390,7 @@ __global__ __launch_bounds__(B2T, 2) void gemm256_kernel(GemmArgs p, int tiles_m
                           acc[i][j][3] + bias[j].w};
             acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
             if constexpr (EPI == EPI_GELU_BF16) {
-              const f32x2 g0 = gelu_erf2((f32x2){v[0], v[1]}), g1 = gelu_erf2((f32x2){v[2], v[3]});
+              const f32x2 g0 = gelu_sig2((f32x2){v[0], v[1]}), g1 = gelu_sig2((f32x2){v[2], v[3]});
               v[0] = g0.x;
               v[1] = g0.y;
               v[2] = g1.x;

@@ -212,7 +212,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
       v[3] = acc[i][j][3] + bias[j].w;
       acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       if constexpr (EPI == EPI_GELU_BF16) {
-        const f32x2 g0 = gelu_erf2((f32x2){v[0], v[1]}), g1 = gelu_erf2((f32x2){v[2], v[3]});
+        const f32x2 g0 = gelu_sig2((f32x2){v[0], v[1]}), g1 = gelu_sig2((f32x2){v[2], v[3]});
         v[0] = g0.x;
         v[1] = g0.y;
         v[2] = g1.x;
