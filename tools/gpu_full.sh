@@ -16,8 +16,4 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT
 bash tools/gpu_pmc_fc1.sh $OUT/pmc
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/$OUT/proflift -o run -- python3 $GRAFT_REPO_ROOT/tools/bench_lift.py --no-cpu --reps 2 > gpurun_out/$OUT/proflift.json 2> gpurun_out/$OUT/proflift.err || { echo PROF LIFT FAILED; tail -20 gpurun_out/$OUT/proflift.err; exit 1; }
 cat gpurun_out/$OUT/proflift.json
-# BASELINE config 3 end to end on one GPU (world 1 through the sharded path) and as 2 ranks sharing it (gloo)
-timeout -k 10 600 python3 tools/run_clip_sharded.py --root /tmp/mq_clip3 --sharded > gpurun_out/$OUT/clip3_world1.json 2> gpurun_out/$OUT/clip3_world1.err || { echo CLIP3 FAILED; tail -20 gpurun_out/$OUT/clip3_world1.err; exit 1; }
-cat gpurun_out/$OUT/clip3_world1.json
-MQ_DIST_BACKEND=gloo MQ_SHARE_GPU=1 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/run_clip_sharded.py --root /tmp/mq_clip3 --results /tmp/mq_clip3/res2 > gpurun_out/$OUT/clip3_world2_gloo.json 2> gpurun_out/$OUT/clip3_world2_gloo.err || { echo CLIP3 W2 FAILED; tail -20 gpurun_out/$OUT/clip3_world2_gloo.err; exit 1; }
-cat gpurun_out/$OUT/clip3_world2_gloo.json
+# config 3 (the clip driver) runs in its own call: tools/gpu_clip3.sh
