@@ -21,6 +21,7 @@
 // Determinism: every reduction is a fixed-order per-block / per-series sum, so
 // results are bitwise reproducible run to run.
 #include <algorithm>
+#include <cstdio>
 #include <vector>
 
 #include "common.hpp"
@@ -31,10 +32,43 @@ namespace {
 constexpr int OPT_MAXJ = 32;
 constexpr int OPT_MAXL = 64;
 constexpr int OPT_MAXN = 3;
-constexpr int OPT_FS = 9 + 18 * OPT_MAXN;  // doubles per frame record of the factored preconditioner
+constexpr int OPT_FS = 9 + 36 * OPT_MAXN;  // doubles per frame record of the factored preconditioner
+constexpr int OPT_MAXK = 16;               // chunks of a series in the chunked substitutions (one lane quad each)
+
+// Chunks the LDS preconditioner splits a series of F frames into: about sqrt(F), at most 16 (one wave of
+// lane quads), each at least n frames long.  Chunk c is frames [c F / K, (c + 1) F / K).
+__host__ __device__ inline int opt_chunks(int F, int n) {
+  int k = 1;
+  while ((k + 1) * (k + 1) <= F) ++k;
+  k = k < OPT_MAXK ? k : OPT_MAXK;
+  const int kn = F / (n > 0 ? n : 1);
+  k = k < kn ? k : kn;
+  return k > 1 ? k : 1;
+}
 constexpr int OPT_MAXC = 16;
 constexpr int OPT_MAXIT = 128;  // PCG iterations per LM step (upper bound)
 constexpr int OPT_THREADS = 128;
+
+// -DOPT_PROFILE builds (tools only, never the shipped library): wall-clock time per phase of the LDS
+// preconditioner kernel, summed over its blocks and printed by optim_points at the end of a solve.
+#ifdef OPT_PROFILE
+__device__ unsigned long long g_opt_prof[9];
+#define OPT_PROF_BEGIN() \
+  unsigned long long prof_t[9]; \
+  prof_t[0] = wall_clock64()
+#define OPT_PROF(k) prof_t[k] = wall_clock64()
+#define OPT_PROF_END()                                                               \
+  do {                                                                               \
+    if (threadIdx.x == 0) {                                                          \
+      for (int k = 1; k < 9; ++k) atomicAdd(&g_opt_prof[k], prof_t[k] - prof_t[k - 1]); \
+      atomicAdd(&g_opt_prof[0], 1ull);                                               \
+    }                                                                                \
+  } while (0)
+#else
+#define OPT_PROF_BEGIN() (void)0
+#define OPT_PROF(k) (void)0
+#define OPT_PROF_END() (void)0
+#endif
 
 struct OptDims {
   int B, C, F, J, NL, nS, fix, n, loss;
@@ -122,11 +156,14 @@ __device__ __forceinline__ void project_jac(const CamParams& cp, const double* X
   }
 }
 
+constexpr int OPT_RTHREADS = 512;  // the per-animal reductions over frames (one block per animal)
+
+template <int NT = OPT_THREADS>
 __device__ double block_sum(double v, double* red) {
   const int t = threadIdx.x;
   red[t] = v;
   __syncthreads();
-  for (int s = OPT_THREADS / 2; s > 0; s >>= 1) {
+  for (int s = NT / 2; s > 0; s >>= 1) {
     if (t < s) red[t] += red[t + s];
     __syncthreads();
   }
@@ -251,7 +288,7 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_eval_kernel(OptDims D, OptB
 // (f = c, c + OPT_RCH, ...) per length, each an unrolled run of independent loads, then the chunk
 // partials in a fixed order -- deterministic, and latency-bound on ~F / OPT_RCH / 8 round trips
 // instead of F.  qLf: [F][NL] (qL partials); lenJ: [F][NL][5] (gradient l[4] l[3], diagonal l[3]^2).
-constexpr int OPT_RCH = OPT_THREADS / 32;
+constexpr int OPT_RCH = OPT_RTHREADS / 32;
 __device__ __forceinline__ void len_partials(const OptDims& D, const double* __restrict__ qLf,
                                              const double* __restrict__ lenJ, double (*pa)[OPT_MAXL],
                                              double (*pb)[OPT_MAXL], int t) {
@@ -281,12 +318,12 @@ __device__ __forceinline__ double len_combine(const double (*p)[OPT_MAXL], int l
 }
 
 // cost[b] = sum_f costF (fixed order); mode 0 also reduces the length-variable gradient and diagonal.
-__global__ void __launch_bounds__(OPT_THREADS) optim_reduce_kernel(OptDims D, OptBufs Bf, double* cost_out, int mode) {
+__global__ void __launch_bounds__(OPT_RTHREADS) optim_reduce_kernel(OptDims D, OptBufs Bf, double* cost_out, int mode) {
   const int b = blockIdx.x, t = threadIdx.x;
-  __shared__ double red[OPT_THREADS];
+  __shared__ double red[OPT_RTHREADS];
   double s = 0;
-  for (int f = t; f < D.F; f += OPT_THREADS) s += Bf.costF[(size_t)b * D.F + f];
-  const double tot = block_sum(s, red);
+  for (int f = t; f < D.F; f += OPT_RTHREADS) s += Bf.costF[(size_t)b * D.F + f];
+  const double tot = block_sum<OPT_RTHREADS>(s, red);
   if (t == 0) cost_out[b] = 0.5 * tot;  // scipy's cost convention
   if (mode == 0 && !D.fix) {
     __shared__ double pg[OPT_RCH][OPT_MAXL], pe[OPT_RCH][OPT_MAXL];
@@ -306,6 +343,10 @@ __device__ __forceinline__ double damp_of(double dg) { return fmax(dg, 1e-12); }
 //   [0 .. 8]                      I_f = inv(L_ff) (lower)
 //   [9 + 9(d-1) ..]   d = 1..n    M_{f,d} = I_f L_{f,f-d}          (zero for f - d < 0)
 //   [9 + 9n + 9(d-1)..] d = 1..n  N_{f,d} = I_f^T L_{f+d,f}^T      (zero for f + d >= F)
+//   [9 + 18n + 9(k-1)..] k = 1..n G_{f,k}: forward response of frame f to its chunk's incoming y_{a-k}
+//   [9 + 27n + 9(k-1)..] k = 1..n H_{f,k}: backward response of frame f to the incoming z_{e+k-1}
+// (chunks [a, e) as opt_chunks; G / H are written by the LDS factor kernel only, for the chunked
+// substitutions of optim_precond_lds_kernel)
 // so that L y = r is y_f = I_f r_f - sum_d M_{f,d} y_{f-d} and L^T z = y is
 // z_f = I_f^T y_f - sum_d N_{f,d} z_{f+d}: the I_f r_f / I_f^T y_f products leave the sequential
 // recurrence and run frame-parallel.  The factor recurrence is latency-bound: the last NN frames'
@@ -346,6 +387,14 @@ __device__ __forceinline__ void assemble_block(const OptDims& D, const OptBufs& 
   A[0][0] += sd + lam * damp_of(dg[0]);
   A[1][1] += sd + lam * damp_of(dg[1]);
   A[2][2] += sd + lam * damp_of(dg[2]);
+}
+
+// 1/sqrt(x) for normal positive x: the hardware estimate refined by one Newton step (the factor only
+// preconditions the solve, so it needs accuracy, not IEEE rounding)
+__device__ __forceinline__ double rsq_f64(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  const double e = fma(-0.5 * x * y, y, 0.5);
+  return fma(y, e, y);
 }
 
 // One step of the block-banded Cholesky recurrence: from frame f's diagonal block A and the last
@@ -396,12 +445,14 @@ __device__ __forceinline__ void factor_frame(const OptDims& D, double s2, int f,
       for (int c = 0; c < 3; ++c)
         A[r][c] -= Lf[3 * r] * Lf[3 * c] + Lf[3 * r + 1] * Lf[3 * c + 1] + Lf[3 * r + 2] * Lf[3 * c + 2];
   }
-  const double l00 = sqrt(fmax(A[0][0], 1e-300));
-  const double l10 = A[1][0] / l00, l20 = A[2][0] / l00;
-  const double l11 = sqrt(fmax(A[1][1] - l10 * l10, 1e-300));
-  const double l21 = (A[2][1] - l20 * l10) / l11;
-  const double l22 = sqrt(fmax(A[2][2] - l20 * l20 - l21 * l21, 1e-300));
-  const double i00 = 1 / l00, i11 = 1 / l11, i22 = 1 / l22;
+  // 3x3 Cholesky by reciprocal square roots: the recurrence's latency chain is three v_rsq_f64 (+ one
+  // Newton step each) instead of three IEEE square roots and five IEEE divisions.  Only inv(L_ff) and
+  // the off-diagonal blocks are kept, so L_ff's own diagonal is never formed.
+  const double i00 = rsq_f64(fmax(A[0][0], 1e-300));
+  const double l10 = A[1][0] * i00, l20 = A[2][0] * i00;
+  const double i11 = rsq_f64(fmax(A[1][1] - l10 * l10, 1e-300));
+  const double l21 = (A[2][1] - l20 * l10) * i11;
+  const double i22 = rsq_f64(fmax(A[2][2] - l20 * l20 - l21 * l21, 1e-300));
   const double i10 = -l10 * i00 * i11;
   const double i21 = -l21 * i11 * i22;
   const double i20 = -(l20 * i00 + l21 * i10) * i22;
@@ -495,8 +546,11 @@ __global__ void __launch_bounds__(256) optim_factor_lds_kernel(OptDims D, OptBuf
   const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   const int F = D.F, J = D.J;
   const double lam = Bf.ctl[2 * b];
-  if (j == J) {
-    if (t == 0) length_pinv(D, Bf, b, lam);
+  if (j == J) {  // the length variables' diagonal, one thread per length
+    if (!D.fix && t < D.NL) {
+      const double E = Bf.diag[(size_t)b * D.NV + D.NX + t];
+      Bf.pinvL[(size_t)b * OPT_MAXL + t] = 1.0 / (E + lam * damp_of(E) + 1e-300);
+    }
     return;
   }
   constexpr int RS = 9 + 9 * NN;  // record doubles: inv(L_ff), L_{f,f-1..n}
@@ -559,15 +613,73 @@ __global__ void __launch_bounds__(256) optim_factor_lds_kernel(OptDims D, OptBuf
       }
     }
   }
+  // Chunk responses for the chunked substitutions: thread per (direction, chunk, incoming column).
+  // Forward, chunk c >= 1 over [a, e): the column (k, comp) is the solution over the chunk of
+  // g_f = -sum_d M_{f,d} X_{f-d} with X = unit vector comp at frame a - k, zero at the other incoming
+  // frames, g inside the chunk.  Backward, chunk c <= K - 2: h_f = -sum_d N_{f,d} X_{f+d} from a unit
+  // vector at frame e + k - 1.  M / N are re-formed from the LDS factor (premul_M / premul_N, the same
+  // arithmetic as the records above).
+  const int K = opt_chunks(F, NN);
+  constexpr int NC = 3 * NN;
+  const int per_dir = (K - 1) * NC;
+  for (int tt = t; tt < 2 * per_dir; tt += 256) {
+    const bool back = tt >= per_dir;
+    const int u = back ? tt - per_dir : tt;
+    const int c = back ? u / NC : 1 + u / NC;  // forward chunks 1 .. K-1, backward 0 .. K-2
+    const int col = u % NC, k = col / 3 + 1, comp = col % 3;
+    const int a = c * F / K, e = (c + 1) * F / K;
+    double X[NN][3];  // X[d-1]: the value d frames back (forward) / ahead (backward)
+#pragma unroll
+    for (int d = 0; d < NN; ++d)
+#pragma unroll
+      for (int r = 0; r < 3; ++r) X[d][r] = (d == k - 1 && r == comp) ? 1.0 : 0.0;
+    // forward: X[d-1] at frame a is frame a - d, so the unit sits at d = k; backward: X[d-1] at frame
+    // e - 1 is frame e - 1 + d, unit at d = k -- the same initial pattern
+    const int len = e - a;
+    for (int s2 = 0; s2 < len; ++s2) {
+      const int f = back ? e - 1 - s2 : a + s2;
+      const double* rec = sRec + (size_t)f * RS;
+      double gv[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+      for (int d = NN; d >= 1; --d) {
+        double Mb[9];
+        if (!back) {
+          premul_M(rec, rec + 9 * d, Mb);
+        } else if (f + d < F) {
+          premul_N(rec, sRec + (size_t)(f + d) * RS + 9 * d, Mb);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 9; ++i) Mb[i] = 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) gv[r] = gv[r] - Mb[3 * r] * X[d - 1][0] - Mb[3 * r + 1] * X[d - 1][1] - Mb[3 * r + 2] * X[d - 1][2];
+      }
+      double* o = fb + (size_t)f * OPT_FS + 9 + (back ? 27 : 18) * NN + 9 * (k - 1);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) o[3 * r + comp] = gv[r];
+#pragma unroll
+      for (int d = NN - 1; d >= 1; --d)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) X[d][r] = X[d - 1][r];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) X[0][r] = gv[r];
+    }
+  }
 }
 
 size_t optim_factor_lds_bytes(int F, int NN) { return (size_t)F * (15 + 9 * NN) * sizeof(double); }
 
+// Sum over the J + 1 series of the r.z partials of PCG iteration it, by the whole wave: lane l loads
+// partial l (one load per lane, a single round trip) and an xor butterfly adds them, so every lane
+// of every wave that asks ends with the same bits (each step adds the same two values, commuted).
+// Every lane of the calling wave must be active.
 __device__ __forceinline__ double rz_at(const OptDims& D, const OptBufs& Bf, int b, int it) {
+  const int lane = threadIdx.x & 63;
   const double* p = Bf.rzJ + ((size_t)b * (OPT_MAXIT + 1) + it) * (D.J + 1);
-  double s = 0;
-  for (int j = 0; j <= D.J; ++j) s += p[j];
-  return s;
+  double v = lane <= D.J ? p[lane] : 0.0;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
 }
 
 __device__ __forceinline__ bool pcg_done(const OptDims& D, const OptBufs& Bf, int b, int it) {
@@ -718,15 +830,15 @@ __device__ double solve_series(const OptDims& D, const OptBufs& Bf, int b, int j
 __global__ void __launch_bounds__(64) optim_precond_kernel(OptDims D, OptBufs Bf, int it) {
   const int b = blockIdx.x, j = threadIdx.x;
   const int J = D.J;
-  if (j > J) return;
   double alpha = 0;
   const double* P = (it & 1) ? Bf.P1 : Bf.P0;
-  if (it >= 0) {
+  if (it >= 0) {  // (the whole wave: rz_at)
     if (pcg_done(D, Bf, b, it)) return;
     const double pq = Bf.pq[(size_t)b * (OPT_MAXIT + 1) + it];
     if (!(pq > 0)) return;
     alpha = rz_at(D, Bf, b, it) / pq;
   }
+  if (j > J) return;
   const size_t base = (size_t)b * D.NV;
   double rz = 0;
   if (j == J) {
@@ -765,26 +877,51 @@ __device__ __forceinline__ double quad_bcast(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// w -= a . v and p -= b . v as two fma chains, interleaved in issue order (the scheduler otherwise
+// emits one chain after the other, and in-order issue then puts both on the latency path)
+__device__ __forceinline__ void fma3_pair(double& w, double& p, const double (&a)[3], const double (&b)[3],
+                                          const double (&v)[3]) {
+  asm("v_fma_f64 %0, -%2, %8, %0\n\t"
+      "v_fma_f64 %1, -%5, %8, %1\n\t"
+      "v_fma_f64 %0, -%3, %9, %0\n\t"
+      "v_fma_f64 %1, -%6, %9, %1\n\t"
+      "v_fma_f64 %0, -%4, %10, %0\n\t"
+      "v_fma_f64 %1, -%7, %10, %1"
+      : "+v"(w), "+v"(p)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(b[0]), "v"(b[1]), "v"(b[2]), "v"(v[0]), "v"(v[1]), "v"(v[2]));
+}
+
 // One sequential substitution over the series, run by lanes 0..3: lane q = 0, 1, 2 owns row q of
-// the 3-vector (lane 3 repeats row 2), so a step is 3n fused products per lane and the new
-// vector reaches every lane by three DPP broadcasts.  Forward (BACK false):
-// out_f = in_f - sum_d A[f][d] out_{f-d}; backward: out_f = in_f - sum_d A[f][n + d] out_{f+d},
-// with A[f] the 18n M / N doubles of frame f.  The nearest frame's term is summed last.
+// the 3-vector (lane 3 repeats row 2), and the new vector reaches every lane by three DPP
+// broadcasts.  Forward (BACK false): out_f = in_f - sum_d A[f][d] out_{f-d}; backward:
+// out_f = in_f - sum_d A[f][n + d] out_{f+d}, with A[f] the 18n M / N doubles of frame f.  The
+// terms are summed farthest frame first, and only the nearest frame's three products wait on the
+// previous step: the far terms of step s + 1 (in_{s+1} - sum_{d >= 2} ...) are formed during step s,
+// off the latency chain.  Operands are read from LDS two steps ahead (three register sets).
+//
+// Chunked form: the quad solves frames [f0, f0 + len) with zero incoming vectors; every quad of the
+// wave runs the same trip count L >= len (chunk lengths differ by one), and the steps past len write a
+// pad slot out[3 * pad + i] instead of a frame.
 template <int NN, bool BACK>
 __device__ __forceinline__ void lane_substitution(const double* __restrict__ smn, const double* __restrict__ in,
-                                                  double* __restrict__ out, int F, int t) {
+                                                  double* __restrict__ out, int f0, int len, int L, int pad,
+                                                  int t) {
 #pragma clang fp contract(fast)
   const int q = t & 3, i = q < 3 ? q : 2;
+  const int F = L;
   double V[NN][3];
 #pragma unroll
   for (int k = 0; k < NN; ++k) V[k][0] = V[k][1] = V[k][2] = 0.0;
-  // step s's 3n + 1 operands are read from LDS one step ahead (two register sets, no copies)
   struct Ops {
     double a[NN][3];
     double in;
   };
+  auto frame = [&](int s) {
+    const int sc = min(s, len - 1);
+    return BACK ? f0 + len - 1 - sc : f0 + sc;
+  };
   auto load = [&](int s, Ops& o) {
-    const int f = BACK ? F - 1 - s : s;
+    const int f = frame(s);
     const double* A = smn + (size_t)f * (18 * NN) + (BACK ? 9 * NN : 0) + 3 * i;
 #pragma unroll
     for (int d = 0; d < NN; ++d) {
@@ -795,12 +932,32 @@ __device__ __forceinline__ void lane_substitution(const double* __restrict__ smn
     o.in = in[3 * f + i];
     __builtin_amdgcn_sched_barrier(0);  // keep the look-ahead loads ahead of the step they overlap
   };
-  auto step = [&](int s, const Ops& o) {
-    const int f = BACK ? F - 1 - s : s;
-    double w = o.in;
+  // in - sum_{d = NN .. 2} a[d-1] . W[d-1-shift] (farthest first): the far terms of a step; shift 1
+  // when formed one step early (step s + 1's V[d-1] is step s's V[d-2]).  dmin = 3 leaves out the
+  // d = 2 terms (formed by fma3_pair below).
+  auto far = [&](const Ops& o, int shift, int dmin) {
+    double p = o.in;
 #pragma unroll
-    for (int d = NN; d >= 1; --d) w = w - o.a[d - 1][0] * V[d - 1][0] - o.a[d - 1][1] * V[d - 1][1] - o.a[d - 1][2] * V[d - 1][2];
-    out[3 * f + i] = w;  // lanes 2 and 3 store the same value
+    for (int d = NN; d >= dmin; --d)
+      p = p - o.a[d - 1][0] * V[d - 1 - shift][0] - o.a[d - 1][1] * V[d - 1 - shift][1] -
+          o.a[d - 1][2] * V[d - 1 - shift][2];
+    return p;
+  };
+  double part;
+  auto step = [&](int s, const Ops& cur, const Ops& nxt) {
+    const int f = s < len ? frame(s) : pad;
+    double w = part;
+    if constexpr (NN >= 2) {
+      // this step's nearest-frame terms and step s + 1's d = 2 terms, both on V[0], as two
+      // interleaved fma chains: the far chain fills the latency of the critical one (same operation
+      // order as the plain expression, so the same rounding)
+      part = far(nxt, 1, 3);
+      fma3_pair(w, part, cur.a[0], nxt.a[1], V[0]);
+    } else {
+      w = w - cur.a[0][0] * V[0][0] - cur.a[0][1] * V[0][1] - cur.a[0][2] * V[0][2];
+      part = nxt.in;
+    }
+    out[3 * f + i] = w;     // lanes 2 and 3 store the same value
 #pragma unroll
     for (int k = NN - 1; k >= 1; --k) {
       V[k][0] = V[k - 1][0];
@@ -812,114 +969,275 @@ __device__ __forceinline__ void lane_substitution(const double* __restrict__ smn
     V[0][2] = quad_bcast<2>(w);
   };
   // the look-ahead loads are unconditional (clamped to the last step) so that the LDS counter
-  // wait before a step covers only that step's operands
-  Ops ra, rb;
+  // wait before a step covers only the operands it uses
+  Ops ra, rb, rc;
   load(0, ra);
-  for (int s = 0; s < F; s += 2) {
-    load(min(s + 1, F - 1), rb);
-    step(s, ra);
-    if (s + 1 >= F) break;
-    load(min(s + 2, F - 1), ra);
-    step(s + 1, rb);
+  load(min(1, F - 1), rb);
+  part = far(ra, 0, 2);
+  // whole rounds of three steps without exits (an exit between the steps would let the compiler sink
+  // the far terms behind the next step's latency chain), then the 0 - 2 remaining steps
+  const int F3 = F - F % 3;
+  int s = 0;
+  for (; s < F3; s += 3) {
+    load(min(s + 2, F - 1), rc);
+    step(s, ra, rb);
+    load(min(s + 3, F - 1), ra);
+    step(s + 1, rb, rc);
+    load(min(s + 4, F - 1), rb);
+    step(s + 2, rc, ra);
+  }
+  if (s < F) {
+    load(min(s + 2, F - 1), rc);
+    step(s, ra, rb);
+    if (s + 1 < F) step(s + 1, rb, rc);
   }
 }
 
 // The same preconditioner step with the series staged in LDS: one 256-thread block per (joint
-// series, animal).  Only the two recurrences are sequential; everything else is frame-parallel.
-//   1. all threads: r_f = r_f - alpha q_f, d_f += alpha p_f, u_f = I_f r_f; stage M / N blocks;
-//   2. lanes 0..3:  y_f = u_f - sum_d M_{f,d} y_{f-d}            (forward, f = 0 .. F-1)
-//   3. all threads: v_f = I_f^T y_f
-//   4. lanes 0..3:  z_f = v_f - sum_d N_{f,d} z_{f+d}            (backward, f = F-1 .. 0)
-//   5. all threads: write r, z; block-reduce r.z.
-// Each sequential step is 3n fused products per lane on LDS operands (lane_substitution).  Run from global memory the same
-// recurrence waits on loads left in another XCD's L2.  LDS: optim_precond_lds_bytes.
+// series, animal).  The two substitutions are split into K chunks (opt_chunks, ~sqrt(F)) solved at
+// once, one lane quad each, and stitched together through the chunk responses G / H of the factor
+// record, so the sequential depth is ~F / K + K steps instead of F:
+//   1. all threads: r_f = r_f - alpha q_f, d_f += alpha p_f, u_f = I_f r_f; stage M / N blocks and the
+//      chunk-boundary G / H blocks;
+//   2. quad c:      y^_f = u_f - sum_d M_{f,d} y^_{f-d} over chunk c, zero incoming  (forward)
+//   3. lanes < 3n:  the true last n vectors of each chunk, chunk by chunk:
+//                   S_c[k] = y_{a_c - k} = y^_{a_c - k} + sum_j G_{a_c - k, j} S_{c-1}[j]
+//   4. all threads: y_f = y^_f + sum_k G_{f,k} S_c[k];  v_f = I_f^T y_f
+//   5-7.            the same backward (N, H, chunks from the last), z_f = z^_f + sum_k H_{f,k} T_c[k]
+//   8. all threads: write r, z; block-reduce r.z.
+// A sequential step is 3n fused products per lane on LDS operands (lane_substitution).  Run from
+// global memory the same recurrence waits on loads left in another XCD's L2.  LDS:
+// optim_precond_lds_bytes.
 template <int NN>
 __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBufs Bf, int it) {
   const int j = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   const int F = D.F, J = D.J, J3 = 3 * J;
-  double alpha = 0;
   const double* P = (it & 1) ? Bf.P1 : Bf.P0;
-  if (it >= 0) {
+  double alpha = 0;
+  if (it >= 0) {  // every wave (rz_at is a wave reduction)
     if (pcg_done(D, Bf, b, it)) return;
     const double pq = Bf.pq[(size_t)b * (OPT_MAXIT + 1) + it];
     if (!(pq > 0)) return;
     alpha = rz_at(D, Bf, b, it) / pq;
   }
   const size_t base = (size_t)b * D.NV;
-  if (j == J) {  // the length variables: diagonal preconditioner (as optim_precond_kernel)
-    if (t != 0) return;
-    double rz = 0;
-    if (!D.fix)
-      for (int k = 0; k < D.NL; ++k) {
-        const size_t o = base + D.NX + k;
-        double r;
-        if (it < 0) {
-          Bf.d[o] = 0;
-          r = -Bf.g[o];
-        } else {
-          Bf.d[o] += alpha * P[o];
-          r = Bf.r[o] - alpha * Bf.q[o];
-        }
-        Bf.r[o] = r;
-        const double z = r * Bf.pinvL[(size_t)b * OPT_MAXL + k];
-        Bf.z[o] = z;
-        rz += r * z;
+  if (j == J) {  // the length variables: diagonal preconditioner, one thread per length
+    __shared__ double srz[OPT_MAXL];
+    const int NLa = D.fix ? 0 : D.NL;
+    if (t < NLa) {
+      const size_t o = base + D.NX + t;
+      double r;
+      if (it < 0) {
+        Bf.d[o] = 0;
+        r = -Bf.g[o];
+      } else {
+        Bf.d[o] += alpha * P[o];
+        r = Bf.r[o] - alpha * Bf.q[o];
       }
-    Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
+      Bf.r[o] = r;
+      const double z = r * Bf.pinvL[(size_t)b * OPT_MAXL + t];
+      Bf.z[o] = z;
+      srz[t] = r * z;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double rz = 0;
+      for (int k = 0; k < NLa; ++k) rz += srz[k];  // length order, as before
+      Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = rz;
+    }
     return;
   }
+  OPT_PROF_BEGIN();
   constexpr int MN = 18 * NN;  // M and N doubles per frame
+  constexpr int GB = 9 * NN;   // G (or H) doubles per frame
+  const int K = opt_chunks(F, NN);
+  const int L = (F + K - 1) / K;  // longest chunk
   extern __shared__ double lds_opt[];
-  double* smn = lds_opt;                // [F][MN]
-  double* sr = smn + (size_t)F * MN;    // [F][3] r
-  double* su = sr + (size_t)F * 3;      // [F][3] u, then v
-  double* sz = su + (size_t)F * 3;      // [F][3] y, then z
+  double* smn = lds_opt;                  // [F][MN]
+  double* sr = smn + (size_t)F * MN;      // [F][3] r
+  double* su = sr + (size_t)F * 3;        // [F + 1][3] u, then v (+ pad frame)
+  double* sz = su + (size_t)(F + 1) * 3;  // [F + 1][3] y^, then z^ / z (+ pad frame)
+  double* sPhi = sz + (size_t)(F + 1) * 3;  // [K][NN][GB] G at each chunk's last NN frames (of chunk c-1)
+  double* sPsi = sPhi + (size_t)K * NN * GB;  // [K][NN][GB] H at the first NN frames of chunk c+1
+  double* sS = sPsi + (size_t)K * NN * GB;    // [K][NN][3] true incoming vectors, forward
+  double* sT = sS + (size_t)K * NN * 3;       // [K][NN][3] backward
   const double* __restrict__ fb = Bf.fac + ((size_t)b * J + j) * F * OPT_FS;
-  for (int idx = t; idx < F * MN; idx += 256) {
-    const int f = idx / MN, e = idx - f * MN;
-    smn[idx] = fb[(size_t)f * OPT_FS + 9 + e];
-  }
-  for (int f = t; f < F; f += 256) {
-    const size_t o = base + (size_t)f * J3 + 3 * j;
-    double rr[3];
+  // Stage M / N and the chunk-boundary G / H blocks into LDS and update r / d for this series.  The
+  // loads of all three are issued before any of their stores (one round trip to memory instead of one
+  // per loop iteration: each trip is ~2 us when the factor was written on another XCD).
+  {
+    constexpr int U = 48;                                       // M / N loads per thread and pass
+    constexpr int UG = (2 * OPT_MAXK * NN * GB + 255) / 256;    // G / H loads per thread
+    const double* __restrict__ gg = Bf.g;
+    const double* __restrict__ rin = Bf.r;
+    const double* __restrict__ qq = Bf.q;
+    const double* __restrict__ pp = P;
+    double* __restrict__ dd = Bf.d;
+    // r / d inputs of frames t and t + 256 (F <= 512 on this path: the LDS image caps F near 450)
+    double Iv[2][9], a0v[2][3], a1v[2][3], a2v[2][3], a3v[2][3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      if (it < 0) {
-        Bf.d[o + i] = 0.0;
-        rr[i] = -Bf.g[o + i];
-      } else {
-        Bf.d[o + i] = Bf.d[o + i] + alpha * P[o + i];
-        rr[i] = Bf.r[o + i] - alpha * Bf.q[o + i];
+    for (int h = 0; h < 2; ++h) {
+      const int f = t + 256 * h;
+      if (f < F) {
+        const size_t o = base + (size_t)f * J3 + 3 * j;
+        const double* I = fb + (size_t)f * OPT_FS;
+#pragma unroll
+        for (int e = 0; e < 9; ++e) Iv[h][e] = I[e];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          if (it < 0) {
+            a0v[h][i] = gg[o + i];
+          } else {
+            a0v[h][i] = dd[o + i];
+            a1v[h][i] = pp[o + i];
+            a2v[h][i] = rin[o + i];
+            a3v[h][i] = qq[o + i];
+          }
+        }
       }
-      sr[3 * f + i] = rr[i];
+    }
+    double gv[UG];
+#pragma unroll
+    for (int u2 = 0; u2 < UG; ++u2) {
+      const int idx = t + 256 * u2;
+      const bool back = idx >= K * NN * GB;
+      const int u = back ? idx - K * NN * GB : idx;
+      const int c = u / (NN * GB), k = (u / GB) % NN + 1, e = u % GB;
+      gv[u2] = 0.0;
+      if (idx < 2 * K * NN * GB) {
+        if (!back && c >= 2) gv[u2] = fb[(size_t)(c * F / K - k) * OPT_FS + 9 + 18 * NN + e];
+        if (back && c <= K - 3) gv[u2] = fb[(size_t)((c + 1) * F / K + k - 1) * OPT_FS + 9 + 27 * NN + e];
+      }
+    }
+    for (int i0 = t; i0 < F * MN; i0 += 256 * U) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = i0 + 256 * u;
+        const int f = idx / MN, e = idx - f * MN;
+        v[u] = idx < F * MN ? fb[(size_t)f * OPT_FS + 9 + e] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (i0 + 256 * u < F * MN) smn[i0 + 256 * u] = v[u];
+    }
+#pragma unroll
+    for (int u2 = 0; u2 < UG; ++u2) {
+      const int idx = t + 256 * u2;
+      if (idx < 2 * K * NN * GB) sPhi[idx] = gv[u2];  // sPsi follows sPhi
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int f = t + 256 * h;
+      if (f < F) {
+        const size_t o = base + (size_t)f * J3 + 3 * j;
+        double rr[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          double dn;
+          if (it < 0) {
+            dn = 0.0;
+            rr[i] = -a0v[h][i];
+          } else {
+            dn = a0v[h][i] + alpha * a1v[h][i];
+            rr[i] = a2v[h][i] - alpha * a3v[h][i];
+          }
+          dd[o + i] = dn;
+          sr[3 * f + i] = rr[i];
+        }
+        su[3 * f] = Iv[h][0] * rr[0];
+        su[3 * f + 1] = Iv[h][3] * rr[0] + Iv[h][4] * rr[1];
+        su[3 * f + 2] = Iv[h][6] * rr[0] + Iv[h][7] * rr[1] + Iv[h][8] * rr[2];
+      }
+    }
+  }
+  __syncthreads();
+  OPT_PROF(1);
+  const int cq = t >> 2;  // this lane's chunk in the substitutions
+  const int a0 = cq * F / K, a1 = (cq + 1) * F / K;
+  if (cq < K) lane_substitution<NN, false>(smn, su, sz, a0, a1 - a0, L, F, t);
+  __syncthreads();
+  OPT_PROF(2);
+  // phase 3 (stitching): lane t < 3n owns row (k, r) of the incoming vectors and exchanges them through
+  // LDS within the wave (LDS operations of a wave complete in order); the G rows do not depend on the
+  // recurrence, so only one LDS round trip and n x 3 fmas sit on each step's chain
+  if (t < 3 * NN) {
+    const int k = t / 3 + 1, r = t % 3;
+    for (int c = 1; c < K; ++c) {
+      const int a = c * F / K;
+      double v = sz[3 * (a - k) + r];
+      if (c >= 2) {
+        const double* G = sPhi + ((size_t)c * NN + k - 1) * GB + 3 * r;
+        const double* Sp = sS + (size_t)(c - 1) * NN * 3;
+#pragma unroll
+        for (int jj = 0; jj < NN; ++jj) v += G[9 * jj] * Sp[3 * jj] + G[9 * jj + 1] * Sp[3 * jj + 1] + G[9 * jj + 2] * Sp[3 * jj + 2];
+      }
+      sS[((size_t)c * NN + k - 1) * 3 + r] = v;
+    }
+  }
+  __syncthreads();
+  OPT_PROF(3);
+  for (int f = t; f < F; f += 256) {
+    const int c = ((f + 1) * K + F - 1) / F - 1;
+    double y[3] = {sz[3 * f], sz[3 * f + 1], sz[3 * f + 2]};
+    if (c >= 1) {
+      const double* G = fb + (size_t)f * OPT_FS + 9 + 18 * NN;
+      const double* Sc = sS + (size_t)c * NN * 3;
+#pragma unroll
+      for (int k = 0; k < NN; ++k)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+          y[r] += G[9 * k + 3 * r] * Sc[3 * k] + G[9 * k + 3 * r + 1] * Sc[3 * k + 1] + G[9 * k + 3 * r + 2] * Sc[3 * k + 2];
     }
     const double* I = fb + (size_t)f * OPT_FS;
-    su[3 * f] = I[0] * rr[0];
-    su[3 * f + 1] = I[3] * rr[0] + I[4] * rr[1];
-    su[3 * f + 2] = I[6] * rr[0] + I[7] * rr[1] + I[8] * rr[2];
+    su[3 * f] = I[0] * y[0] + I[3] * y[1] + I[6] * y[2];
+    su[3 * f + 1] = I[4] * y[1] + I[7] * y[2];
+    su[3 * f + 2] = I[8] * y[2];
   }
   __syncthreads();
-  if (t < 4) lane_substitution<NN, false>(smn, su, sz, F, t);
+  OPT_PROF(4);
+  if (cq < K) lane_substitution<NN, true>(smn, su, sz, a0, a1 - a0, L, F, t);
   __syncthreads();
-  for (int f = t; f < F; f += 256) {
-    const double* I = fb + (size_t)f * OPT_FS;
-    const double y0 = sz[3 * f], y1 = sz[3 * f + 1], y2 = sz[3 * f + 2];
-    su[3 * f] = I[0] * y0 + I[3] * y1 + I[6] * y2;
-    su[3 * f + 1] = I[4] * y1 + I[7] * y2;
-    su[3 * f + 2] = I[8] * y2;
+  OPT_PROF(5);
+  if (t < 3 * NN) {  // backward stitching, as the forward one
+    const int k = t / 3 + 1, r = t % 3;
+    for (int c = K - 2; c >= 0; --c) {
+      const int e = (c + 1) * F / K;
+      double v = sz[3 * (e + k - 1) + r];
+      if (c <= K - 3) {
+        const double* H = sPsi + ((size_t)c * NN + k - 1) * GB + 3 * r;
+        const double* Tn = sT + (size_t)(c + 1) * NN * 3;
+#pragma unroll
+        for (int jj = 0; jj < NN; ++jj) v += H[9 * jj] * Tn[3 * jj] + H[9 * jj + 1] * Tn[3 * jj + 1] + H[9 * jj + 2] * Tn[3 * jj + 2];
+      }
+      sT[((size_t)c * NN + k - 1) * 3 + r] = v;
+    }
   }
   __syncthreads();
-  if (t < 4) lane_substitution<NN, true>(smn, su, sz, F, t);
-  __syncthreads();
+  OPT_PROF(6);
   double rz = 0;
-  for (int idx = t; idx < F * 3; idx += 256) {
-    const int f = idx / 3, i = idx - f * 3;
-    const size_t o = base + (size_t)f * J3 + 3 * j + i;
-    Bf.r[o] = sr[idx];
-    Bf.z[o] = sz[idx];
-    rz += sr[idx] * sz[idx];
+  for (int f = t; f < F; f += 256) {
+    const int c = ((f + 1) * K + F - 1) / F - 1;
+    double z[3] = {sz[3 * f], sz[3 * f + 1], sz[3 * f + 2]};
+    if (c <= K - 2) {
+      const double* H = fb + (size_t)f * OPT_FS + 9 + 27 * NN;
+      const double* Tc = sT + (size_t)c * NN * 3;
+#pragma unroll
+      for (int k = 0; k < NN; ++k)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+          z[r] += H[9 * k + 3 * r] * Tc[3 * k] + H[9 * k + 3 * r + 1] * Tc[3 * k + 1] + H[9 * k + 3 * r + 2] * Tc[3 * k + 2];
+    }
+    const size_t o = base + (size_t)f * J3 + 3 * j;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      Bf.r[o + i] = sr[3 * f + i];
+      Bf.z[o + i] = z[i];
+      rz += sr[3 * f + i] * z[i];
+    }
   }
   __syncthreads();
+  OPT_PROF(7);
   double* red = lds_opt;  // r / z are in registers or global memory now
   red[t] = rz;
   __syncthreads();
@@ -928,20 +1246,24 @@ __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBu
     __syncthreads();
   }
   if (t == 0) Bf.rzJ[((size_t)b * (OPT_MAXIT + 1) + (it + 1)) * (J + 1) + j] = red[0];
+  OPT_PROF(8);
+  OPT_PROF_END();
 }
 
 size_t optim_precond_lds_bytes(int F, int NN) {
-  return std::max((size_t)F * (18 * NN + 9), (size_t)256) * sizeof(double);
+  const size_t K = (size_t)opt_chunks(F, NN);
+  const size_t n = (size_t)F * (18 * NN + 3) + (size_t)(F + 1) * 6 + 2 * K * NN * 9 * NN + 2 * K * NN * 3;
+  return std::max(n, (size_t)256) * sizeof(double);
 }
 
 // q = (H + lam diag(H)) p_it with p_it = z + beta p_{it-1} (computed here, written to P[it & 1]).
 __global__ void __launch_bounds__(OPT_THREADS) optim_matvec_kernel(OptDims D, OptBufs Bf, int it) {
   const int f = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   const int F = D.F, J = D.J, J3 = 3 * J, n = D.n;
-  if (pcg_done(D, Bf, b, it)) return;
   __shared__ double sp[2 * OPT_MAXN + 1][OPT_MAXJ * 3];
   __shared__ double spL[OPT_MAXL], stk[OPT_MAXL];
   __shared__ double red[OPT_THREADS];
+  if (pcg_done(D, Bf, b, it)) return;
   const double beta = it == 0 ? 0.0 : rz_at(D, Bf, b, it) / rz_at(D, Bf, b, it - 1);
   double* Pc = (it & 1) ? Bf.P1 : Bf.P0;
   const double* Pp = (it & 1) ? Bf.P0 : Bf.P1;
@@ -1007,15 +1329,15 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_matvec_kernel(OptDims D, Op
 }
 
 // Length part of q and the full p.q (fixed-order reductions over frames).
-__global__ void __launch_bounds__(OPT_THREADS) optim_reduce_pq_kernel(OptDims D, OptBufs Bf, int it) {
+__global__ void __launch_bounds__(OPT_RTHREADS) optim_reduce_pq_kernel(OptDims D, OptBufs Bf, int it) {
   const int b = blockIdx.x, t = threadIdx.x;
   if (pcg_done(D, Bf, b, it)) return;
-  __shared__ double red[OPT_THREADS];
+  __shared__ double red[OPT_RTHREADS];
   const double* P = (it & 1) ? Bf.P1 : Bf.P0;
   const size_t base = (size_t)b * D.NV;
   __shared__ double part[OPT_RCH][OPT_MAXL];
   double s = 0;
-  for (int f = t; f < D.F; f += OPT_THREADS) s += Bf.pqF[(size_t)b * D.F + f];
+  for (int f = t; f < D.F; f += OPT_RTHREADS) s += Bf.pqF[(size_t)b * D.F + f];
   if (!D.fix) len_partials(D, Bf.qLf + (size_t)b * D.F * D.NL, nullptr, part, nullptr, t);
   __syncthreads();
   if (!D.fix && t < D.NL) {
@@ -1025,7 +1347,7 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_reduce_pq_kernel(OptDims D,
     Bf.q[o] = qL;
     s += P[o] * qL;
   }
-  const double tot = block_sum(s, red);
+  const double tot = block_sum<OPT_RTHREADS>(s, red);
   if (t == 0) Bf.pq[(size_t)b * (OPT_MAXIT + 1) + it] = tot;
 }
 
@@ -1143,7 +1465,10 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
 
   // preconditioner step: series staged in LDS when they fit (every clip up to ~450 frames at n = 2)
   const size_t lds_b = optim_precond_lds_bytes(F, D.n);
-  const bool use_lds = g_optim_precond_lds && lds_b <= 160 * 1024;
+  const size_t fac_lds_b = optim_factor_lds_bytes(F, D.n);
+  const bool fac_lds = g_optim_precond_lds && fac_lds_b + 512 <= 160 * 1024;  // + the static constraint list
+  // the chunked LDS apply reads the chunk responses that only the LDS factor kernel writes
+  const bool use_lds = fac_lds && lds_b + 1024 <= 160 * 1024 && F <= 512;  // (two frames per thread)
   auto precond = [&](int it) {
     if (!use_lds) {
       hipLaunchKernelGGL(optim_precond_kernel, dim3(B), dim3(64), 0, s, D, Bf, it);
@@ -1154,9 +1479,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
     else if (D.n == 2) hipLaunchKernelGGL(optim_precond_lds_kernel<2>, grid, dim3(256), lds_b, s, D, Bf, it);
     else hipLaunchKernelGGL(optim_precond_lds_kernel<3>, grid, dim3(256), lds_b, s, D, Bf, it);
   };
-  // factorization: the same choice (the LDS kernel's footprint is smaller than the apply's)
-  const size_t fac_lds_b = optim_factor_lds_bytes(F, D.n);
-  const bool fac_lds = g_optim_precond_lds && fac_lds_b + 512 <= 160 * 1024;  // + the static constraint list
+  // factorization: the LDS kernel whenever the series fits (its footprint is smaller than the apply's)
   auto factor = [&]() {
     if (!fac_lds) {
       hipLaunchKernelGGL(optim_factor_kernel, dim3(B), dim3(64), 0, s, D, Bf);
@@ -1171,10 +1494,11 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
     static bool attr = false;
     if (!attr) {
       const int mx = 160 * 1024;
-      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-      // (dynamic + static LDS may not exceed the CU's 160 KB, or the call fails and leaves a sticky error)
+      // (dynamic + static LDS may not exceed the CU's 160 KB, or the call fails and leaves a sticky error;
+      // both kernels keep under 1 KB of static LDS)
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 1024);
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 1024);
+      (void)hipFuncSetAttribute((const void*)optim_precond_lds_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 1024);
       (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
       (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
       (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
@@ -1183,7 +1507,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
   }
   auto eval = [&](const double* xx, int mode, double* out) {
     hipLaunchKernelGGL(optim_eval_kernel, gridFB, dim3(OPT_THREADS), 0, s, D, Bf, xx, mode);
-    hipLaunchKernelGGL(optim_reduce_kernel, dim3(B), dim3(OPT_THREADS), 0, s, D, Bf, out, mode);
+    hipLaunchKernelGGL(optim_reduce_kernel, dim3(B), dim3(OPT_RTHREADS), 0, s, D, Bf, out, mode);
   };
   eval(x, 0, Bf.cost);
   if (hipMemcpyAsync(cost.data(), Bf.cost, sizeof(double) * B, hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
@@ -1209,7 +1533,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
     precond(-1);
     for (int it = 0; it < npcg; ++it) {
       hipLaunchKernelGGL(optim_matvec_kernel, gridFB, dim3(OPT_THREADS), 0, s, D, Bf, it);
-      hipLaunchKernelGGL(optim_reduce_pq_kernel, dim3(B), dim3(OPT_THREADS), 0, s, D, Bf, it);
+      hipLaunchKernelGGL(optim_reduce_pq_kernel, dim3(B), dim3(OPT_RTHREADS), 0, s, D, Bf, it);
       precond(it);
     }
     hipLaunchKernelGGL(optim_axpy_kernel, dim3(ew_blocks), dim3(256), 0, s, x, Bf.d, xt, D.NX, D.NV, B, D.fix);
@@ -1245,6 +1569,16 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
     }
   }
   if (hipStreamSynchronize(s) != hipSuccess) return -3;
+#ifdef OPT_PROFILE
+  {
+    unsigned long long h[9];
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_opt_prof), sizeof(h));
+    const double n = h[0] ? (double)h[0] : 1.0;
+    fprintf(stderr, "opt_prof blocks %llu us/block:", h[0]);
+    for (int k = 1; k < 9; ++k) fprintf(stderr, " %.2f", h[k] / n / 100.0);  // wall clock: 100 MHz
+    fprintf(stderr, "\n");
+  }
+#endif
   for (int b = 0; b < B; ++b) {
     stats[4 * b + 1] = cost[b];
     stats[4 * b + 2] = iters[b];

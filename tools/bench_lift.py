@@ -26,9 +26,13 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--cpu-optim-frames", type=int, default=300)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--lib", default=None, help="libmq_hip.so to load instead of the in-tree build (A/B runs)")
     args = ap.parse_args()
     import numpy as np
     import torch
+    if args.lib:  # after torch: torch's HIP runtime must be the one the library binds to
+        from mqhip import _lib
+        _lib.load(args.lib)
     from mqhip import synth
     from mqhip.geometry import CameraGroup, viterbi_filter
     from mqhip.optim import optim_points_batch
@@ -66,8 +70,7 @@ def main():
     res["gpu_ms"]["ransac_a13"] = ms
     P2 = np.ascontiguousarray(pts.transpose(0, 2, 1, 3, 4))              # (A,C,F,J,2)
     I3 = init.reshape(A, F, J, 3)
-    ms, (p3, jl, stats, ssf) = timed(lambda: optim_points_batch(g, P2, I3, cons, weak, return_stats=True, **tri),
-                                     reps=1)
+    ms, (p3, jl, stats, ssf) = timed(lambda: optim_points_batch(g, P2, I3, cons, weak, return_stats=True, **tri))
     res["gpu_ms"]["optim_points_a16"] = ms
     res["optim_stats"] = {"cost0": stats[:, 0].tolist(), "cost": stats[:, 1].tolist(),
                           "lm_iters": stats[:, 2].tolist(), "status": stats[:, 3].tolist()}
