@@ -85,6 +85,7 @@ struct OptBufs {
   const double* ctl;  // [B][2]: lambda, accept flag
   double *g, *diag, *R, *lenJ, *costF, *cost;
   double *d, *r, *z, *P0, *P1, *q, *fac, *pinvL, *rzJ, *pq, *pqF, *qLf;
+  double* mn;  // [B][J][F][18 n]: the M / N blocks again, contiguous per series (LDS-DMA staging)
 };
 
 __device__ __forceinline__ const CamParams& cam_at(const double* cams, int c) {
@@ -402,6 +403,10 @@ __device__ __forceinline__ double rsq_f64(double x) {
 template <int NN>
 __device__ __forceinline__ void factor_frame(const OptDims& D, double s2, int f, double (&A)[3][3],
                                              const FacRec (&W)[NN], FacRec& cur) {
+  // Only the structural non-zeros are formed: inv(L_ii) is lower triangular, so L_{f,i} = M inv(L_ii)^T
+  // needs the k <= c terms of each entry; with no older block the product is off * inv(L_ii)^T alone;
+  // and A_f only feeds its lower triangle to the Cholesky below.  (Zero terms added nothing before:
+  // the same values, a third fewer dependent f64 operations on the sequential chain.)
   const int F = D.F;
 #pragma unroll
   for (int d = NN; d >= 1; --d) {
@@ -411,8 +416,19 @@ __device__ __forceinline__ void factor_frame(const OptDims& D, double s2, int f,
       for (int e = 0; e < 9; ++e) cur.L[d - 1][e] = 0.0;
       continue;
     }
-    double M[3][3];
     const double off = s2 * dtd(f, i, F, NN, D.c);
+    const double* Ii = W[d - 1].inv;  // inv(L_ii) (lower)
+    bool older = false;
+#pragma unroll
+    for (int e = d + 1; e <= NN; ++e) older |= f - e >= 0;
+    if (!older) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) cur.L[d - 1][3 * r + c] = r <= c ? off * Ii[3 * c + r] : 0.0;
+      continue;
+    }
+    double M[3][3];
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -428,12 +444,12 @@ __device__ __forceinline__ void factor_frame(const OptDims& D, double s2, int f,
         for (int c = 0; c < 3; ++c)
           M[r][c] -= Lf[3 * r] * Li[3 * c] + Lf[3 * r + 1] * Li[3 * c + 1] + Lf[3 * r + 2] * Li[3 * c + 2];
     }
-    const double* Ii = W[d - 1].inv;  // inv(L_ii) (lower)
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        cur.L[d - 1][3 * r + c] = M[r][0] * Ii[3 * c] + M[r][1] * Ii[3 * c + 1] + M[r][2] * Ii[3 * c + 2];
+    for (int r = 0; r < 3; ++r) {
+      cur.L[d - 1][3 * r + 0] = M[r][0] * Ii[0];
+      cur.L[d - 1][3 * r + 1] = M[r][0] * Ii[3] + M[r][1] * Ii[4];
+      cur.L[d - 1][3 * r + 2] = M[r][0] * Ii[6] + M[r][1] * Ii[7] + M[r][2] * Ii[8];
+    }
   }
 #pragma unroll
   for (int d = 1; d <= NN; ++d) {
@@ -442,7 +458,7 @@ __device__ __forceinline__ void factor_frame(const OptDims& D, double s2, int f,
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
+      for (int c = 0; c <= r; ++c)
         A[r][c] -= Lf[3 * r] * Lf[3 * c] + Lf[3 * r + 1] * Lf[3 * c + 1] + Lf[3 * r + 2] * Lf[3 * c + 2];
   }
   // 3x3 Cholesky by reciprocal square roots: the recurrence's latency chain is three v_rsq_f64 (+ one
@@ -596,21 +612,28 @@ __global__ void __launch_bounds__(256) optim_factor_lds_kernel(OptDims D, OptBuf
   }
   __syncthreads();
   double* fb = Bf.fac + ((size_t)b * J + j) * F * OPT_FS;
+  double* mnb = Bf.mn + ((size_t)b * J + j) * F * (18 * NN);
   for (int f = t; f < F; f += 256) {
     const double* rec = sRec + (size_t)f * RS;
     double* o = fb + (size_t)f * OPT_FS;
 #pragma unroll
     for (int e = 0; e < 9; ++e) o[e] = rec[e];
+    double mnv[18 * NN];
 #pragma unroll
     for (int d = 1; d <= NN; ++d) {
-      premul_M(rec, rec + 9 * d, o + 9 * d);
-      double* on = o + 9 + 9 * NN + 9 * (d - 1);
+      premul_M(rec, rec + 9 * d, mnv + 9 * (d - 1));
+      double* on = mnv + 9 * NN + 9 * (d - 1);
       if (f + d < F) {
         premul_N(rec, sRec + (size_t)(f + d) * RS + 9 * d, on);
       } else {
 #pragma unroll
         for (int e = 0; e < 9; ++e) on[e] = 0.0;
       }
+    }
+#pragma unroll
+    for (int e = 0; e < 18 * NN; ++e) {
+      o[9 + e] = mnv[e];
+      mnb[(size_t)f * 18 * NN + e] = mnv[e];
     }
   }
   // Chunk responses for the chunked substitutions: thread per (direction, chunk, incoming column).
@@ -1053,8 +1076,9 @@ __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBu
   const int K = opt_chunks(F, NN);
   const int L = (F + K - 1) / K;  // longest chunk
   extern __shared__ double lds_opt[];
+  const int MNP = (F * MN + 127) / 128 * 128;  // M / N image padded to whole 1-KiB DMA instructions
   double* smn = lds_opt;                  // [F][MN]
-  double* sr = smn + (size_t)F * MN;      // [F][3] r
+  double* sr = smn + (size_t)MNP;         // [F][3] r
   double* su = sr + (size_t)F * 3;        // [F + 1][3] u, then v (+ pad frame)
   double* sz = su + (size_t)(F + 1) * 3;  // [F + 1][3] y^, then z^ / z (+ pad frame)
   double* sPhi = sz + (size_t)(F + 1) * 3;  // [K][NN][GB] G at each chunk's last NN frames (of chunk c-1)
@@ -1066,7 +1090,6 @@ __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBu
   // loads of all three are issued before any of their stores (one round trip to memory instead of one
   // per loop iteration: each trip is ~2 us when the factor was written on another XCD).
   {
-    constexpr int U = 48;                                       // M / N loads per thread and pass
     constexpr int UG = (2 * OPT_MAXK * NN * GB + 255) / 256;    // G / H loads per thread
     const double* __restrict__ gg = Bf.g;
     const double* __restrict__ rin = Bf.r;
@@ -1109,17 +1132,16 @@ __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBu
         if (back && c <= K - 3) gv[u2] = fb[(size_t)((c + 1) * F / K + k - 1) * OPT_FS + 9 + 27 * NN + e];
       }
     }
-    for (int i0 = t; i0 < F * MN; i0 += 256 * U) {
-      double v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int idx = i0 + 256 * u;
-        const int f = idx / MN, e = idx - f * MN;
-        v[u] = idx < F * MN ? fb[(size_t)f * OPT_FS + 9 + e] : 0.0;
+    // M / N: the contiguous copy of the series (Bf.mn) by LDS-DMA, 1 KiB per wave instruction (16 B per
+    // lane); the last instruction's lanes past the end re-read the series' last 16 B into the pad
+    {
+      const char* src = reinterpret_cast<const char*>(Bf.mn + ((size_t)b * J + j) * F * MN);
+      const int nbytes = F * MN * 8, nins = MNP * 8 / 1024;
+      for (int ins = t >> 6; ins < nins; ins += 4) {
+        const int off = min(ins * 1024 + (t & 63) * 16, nbytes - 16);
+        __builtin_amdgcn_global_load_lds(MQ_LDS_GLOBAL(src + off), MQ_LDS_LOCAL(reinterpret_cast<char*>(smn) + ins * 1024),
+                                         16, 0, 0);
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (i0 + 256 * u < F * MN) smn[i0 + 256 * u] = v[u];
     }
 #pragma unroll
     for (int u2 = 0; u2 < UG; ++u2) {
@@ -1151,6 +1173,7 @@ __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBu
       }
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA of M / N
   __syncthreads();
   OPT_PROF(1);
   const int cq = t >> 2;  // this lane's chunk in the substitutions
@@ -1252,7 +1275,8 @@ __global__ void __launch_bounds__(256) optim_precond_lds_kernel(OptDims D, OptBu
 
 size_t optim_precond_lds_bytes(int F, int NN) {
   const size_t K = (size_t)opt_chunks(F, NN);
-  const size_t n = (size_t)F * (18 * NN + 3) + (size_t)(F + 1) * 6 + 2 * K * NN * 9 * NN + 2 * K * NN * 3;
+  const size_t mnp = ((size_t)F * 18 * NN + 127) / 128 * 128;
+  const size_t n = mnp + (size_t)F * 3 + (size_t)(F + 1) * 6 + 2 * K * NN * 9 * NN + 2 * K * NN * 3;
   return std::max(n, (size_t)256) * sizeof(double);
 }
 
@@ -1378,6 +1402,7 @@ size_t optim_workspace_bytes(int B, int F, int J, int NL) {
   n += (size_t)B * F * 2;                        // costF pqF
   n += (size_t)B * F * NL;                       // qLf
   n += (size_t)B * J * F * OPT_FS + (size_t)B * OPT_MAXL;  // fac pinvL
+  n += (size_t)B * J * F * 18 * OPT_MAXN + 2;               // mn (+ 16-B alignment)
   n += (size_t)B * (OPT_MAXIT + 1) * (J + 2);    // rzJ, pq
   n += (size_t)B * 4;                            // cost, cost_t, ctl(2)
   n += (size_t)NL + 2 + B;                       // constraint pairs (int32), ssf
@@ -1440,6 +1465,8 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
   Bf.pqF = take((size_t)B * F);
   Bf.qLf = take((size_t)B * F * NL);
   Bf.fac = take((size_t)B * J * F * OPT_FS);
+  Bf.mn = take((size_t)B * J * F * 18 * OPT_MAXN + 2);
+  if (reinterpret_cast<uintptr_t>(Bf.mn) & 15) ++Bf.mn;  // 16-B aligned for the LDS-DMA
   Bf.pinvL = take((size_t)B * OPT_MAXL);
   Bf.rzJ = take((size_t)B * (OPT_MAXIT + 1) * (J + 1));
   Bf.pq = take((size_t)B * (OPT_MAXIT + 1));
