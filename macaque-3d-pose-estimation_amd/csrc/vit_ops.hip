@@ -203,11 +203,10 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
   if (wave >= ntb) return;
   const bool has1 = (TT == MAXT) ? true : (wave + ATT_WAVES < ntb);
 
-  // Per query block u: QK(u) -> softmax(u) -> PV(u).  They are issued software-pipelined over the
-  // two blocks -- QK(0); QK(1) with softmax(0); PV(0) with softmax(1); PV(1) -- so that one block's
-  // VALU softmax can fill the MFMA shadow of the other block's matrix products inside the same wave
-  // (an MFMA occupies the matrix pipe for 16 cycles, in which the wave can issue about four
-  // independent VALU instructions).  K / V fragments are read from LDS once per block.  Per value, the arithmetic and its order are those of the unpipelined form.
+  // Per query block u: QK(u) -> softmax(u) -> PV(u), the two blocks one after the other (a
+  // software-pipelined order -- QK(1) under softmax(0) -- needs both blocks' scores live: 138 VGPRs,
+  // three waves per SIMD, and a second workgroup then only fits a CU on complementary SIMDs; the
+  // sequential order stays at <= 128 VGPRs).  K / V fragments are read from LDS once per block.
   f32x4 S[2][MAXT / 16];
 #pragma unroll
   for (int u = 0; u < 2; ++u)

@@ -17,7 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--knob", default="17=1,0", help="KEY=V1,V2,... (default: attention v2 vs v1)")
+    ap.add_argument("--knob", default="20=1,0", help="KEY=V1,V2,... (default: head-major vs row-major QKV)")
     ap.add_argument("--crops", type=int, default=32)
     ap.add_argument("--lib", default=None, help="another build of libmq_hip.so (A/B across builds)")
     args = ap.parse_args()
