@@ -11,7 +11,7 @@
 //   * x0 = [interpolated p3d, strong lengths, weak lengths], non-finite -> 0
 //
 // Pure host code (no HIP call), compiled without FMA contraction so that every expression rounds as
-// numpy's does.  One thread per animal.
+// numpy's does.  One thread per animal for long clips (>= ~1200 frames).
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -108,11 +108,30 @@ void interpolate_series(double* x, long F, long s) {
   }
 }
 
-// medfilt_data (cameras.py:129-133): reflect pad by size + 5, zero pad size // 2, running median
-void median_filter(const double* x, long F, long s, int size, double* out) {
+// the middle of 7 values by the optimal 16-comparator sorting network (the values are finite here:
+// every series is gap-filled first); the median is one of the inputs, so any exact sort gives it
+inline double median7(const double* in) {
+  double a[7] = {in[0], in[1], in[2], in[3], in[4], in[5], in[6]};
+  auto cx = [&](int i, int j) {
+    const double lo = a[i] < a[j] ? a[i] : a[j], hi = a[i] < a[j] ? a[j] : a[i];
+    a[i] = lo;
+    a[j] = hi;
+  };
+  cx(0, 6); cx(2, 3); cx(4, 5);
+  cx(0, 2); cx(1, 4); cx(3, 6);
+  cx(0, 1); cx(2, 5); cx(3, 4);
+  cx(1, 2); cx(4, 6);
+  cx(2, 3); cx(4, 5);
+  cx(1, 2); cx(3, 4); cx(5, 6);
+  return a[3];
+}
+
+// medfilt_data (cameras.py:129-133): reflect pad by size + 5, zero pad size // 2, running median.
+// v: scratch of at least F + 2 (size + 5) + 2 (size / 2) doubles.
+void median_filter(const double* x, long F, long s, int size, double* out, double* v) {
   const long pad = size + 5, h = size / 2;
   const long n = F + 2 * pad;
-  std::vector<double> v(n + 2 * h, 0.0);
+  for (long i = 0; i < h; ++i) v[i] = v[n + h + i] = 0.0;
   for (long i = 0; i < n; ++i) {
     long j = i - pad;   // np.pad mode="reflect" (no edge repeat)
     const long period = 2 * (F - 1);
@@ -123,6 +142,10 @@ void median_filter(const double* x, long F, long s, int size, double* out) {
       if (j >= F) j = period - j;
     }
     v[i + h] = x[j * s];
+  }
+  if (size == 7) {
+    for (long f = 0; f < F; ++f) out[f] = median7(v + f + pad);   // window centre f + pad
+    return;
   }
   std::vector<double> w(size);
   for (long f = 0; f < F; ++f) {
@@ -143,10 +166,10 @@ void prepare_one(const double* p3d, long F, long J, const int32_t* cons, int nS,
     if (gap) interpolate_series(intp.data() + i, F, J * 3);
   }
   // smoothness scale: medfilt per series, |diff| laid out [joint][axis][frame]
-  std::vector<double> med(F), dif;
+  std::vector<double> med(F), dif, scratch(F + 2 * (7 + 5) + 2 * (7 / 2));
   dif.reserve((size_t)std::max<long>(F - 1, 0) * J * 3);
   for (long i = 0; i < J * 3; ++i) {
-    median_filter(intp.data() + i, F, J * 3, 7, med.data());
+    median_filter(intp.data() + i, F, J * 3, 7, med.data(), scratch.data());
     for (long f = 0; f + 1 < F; ++f) dif.push_back(std::fabs(med[f + 1] - med[f]));
   }
   const double m = dif.empty() ? NAN : np_mean(dif);
@@ -197,7 +220,7 @@ extern "C" int mq_optim_prepare(const double* p3ds, int B, int F, int J, const i
       prepare_one(p3ds + (size_t)b * F * J * 3, F, J, constraints, n_strong, n_weak, scale_smooth, x0 + (size_t)b * nx,
                   ssf + b);
     };
-    if (B == 1)
+    if (B == 1 || (long)F * J < 20000)  // ~0.3 ms per animal at 300 frames: threads cost more than they save
       job();
     else
       pool.emplace_back(job);
