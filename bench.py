@@ -415,16 +415,20 @@ def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
                     "box selection and trackers at thresholds 0)"}
 
 
-def clip_lift(kp, cams_np, device):
+def clip_lift(kp, cams_np, device, clips=1):
     """The step-4 lift (Viterbi 2D filter, DLT triangulation, optim_points, reprojection errors; the
     default config_tmpl.toml path) of the keypoints every rank produced in the timed region, gathered in
-    frame order: kp (F, C, A, J, 3) -> wall seconds on rank 0 (BASELINE config 3's last stage)."""
+    frame order: kp (F, C, A, J, 3) -> wall seconds on rank 0 (BASELINE config 3's last stage).  Each
+    rank's frames are its own synthetic sequence, so the gathered frames are lifted as `clips` clips (one
+    per rank), batched as clips x A individuals in one solve."""
     import numpy as np
     import torch
     from mqhip import io as mqio
     from mqhip.geometry import CameraGroup
     from src.pipeline.step4_aniposefiltering import CONFIG_TMPL, filter_2d, reconstruct_3d
-    kp2d = np.ascontiguousarray(kp.transpose(2, 0, 1, 3, 4)).astype(np.float64)   # (A, F, C, J, 3)
+    Ft, C, A = kp.shape[:3]
+    kp = kp.reshape((clips, Ft // clips) + kp.shape[1:])                         # (clips, F, C, A, J, 3)
+    kp2d = np.ascontiguousarray(kp.transpose(0, 3, 1, 2, 4, 5).reshape((clips * A, Ft // clips) + kp.shape[2:3] + kp.shape[4:])).astype(np.float64)   # (clips*A, F, C, J, 3)
     config = mqio.load_toml(CONFIG_TMPL)
     cg = CameraGroup.from_dicts(cams_np, device=device)
     torch.cuda.synchronize(device)
@@ -434,12 +438,13 @@ def clip_lift(kp, cams_np, device):
     kp3d, _, _, _ = reconstruct_3d(kf, cg, config)
     torch.cuda.synchronize(device)
     t2 = time.perf_counter()
-    A, F = kp2d.shape[:2]
-    return {"frames": int(F), "individuals": int(A), "ms": round((t2 - t0) * 1e3, 3),
+    A2, F = kp2d.shape[:2]
+    return {"frames": int(F), "clips": int(clips), "individuals": int(A2 // clips), "ms": round((t2 - t0) * 1e3, 3),
             "viterbi_ms": round((t1 - t0) * 1e3, 3), "triangulate_optim_ms": round((t2 - t1) * 1e3, 3),
             "finite_3d_fraction": round(float(np.isfinite(kp3d).mean()), 4),
             "what": "step 4 (config_tmpl.toml: Viterbi filter, DLT, optim_points, reprojection errors) on the 2D "
-                    "keypoints of every frame of the timed region, gathered from all ranks, run on rank 0"}
+                    "keypoints of every frame of the timed region, gathered from all ranks (one clip per rank, "
+                    "lifted together), run on rank 0"}
 
 
 class Pipeline:
@@ -717,7 +722,7 @@ def main():
     log(f"timed region {dt:.3f} s")
     if rank == 0 and not args.no_lift:
         # BASELINE config 3's last stage: the clip lift of every frame the ranks just processed (rank 0)
-        cl = clip_lift(gathered.cpu().numpy(), cams_np, local)
+        cl = clip_lift(gathered.cpu().numpy(), cams_np, local, clips=world)
         cl["value_with_lift"] = round(frames_done * N_ANIMALS / (dt + cl["ms"] * 1e-3), 3)
         result["clip_lift"] = cl
         log(f"clip lift of {cl['frames']} gathered frames: {cl['ms']:.1f} ms")
