@@ -16,9 +16,15 @@
  *     for missing frames exactly like anipose).
  *
  * Camera parameter rows (`cams`, float64, 24 values per camera, device memory):
- *   fx, fy, skew, cx, cy, xi, k1, k2, p1, p2, R00..R22 (row-major, from rvec via
- *   Rodrigues), t0, t1, t2, 0, 0.   (OmnidirCamera K / xi / D / rvec / tvec,
- *   /root/reference/src/third_party/aniposelib/cameras.py:429-555)
+ *   fx, fy, skew, cx, cy, xi, d0, d1, d2, d3, R00..R22 (row-major, from rvec via
+ *   Rodrigues), t0, t1, t2, model, d4.  `model` selects the camera class
+ *   CameraGroup.from_dicts builds (cameras.py:1972-1982):
+ *     0  OmnidirCamera (cameras.py:429-555): K / xi, d0..d3 = D (k1, k2, p1, p2), d4 = 0;
+ *     1  Camera, pinhole (cameras.py:173-337): matrix, d0..d4 = distortions (k1, k2, p1, p2, k3),
+ *        xi = skew = 0 (cv2.projectPoints / undistortPoints do not use the matrix's skew);
+ *     2  FisheyeCamera (cameras.py:339-426): matrix, d0..d3 = distortions (k1..k4), xi = skew = d4 = 0.
+ *   Every geometry entry point below (undistort, project, DLT, RANSAC, reprojection error,
+ *   optim_points) runs the model of each row.
  */
 #ifndef MQ_HIP_H
 #define MQ_HIP_H
@@ -34,8 +40,11 @@ extern "C" {
  *   2 -- mq_viterbi_filter accepts n_back in [1, 3] only (was [1, 8]); the timing-ablation tuning keys and
  *        MQ_TUNE_ATTENTION_V2 (key 17, the first-generation attention kernel) were removed and now return -2;
  *        MQ_TUNE_OPTIM_PCG_ITERS defaults to 20 (was 40; optim_points results stay within their tolerance);
- *        mq_det_topk_boxes (config-5 capturable box selection) and mq_optim_prepare (host initialisation) added. */
-#define MQ_ABI_VERSION 2
+ *        mq_det_topk_boxes (config-5 capturable box selection) and mq_optim_prepare (host initialisation) added.
+ *   3 -- camera rows carry a model (slot 22: 0 omnidir, 1 pinhole, 2 fisheye) and a fifth distortion
+ *        coefficient (slot 23); rows written for ABI 1-2 (zeros there) keep the omnidir meaning.
+ *        mq_camera_undistort / mq_camera_project added (mq_omnidir_* are the same functions). */
+#define MQ_ABI_VERSION 3
 
 typedef struct mq_ctx mq_ctx;
 typedef struct mq_vitpose mq_vitpose;
@@ -287,11 +296,17 @@ int mq_id_head(mq_ctx* ctx, const float* x, int n, int hw, int c, const float* f
  * (filter_pose.py:48-186) and the mvpose DLT (multicam_toolbox.py:393-486).
  */
 
-/* OmnidirCamera.undistort_points for every camera: pts/out float64 (C, N, 2). */
+/* Camera.undistort_points (cameras.py:310-316, 376-382, 498-507; the row's model) for every camera:
+ * pts/out float64 (C, N, 2) normalised image coordinates.  mq_omnidir_undistort is the ABI-2 name. */
+int mq_camera_undistort(mq_ctx* ctx, const double* cams, int n_cams, const double* pts, int n, double* out,
+                        void* stream);
 int mq_omnidir_undistort(mq_ctx* ctx, const double* cams, int n_cams, const double* pts, int n, double* out,
                          void* stream);
 
-/* OmnidirCamera.project for every camera: p3d (N, 3) -> out (C, N, 2). */
+/* Camera.project (cameras.py:318-323, 384-390, 509-516; the row's model) for every camera:
+ * p3d (N, 3) -> out (C, N, 2) pixels.  mq_omnidir_project is the ABI-2 name. */
+int mq_camera_project(mq_ctx* ctx, const double* cams, int n_cams, const double* p3d, int n, double* out,
+                      void* stream);
 int mq_omnidir_project(mq_ctx* ctx, const double* cams, int n_cams, const double* p3d, int n, double* out,
                        void* stream);
 

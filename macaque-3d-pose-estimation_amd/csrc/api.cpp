@@ -1049,6 +1049,14 @@ int mq_omnidir_project(mq_ctx* ctx, const double* cams, int C, const double* p3d
   return 0;
 }
 
+int mq_camera_undistort(mq_ctx* ctx, const double* cams, int C, const double* pts, int n, double* out, void* stream) {
+  return mq_omnidir_undistort(ctx, cams, C, pts, n, out, stream);
+}
+
+int mq_camera_project(mq_ctx* ctx, const double* cams, int C, const double* p3d, int n, double* out, void* stream) {
+  return mq_omnidir_project(ctx, cams, C, p3d, n, out, stream);
+}
+
 int mq_triangulate_dlt(mq_ctx* ctx, const double* cams, int C, const double* pts, int n, int undistort, double* out,
                        void* stream) {
   int rc = check_geo(ctx, cams, C, n);

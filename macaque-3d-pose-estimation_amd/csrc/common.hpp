@@ -124,10 +124,11 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// Camera row layout shared with include/mq_hip.h (24 doubles per camera).
+// Camera row layout shared with include/mq_hip.h (24 doubles per camera).  model: 0 omnidir, 1 pinhole
+// (k3 = its fifth distortion coefficient), 2 fisheye (k1..k4 in k1, k2, p1, p2); camera.hpp.
 struct CamParams {
   double fx, fy, skew, cx, cy, xi, k1, k2, p1, p2;
   double R[9];
   double t[3];
-  double pad[2];
+  double model, k3;
 };

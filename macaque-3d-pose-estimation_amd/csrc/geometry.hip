@@ -1,55 +1,13 @@
 // float64 multi-view geometry kernels (anipose / mvpose lift).
 // Compiled with -ffp-contract=off so every expression rounds like the numpy oracle.
 #include "common.hpp"
+#include "camera.hpp"
 #include "geometry.hpp"
 
 namespace mq {
 
 __device__ __forceinline__ const CamParams& cam_at(const double* cams, int c) {
   return *reinterpret_cast<const CamParams*>(cams + 24 * c);
-}
-
-// cv2.omnidir.undistortPoints(p, K, D, xi, R = I) restated (oracle/geometry.py).
-__device__ __forceinline__ void omni_undistort(const CamParams& cp, double u, double v, double& ox, double& oy) {
-  const double fx = cp.fx, fy = cp.fy, cx = cp.cx, cy = cp.cy, s = cp.skew;
-  const double ppx = (u * fy - cx * fy - s * (v - cy)) / (fx * fy);
-  const double ppy = (v - cy) / fy;
-  double x = ppx, y = ppy;
-  for (int it = 0; it < 20; ++it) {
-    const double r2 = x * x + y * y;
-    const double r4 = r2 * r2;
-    x = (ppx - 2 * cp.p1 * x * y - cp.p2 * (r2 + 2 * x * x)) / (1 + cp.k1 * r2 + cp.k2 * r4);
-    y = (ppy - 2 * cp.p2 * x * y - cp.p1 * (r2 + 2 * y * y)) / (1 + cp.k1 * r2 + cp.k2 * r4);
-  }
-  const double xi = cp.xi;
-  const double r2 = x * x + y * y;
-  const double a = r2 + 1;
-  const double b = 2 * xi * r2;
-  const double cc = r2 * xi * xi - 1;
-  const double Zs = (-b + sqrt(b * b - 4 * a * cc)) / (2 * a);
-  const double Xw = x * (Zs + xi), Yw = y * (Zs + xi);
-  const double nrm = sqrt(Xw * Xw + Yw * Yw + Zs * Zs);
-  const double Xs = Xw / nrm, Ys = Yw / nrm, Zn = Zs / nrm;
-  ox = Xs / Zn;
-  oy = Ys / Zn;
-}
-
-// cv2.omnidir.projectPoints(X, rvec, tvec, K, xi, D) restated.
-__device__ __forceinline__ void omni_project(const CamParams& cp, double X, double Y, double Z, double& u,
-                                             double& v) {
-  const double* R = cp.R;
-  const double x0 = R[0] * X + R[1] * Y + R[2] * Z + cp.t[0];
-  const double x1 = R[3] * X + R[4] * Y + R[5] * Z + cp.t[1];
-  const double x2 = R[6] * X + R[7] * Y + R[8] * Z + cp.t[2];
-  const double nrm = sqrt(x0 * x0 + x1 * x1 + x2 * x2);
-  const double xs = x0 / nrm, ys = x1 / nrm, zs = x2 / nrm;
-  const double xu = xs / (zs + cp.xi), yu = ys / (zs + cp.xi);
-  const double r2 = xu * xu + yu * yu;
-  const double r4 = r2 * r2;
-  const double xd = xu * (1 + cp.k1 * r2 + cp.k2 * r4) + 2 * cp.p1 * xu * yu + cp.p2 * (r2 + 2 * xu * xu);
-  const double yd = yu * (1 + cp.k1 * r2 + cp.k2 * r4) + cp.p1 * (r2 + 2 * yu * yu) + 2 * cp.p2 * xu * yu;
-  u = cp.fx * xd + cp.skew * yd + cp.cx;
-  v = cp.fy * yd + cp.cy;
 }
 
 // One-sided (Hestenes) Jacobi SVD of an m x N matrix held as N columns of length M
@@ -306,7 +264,7 @@ __global__ void undistort_kernel(const double* __restrict__ cams, int C, const d
   if (i >= C * N) return;
   const int c = i / N;
   double ox, oy;
-  omni_undistort(cam_at(cams, c), pts[2 * i], pts[2 * i + 1], ox, oy);
+  cam_undistort(cam_at(cams, c), pts[2 * i], pts[2 * i + 1], ox, oy);
   out[2 * i] = ox;
   out[2 * i + 1] = oy;
 }
@@ -317,7 +275,7 @@ __global__ void project_kernel(const double* __restrict__ cams, int C, const dou
   if (i >= C * N) return;
   const int c = i / N, n = i % N;
   double u, v;
-  omni_project(cam_at(cams, c), p3d[3 * n], p3d[3 * n + 1], p3d[3 * n + 2], u, v);
+  cam_project(cam_at(cams, c), p3d[3 * n], p3d[3 * n + 1], p3d[3 * n + 2], u, v);
   out[2 * i] = u;
   out[2 * i + 1] = v;
 }
@@ -340,7 +298,7 @@ __global__ __launch_bounds__(64) void triangulate_kernel(const double* __restric
     if (c < C) {
       const double u = pts[2 * ((size_t)c * N + n)], v = pts[2 * ((size_t)c * N + n) + 1];
       double x = u, y = v;
-      if (undistort) omni_undistort(cam_at(cams, c), u, v, x, y);
+      if (undistort) cam_undistort(cam_at(cams, c), u, v, x, y);
       ux[c] = x;
       uy[c] = y;
       if (!(x != x)) {
@@ -365,7 +323,7 @@ __global__ void reproj_kernel(const double* __restrict__ cams, int C, const doub
   double sum = 0.0, cnt = 0.0;
   for (int c = 0; c < C; ++c) {
     double u, v;
-    omni_project(cam_at(cams, c), X, Y, Z, u, v);
+    cam_project(cam_at(cams, c), X, Y, Z, u, v);
     const size_t o = 2 * ((size_t)c * N + n);
     const double ex = p2d[o] - u, ey = p2d[o + 1] - v;
     if (!mean) {
@@ -408,7 +366,7 @@ __global__ __launch_bounds__(64) void ransac_kernel(const double* __restrict__ c
       raw_u[c] = pts[o];
       raw_v[c] = pts[o + 1];
       if (!(raw_u[c] != raw_u[c])) {
-        omni_undistort(cam_at(cams, c), raw_u[c], raw_v[c], ux[c], uy[c]);
+        cam_undistort(cam_at(cams, c), raw_u[c], raw_v[c], ux[c], uy[c]);
         if (!(ux[c] != ux[c])) und_ok |= 1u << c;
         pos2cam[m] = c;
         ++m;
@@ -438,7 +396,7 @@ __global__ __launch_bounds__(64) void ransac_kernel(const double* __restrict__ c
           for (int c = 0; c < C; ++c) {
             if (!((use >> c) & 1u)) continue;
             double u, v;
-            omni_project(cam_at(cams, c), p[0], p[1], p[2], u, v);
+            cam_project(cam_at(cams, c), p[0], p[1], p[2], u, v);
             const double ex = raw_u[c] - u, ey = raw_v[c] - v;
             const double nr = sqrt(ex * ex + ey * ey);
             if (!(nr != nr)) {
@@ -487,7 +445,7 @@ __global__ __launch_bounds__(64) void ransac_kernel(const double* __restrict__ c
     for (int c = 0; c < C; ++c) {
       if (!((use >> c) & 1u)) continue;
       double u, v;
-      omni_project(cam_at(cams, c), p[0], p[1], p[2], u, v);
+      cam_project(cam_at(cams, c), p[0], p[1], p[2], u, v);
       const double ex = raw_u[c] - u, ey = raw_v[c] - v;
       const double nr = sqrt(ex * ex + ey * ey);
       if (!(nr != nr)) {

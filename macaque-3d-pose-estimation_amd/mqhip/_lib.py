@@ -13,13 +13,13 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmq_hip.so"))
-ABI_VERSION = 2  # include/mq_hip.h MQ_ABI_VERSION
+ABI_VERSION = 3  # include/mq_hip.h MQ_ABI_VERSION
 
 EXPORTED = [
     "mq_abi_version", "mq_last_error", "mq_set_tuning", "mq_get_tuning", "mq_create", "mq_destroy",
     "mq_vitpose_create", "mq_vitpose_destroy", "mq_vitpose_set_param", "mq_vitpose_finalize",
     "mq_vitpose_set_graph", "mq_vitpose_timing", "mq_vitpose_timing_result", "mq_crop_udp", "mq_vitpose_forward", "mq_decode_udp", "mq_topdown",
-    "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_triangulate_dlt", "mq_reproj_error",
+    "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_camera_undistort", "mq_camera_project", "mq_triangulate_dlt", "mq_reproj_error",
     "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_geometry_affinity", "mq_match_svt", "mq_viterbi_filter",
     "mq_det_resize_patch", "mq_layernorm", "mq_window_attention", "mq_patch_merge_gather", "mq_upsample_add",
     "mq_im2col3x3", "mq_conv3x3_bf16", "mq_gemm_resid_relu_bf16", "mq_id_conv_bf16", "mq_deconv_subpixel_pack", "mq_deconv_subpixel_bf16", "mq_f32_to_bf16", "mq_subsample2", "mq_nms", "mq_rpn_proposals", "mq_roi_align", "mq_rcnn_post", "mq_det_topk_boxes", "mq_optim_prepare", "mq_optim_points", "mq_attention_bf16",
@@ -61,6 +61,8 @@ _SIGS = {
     "mq_gemm_bf16": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
     "mq_omnidir_undistort": (i32, [vp, vp, i32, vp, i32, vp, vp]),
     "mq_omnidir_project": (i32, [vp, vp, i32, vp, i32, vp, vp]),
+    "mq_camera_undistort": (i32, [vp, vp, i32, vp, i32, vp, vp]),
+    "mq_camera_project": (i32, [vp, vp, i32, vp, i32, vp, vp]),
     "mq_triangulate_dlt": (i32, [vp, vp, i32, vp, i32, i32, vp, vp]),
     "mq_reproj_error": (i32, [vp, vp, i32, vp, vp, i32, i32, vp, vp]),
     "mq_triangulate_ransac": (i32, [vp, vp, i32, vp, i32, i32, f64, vp, vp, vp, vp, vp]),

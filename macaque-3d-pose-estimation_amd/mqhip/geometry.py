@@ -1,7 +1,7 @@
 """Multi-view geometry on MI355X: the aniposelib ``CameraGroup`` surface used by step 4.
 
-Mirrors ``/root/reference/src/third_party/aniposelib/cameras.py`` (OmnidirCamera
-:429-555, CameraGroup :557-2017) for the calls step 4 makes
+Mirrors ``/root/reference/src/third_party/aniposelib/cameras.py`` (Camera :173-337,
+FisheyeCamera :339-426, OmnidirCamera :429-555, CameraGroup :557-2017) for the calls step 4 makes
 (``src/pipeline/step4_aniposefiltering.py``:212-291): ``load``,
 ``subset_cameras_names``, ``triangulate``, ``triangulate_ransac``,
 ``reprojection_error``, ``project``, ``optim_points``.  Inputs/outputs are numpy
@@ -18,7 +18,8 @@ from . import _lib
 
 
 def rodrigues(rvec):
-    """cv2.Rodrigues(rvec) (host-side parameter packing only)."""
+    """cv2.Rodrigues(rvec) (host-side parameter packing only): R = (c I + (1 - c) r r^T) + s [r]_x
+    entry by entry, as OpenCV's cvRodrigues2 / Affine3::rotation evaluate it."""
     r = np.asarray(rvec, dtype=np.float64).ravel()
     th = np.sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2])
     if th < np.finfo(np.float64).eps:
@@ -27,26 +28,124 @@ def rodrigues(rvec):
     c1 = 1.0 - c
     it = 1.0 / th
     x, y, z = r[0] * it, r[1] * it, r[2] * it
-    return np.array([[c + c1 * x * x, c1 * x * y - s * z, c1 * x * z + s * y],
-                     [c1 * x * y + s * z, c + c1 * y * y, c1 * y * z - s * x],
-                     [c1 * x * z - s * y, c1 * y * z + s * x, c + c1 * z * z]])
+    rrt = np.array([[x * x, x * y, x * z], [x * y, y * y, y * z], [x * z, y * z, z * z]])
+    r_x = np.array([[0.0, -z, y], [z, 0.0, -x], [-y, x, 0.0]])
+    return (c * np.eye(3) + c1 * rrt) + s * r_x
 
 
-class OmnidirCamera:
-    """Parameter holder with the OmnidirCamera field names (cameras.py:429-470)."""
+# camera row slot 22 (include/mq_hip.h, csrc/camera.hpp)
+MODEL_OMNIDIR, MODEL_PINHOLE, MODEL_FISHEYE = 0, 1, 2
 
-    def __init__(self, matrix=None, dist=None, size=None, rvec=None, tvec=None, xi=None, K=None, D=None,
-                 name=None):
+
+class Camera:
+    """Pinhole camera with the field names of aniposelib's Camera (cameras.py:173-337); the
+    undistortion / projection (cv2.undistortPoints / cv2.projectPoints, distortions k1, k2, p1, p2[, k3])
+    run in libmq_hip (csrc/camera.hpp)."""
+
+    model = MODEL_PINHOLE
+    n_dist = 5
+
+    def __init__(self, matrix=None, dist=None, size=None, rvec=None, tvec=None, name=None, extra_dist=False):
         self.matrix = np.eye(3) if matrix is None else np.asarray(matrix, dtype=np.float64)
-        self.dist = np.zeros(4) if dist is None else np.asarray(dist, dtype=np.float64).ravel()
+        self.dist = np.zeros(self.n_dist) if dist is None else np.asarray(dist, dtype=np.float64).ravel()
         self.size = size
         self.rvec = np.zeros(3) if rvec is None else np.asarray(rvec, dtype=np.float64).ravel()
         self.tvec = np.zeros(3) if tvec is None else np.asarray(tvec, dtype=np.float64).ravel()
+        self.name = None if name is None else str(name)
+        self.extra_dist = extra_dist
+        self.R = None  # explicit rotation (from_projection); otherwise rodrigues(rvec)
+
+    @classmethod
+    def from_dict(cls, d):
+        """cameras.py:201-212 load_dict keys."""
+        return cls(matrix=d.get("matrix"), dist=d.get("distortions"), size=d.get("size"),
+                   rvec=d.get("rotation", d.get("rvec")), tvec=d.get("translation", d.get("tvec")), name=d.get("name"))
+
+    def get_dict(self):
+        """cameras.py:191-199."""
+        return {"name": self.get_name(), "size": list(self.size) if self.size is not None else None,
+                "matrix": self.matrix.tolist(), "distortions": self.dist.tolist(), "rotation": self.rvec.tolist(),
+                "translation": self.tvec.tolist()}
+
+    def get_name(self):
+        return self.name
+
+    def get_camera_matrix(self):
+        return self.matrix
+
+    def get_distortions(self):
+        return self.dist
+
+    def get_rotation(self):
+        return self.rvec
+
+    def get_translation(self):
+        return self.tvec
+
+    def get_extrinsics_mat(self):
+        M = np.eye(4)
+        M[:3, :3] = rodrigues(self.rvec) if self.R is None else self.R
+        M[:3, 3] = self.tvec
+        return M
+
+    def _extrinsic_rows(self, row):
+        row[10:19] = (rodrigues(self.rvec) if self.R is None else self.R).ravel()
+        row[19:22] = self.tvec[:3]
+        row[22] = self.model
+
+    def param_row(self):
+        """24-double camera row (include/mq_hip.h): fx, fy, 0, cx, cy, 0, k1, k2, p1, p2, R, t, model, k3.
+        cv2.projectPoints / undistortPoints take 4, 5, 8, 12 or 14 coefficients; the rational, thin-prism
+        and tilt terms past the fifth must be zero here."""
+        d = self.dist
+        if d.size < 4 or np.any(d[5:] != 0):
+            raise NotImplementedError(f"camera {self.name!r}: pinhole distortions must be (k1, k2, p1, p2[, k3]) "
+                                      f"(the rational / thin-prism / tilt terms are not implemented), got {d.size}")
+        m = self.matrix
+        row = np.zeros(24)
+        row[0:6] = [m[0, 0], m[1, 1], 0.0, m[0, 2], m[1, 2], 0.0]
+        row[6:10] = d[:4]
+        row[23] = d[4] if d.size > 4 else 0.0
+        self._extrinsic_rows(row)
+        return row
+
+
+class FisheyeCamera(Camera):
+    """aniposelib's FisheyeCamera (cameras.py:339-426): cv2.fisheye.undistortPoints / projectPoints,
+    distortions k1..k4, alpha 0."""
+
+    model = MODEL_FISHEYE
+    n_dist = 4
+
+    def get_dict(self):
+        d = super().get_dict()
+        d["fisheye"] = True
+        return d
+
+    def param_row(self):
+        d = self.dist
+        if d.size != 4:
+            raise NotImplementedError(f"camera {self.name!r}: fisheye distortions must be (k1, k2, k3, k4)")
+        m = self.matrix
+        row = np.zeros(24)
+        row[0:6] = [m[0, 0], m[1, 1], 0.0, m[0, 2], m[1, 2], 0.0]
+        row[6:10] = d
+        self._extrinsic_rows(row)
+        return row
+
+
+class OmnidirCamera(Camera):
+    """Parameter holder with the OmnidirCamera field names (cameras.py:429-555)."""
+
+    model = MODEL_OMNIDIR
+    n_dist = 4
+
+    def __init__(self, matrix=None, dist=None, size=None, rvec=None, tvec=None, xi=None, K=None, D=None,
+                 name=None, extra_dist=False):
+        super().__init__(matrix=matrix, dist=dist, size=size, rvec=rvec, tvec=tvec, name=name, extra_dist=extra_dist)
         self.xi = np.zeros(1) if xi is None else np.asarray(xi, dtype=np.float64).ravel()
         self.K = np.zeros((3, 3)) if K is None else np.asarray(K, dtype=np.float64)
         self.D = np.zeros(4) if D is None else np.asarray(D, dtype=np.float64).ravel()
-        self.name = None if name is None else str(name)
-        self.R = None  # explicit rotation (from_projection); otherwise rodrigues(rvec)
 
     @staticmethod
     def from_projection(P, name=None):
@@ -62,21 +161,16 @@ class OmnidirCamera:
                              rvec=d.get("rotation", d.get("rvec")), tvec=d.get("translation", d.get("tvec")),
                              xi=d.get("xi"), K=d.get("K"), D=d.get("D"), name=d.get("name"))
 
-    def get_name(self):
-        return self.name
-
-    def get_extrinsics_mat(self):
-        M = np.eye(4)
-        M[:3, :3] = rodrigues(self.rvec) if self.R is None else self.R
-        M[:3, 3] = self.tvec
-        return M
+    def get_dict(self):
+        d = super().get_dict()
+        d.update({"Omnidir": True, "xi": self.xi, "K": self.K, "D": self.D})
+        return d
 
     def param_row(self):
         row = np.zeros(24)
         row[0:6] = [self.K[0, 0], self.K[1, 1], self.K[0, 1], self.K[0, 2], self.K[1, 2], float(self.xi[0])]
         row[6:10] = self.D[:4]
-        row[10:19] = (rodrigues(self.rvec) if self.R is None else self.R).ravel()
-        row[19:22] = self.tvec[:3]
+        self._extrinsic_rows(row)
         return row
 
 
@@ -90,28 +184,25 @@ class CameraGroup:
     # ------------------------------------------------------------------ construction
     @staticmethod
     def from_dicts(arr, device: int = 0):
-        """cameras.py:1972-1982: the camera model is chosen per dict -- ``fisheye`` ->
-        FisheyeCamera, ``omnidir`` -> OmnidirCamera, otherwise the pinhole Camera.  The
-        reference pipeline only ever writes omnidir calibrations (step4:101-138,
-        configs/calibration_tmpl.toml:9), so only OmnidirCamera has HIP kernels; a fisheye or
-        pinhole dict raises instead of being run through the omnidir model."""
+        """cameras.py:1972-1982: the camera model is chosen per dict -- ``fisheye`` -> FisheyeCamera,
+        ``omnidir`` -> OmnidirCamera, otherwise the pinhole Camera; groups may mix models."""
         cams = []
-        for i, d in enumerate(arr):
+        for d in arr:
             if d.get("fisheye", False):
-                kind = "fisheye (FisheyeCamera)"
+                cams.append(FisheyeCamera.from_dict(d))
             elif d.get("omnidir", False):
                 cams.append(OmnidirCamera.from_dict(d))
-                continue
             else:
-                kind = "pinhole (Camera)"
-            raise NotImplementedError(
-                f"camera {d.get('name', i)!r} is a {kind} calibration: only omnidir cameras "
-                f"(omnidir = true, the model step 4 writes) are implemented on MI355X")
+                cams.append(Camera.from_dict(d))
         return CameraGroup(cams, device=device)
+
+    def get_dicts(self):
+        """cameras.py:1966-1970."""
+        return [c.get_dict() for c in self.cameras]
 
     @staticmethod
     def load(path, device: int = 0):
-        """cameras.py:1995-2013 (TOML calibration; omnidir cameras)."""
+        """cameras.py:2006-2013 (TOML calibration; every camera model)."""
         try:
             import tomllib as _toml  # py >= 3.11
         except ImportError:  # pragma: no cover - py3.10 image
@@ -164,8 +255,8 @@ class CameraGroup:
         ctx = self._ctx()
         out = torch.empty((C, n, 2), dtype=torch.float64, device=self._dev())
         p_d = self._to_dev(p)  # keep device temporaries alive until the call is enqueued
-        _lib.check(ctx.lib.mq_omnidir_project(ctx.handle, _lib.ptr(self.cams_tensor()), C, _lib.ptr(p_d),
-                                              n, _lib.ptr(out), _lib.stream_ptr(self._dev())), "mq_omnidir_project")
+        _lib.check(ctx.lib.mq_camera_project(ctx.handle, _lib.ptr(self.cams_tensor()), C, _lib.ptr(p_d),
+                                              n, _lib.ptr(out), _lib.stream_ptr(self._dev())), "mq_camera_project")
         return out.cpu().numpy()
 
     def undistort_points(self, points):
@@ -178,9 +269,9 @@ class CameraGroup:
         ctx = self._ctx()
         out = torch.empty((C, n, 2), dtype=torch.float64, device=self._dev())
         flat_d = self._to_dev(flat)
-        _lib.check(ctx.lib.mq_omnidir_undistort(ctx.handle, _lib.ptr(self.cams_tensor()), C,
+        _lib.check(ctx.lib.mq_camera_undistort(ctx.handle, _lib.ptr(self.cams_tensor()), C,
                                                 _lib.ptr(flat_d), n, _lib.ptr(out),
-                                                _lib.stream_ptr(self._dev())), "mq_omnidir_undistort")
+                                                _lib.stream_ptr(self._dev())), "mq_camera_undistort")
         return out.cpu().numpy().reshape(shape)
 
     def triangulate(self, points, undistort=True, progress=False):

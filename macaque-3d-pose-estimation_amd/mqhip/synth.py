@@ -190,7 +190,10 @@ def make_skeletons(n_animals: int = 4, n_frames: int = 300, seed: int = 2):
 
 
 def project_numpy(cam, X):
-    """Omnidir projection (float64) used only to fabricate observations."""
+    """Projection (float64) used only to fabricate observations: the dict's camera model
+    (pinhole / fisheye dicts from make_cameras_model, otherwise omnidir)."""
+    if cam.get("fisheye", False) or not cam.get("omnidir", True):
+        return _project_plain(cam, X)
     R = rodrigues_to_mat(cam["rvec"])
     Xc = X @ R.T + np.asarray(cam["tvec"]).ravel()
     nrm = np.sqrt(np.sum(Xc * Xc, axis=-1, keepdims=True))
@@ -208,6 +211,50 @@ def project_numpy(cam, X):
     u = K[0, 0] * xd + K[0, 1] * yd + K[0, 2]
     v = K[1, 1] * yd + K[1, 2]
     return np.stack([u, v], axis=-1)
+
+
+def _project_plain(cam, X):
+    R = rodrigues_to_mat(cam["rvec"])
+    Xc = X @ R.T + np.asarray(cam["tvec"]).ravel()
+    x, y = Xc[..., 0] / Xc[..., 2], Xc[..., 1] / Xc[..., 2]
+    d = np.asarray(cam["distortions"], dtype=np.float64).ravel()
+    r2 = x * x + y * y
+    if cam.get("fisheye", False):
+        r = np.sqrt(r2)
+        th = np.arctan(r)
+        td = th * (1 + d[0] * th ** 2 + d[1] * th ** 4 + d[2] * th ** 6 + d[3] * th ** 8)
+        g = np.where(r > 1e-8, td / np.maximum(r, 1e-300), 1.0)
+        xd, yd = x * g, y * g
+    else:
+        k = np.zeros(5)
+        k[:d.size] = d[:5]
+        rad = 1 + k[0] * r2 + k[1] * r2 ** 2 + k[4] * r2 ** 3
+        xd = x * rad + 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x)
+        yd = y * rad + k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y
+    m = np.asarray(cam["matrix"], dtype=np.float64)
+    return np.stack([m[0, 0] * xd + m[0, 2], m[1, 1] * yd + m[1, 2]], axis=-1)
+
+
+def make_cameras_model(n_cams: int = 8, model: str = "pinhole", seed: int = 5):
+    """Camera dicts of aniposelib's pinhole ``Camera`` or ``FisheyeCamera`` (cameras.py:173-426) in the
+    calibration.toml key layout (name, size, matrix, distortions, rotation, translation, fisheye), on the
+    extrinsics of make_cameras.  The matrix is each camera's omnidir "matrix" (its effective focal
+    length) with a non-zero skew entry, which OpenCV's pinhole and fisheye functions ignore."""
+    assert model in ("pinhole", "fisheye")
+    rng = np.random.default_rng(seed)
+    out = []
+    for c in make_cameras(n_cams):
+        m = np.asarray(c["matrix"], dtype=np.float64).copy()
+        m[0, 1] = 3.0
+        if model == "pinhole":
+            dist = rng.normal(0.0, 1.0, 5) * np.array([0.05, 0.02, 1e-3, 1e-3, 0.005])
+        else:
+            dist = rng.normal(0.0, 1.0, 4) * np.array([0.02, 0.005, 1e-3, 5e-4])
+        out.append(dict(name=c["name"], size=list(c["size"]), matrix=m, distortions=dist,
+                        rotation=np.ravel(c["rvec"]).copy(), translation=np.ravel(c["tvec"]).copy(),
+                        rvec=np.ravel(c["rvec"]).copy(), tvec=np.ravel(c["tvec"]).copy(),
+                        fisheye=model == "fisheye", omnidir=False))
+    return out
 
 
 def make_kp2d(cams, skel, noise_px: float = 2.0, drop: float = 0.1, seed: int = 3):

@@ -26,7 +26,10 @@ from scipy.sparse import dok_matrix
 # ----------------------------------------------------------------------------- cameras
 
 def rodrigues(rvec):
-    """cv2.Rodrigues(rvec) -> 3x3 (the theta < DBL_EPSILON branch returns I)."""
+    """cv2.Rodrigues(rvec) -> 3x3 (calibration.cpp cvRodrigues2; the same expression as
+    Affine3::rotation, which cv2.fisheye.projectPoints uses): r = rvec / theta,
+    R = (c I + (1 - c) r r^T) + s [r]_x evaluated entry by entry as OpenCV's Matx expression
+    does; theta < DBL_EPSILON returns I."""
     r = np.asarray(rvec, dtype=np.float64).ravel()
     th = np.sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2])
     if th < np.finfo(np.float64).eps:
@@ -36,9 +39,9 @@ def rodrigues(rvec):
     c1 = 1.0 - c
     it = 1.0 / th
     x, y, z = r[0] * it, r[1] * it, r[2] * it
-    return np.array([[c + c1 * x * x, c1 * x * y - s * z, c1 * x * z + s * y],
-                     [c1 * x * y + s * z, c + c1 * y * y, c1 * y * z - s * x],
-                     [c1 * x * z - s * y, c1 * y * z + s * x, c + c1 * z * z]])
+    rrt = np.array([[x * x, x * y, x * z], [x * y, y * y, y * z], [x * z, y * z, z * z]])
+    r_x = np.array([[0.0, -z, y], [z, 0.0, -x], [-y, x, 0.0]])
+    return (c * np.eye(3) + c1 * rrt) + s * r_x
 
 
 def make_M(rvec, tvec):
@@ -126,6 +129,187 @@ class OmnidirCam:
         return p2d - proj
 
 
+class PinholeCam:
+    """cameras.py:173-337 Camera (the hot-path methods) on cv2.undistortPoints / cv2.projectPoints
+    (OpenCV 4.11 undistort.dispatch.cpp cvUndistortPointsInternal, calibration.cpp
+    cvProjectPoints2Internal) restated for the 4- or 5-coefficient model (k1, k2, p1, p2[, k3]); the
+    rational / thin-prism / tilt terms are zero, and the camera matrix's skew entry is not used by
+    either function.  cv2 is absent here: parity with OpenCV itself is unpinned."""
+
+    model = 1
+
+    def __init__(self, d):
+        self.name = str(d["name"])
+        self.K = np.asarray(d["matrix"], dtype=np.float64)
+        dist = np.asarray(d.get("distortions", np.zeros(5)), dtype=np.float64).ravel()
+        if dist.size < 4 or np.any(dist[5:] != 0):
+            raise NotImplementedError("pinhole distortion must be (k1, k2, p1, p2[, k3])")
+        self.dist = np.zeros(5)
+        self.dist[:min(5, dist.size)] = dist[:5]
+        self.rvec = np.asarray(d["rvec"] if "rvec" in d else d["rotation"], dtype=np.float64).ravel()
+        self.tvec = np.asarray(d["tvec"] if "tvec" in d else d["translation"], dtype=np.float64).ravel()
+
+    def extrinsics_mat(self):
+        return make_M(self.rvec, self.tvec)
+
+    def undistort_points(self, pts):
+        """cameras.py:310-316 -> cv2.undistortPoints(pts, K, dist): criteria COUNT 5 (the default of
+        the 6-argument overload), R = P = I."""
+        shape = pts.shape
+        p = np.asarray(pts, dtype=np.float64).reshape(-1, 2)
+        fx, fy, cx, cy = self.K[0, 0], self.K[1, 1], self.K[0, 2], self.K[1, 2]
+        ifx, ify = 1.0 / fx, 1.0 / fy
+        k0, k1, k2, k3, k4 = self.dist
+        out = np.empty_like(p)
+        for i in range(p.shape[0]):
+            u, v = p[i, 0], p[i, 1]
+            x = (u - cx) * ifx
+            y = (v - cy) * ify
+            x0, y0 = x, y
+            for _ in range(5):
+                r2 = x * x + y * y
+                icdist = (1 + ((0.0 * r2 + 0.0) * r2 + 0.0) * r2) / (1 + ((k4 * r2 + k1) * r2 + k0) * r2)
+                if icdist < 0:
+                    x = (u - cx) * ifx
+                    y = (v - cy) * ify
+                    break
+                dx = 2 * k2 * x * y + k3 * (r2 + 2 * x * x) + 0.0 * r2 + 0.0 * r2 * r2
+                dy = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y + 0.0 * r2 + 0.0 * r2 * r2
+                x = (x0 - dx) * icdist
+                y = (y0 - dy) * icdist
+            out[i] = x, y
+        return out.reshape(shape)
+
+    def project(self, p3d):
+        """cameras.py:318-323 -> cv2.projectPoints(p, rvec, tvec, K, dist)."""
+        X = np.asarray(p3d, dtype=np.float64).reshape(-1, 3)
+        R = rodrigues(self.rvec)
+        t = self.tvec
+        x = R[0, 0] * X[:, 0] + R[0, 1] * X[:, 1] + R[0, 2] * X[:, 2] + t[0]
+        y = R[1, 0] * X[:, 0] + R[1, 1] * X[:, 1] + R[1, 2] * X[:, 2] + t[1]
+        z = R[2, 0] * X[:, 0] + R[2, 1] * X[:, 1] + R[2, 2] * X[:, 2] + t[2]
+        with np.errstate(divide="ignore"):
+            iz = np.where(z != 0, 1.0 / z, 1.0)
+        x = x * iz
+        y = y * iz
+        k0, k1, k2, k3, k4 = self.dist
+        r2 = x * x + y * y
+        r4 = r2 * r2
+        r6 = r4 * r2
+        a1 = 2 * x * y
+        a2 = r2 + 2 * x * x
+        a3 = r2 + 2 * y * y
+        cdist = 1 + k0 * r2 + k1 * r4 + k4 * r6
+        xd = x * cdist + k2 * a1 + k3 * a2
+        yd = y * cdist + k2 * a3 + k3 * a1
+        u = xd * self.K[0, 0] + self.K[0, 2]
+        v = yd * self.K[1, 1] + self.K[1, 2]
+        return np.stack([u, v], axis=-1)
+
+    def reprojection_error(self, p3d, p2d):
+        """cameras.py:325-327."""
+        proj = self.project(p3d).reshape(p2d.shape)
+        return p2d - proj
+
+
+class FisheyeCam(PinholeCam):
+    """cameras.py:339-426 FisheyeCamera on cv2.fisheye.undistortPoints / cv2.fisheye.projectPoints
+    (OpenCV 4.11 fisheye.cpp) restated: equidistant model theta_d = theta (1 + k1 theta^2 + ... +
+    k4 theta^8), alpha (skew) 0 as in the reference's calls.  Parity with OpenCV itself is unpinned."""
+
+    model = 2
+
+    def __init__(self, d):
+        self.name = str(d["name"])
+        self.K = np.asarray(d["matrix"], dtype=np.float64)
+        dist = np.asarray(d.get("distortions", np.zeros(4)), dtype=np.float64).ravel()
+        if dist.size != 4:
+            raise NotImplementedError("fisheye distortion must be (k1, k2, k3, k4)")
+        self.dist = dist.copy()
+        self.rvec = np.asarray(d["rvec"] if "rvec" in d else d["rotation"], dtype=np.float64).ravel()
+        self.tvec = np.asarray(d["tvec"] if "tvec" in d else d["translation"], dtype=np.float64).ravel()
+
+    def undistort_points(self, pts):
+        """cameras.py:376-382 -> cv2.fisheye.undistortPoints(pts, K, D): Newton on theta, criteria
+        MAX_ITER + EPS (10, 1e-8) (the binding's default); a point that does not converge, or whose
+        theta changes sign, comes out as (-1e6, -1e6)."""
+        shape = pts.shape
+        p = np.asarray(pts, dtype=np.float64).reshape(-1, 2)
+        f0, f1, c0, c1 = self.K[0, 0], self.K[1, 1], self.K[0, 2], self.K[1, 2]
+        k0, k1, k2, k3 = self.dist
+        out = np.empty_like(p)
+        for i in range(p.shape[0]):
+            pw0 = (p[i, 0] - c0) / f0
+            pw1 = (p[i, 1] - c1) / f1
+            theta_d = np.sqrt(pw0 * pw0 + pw1 * pw1)
+            theta_d = min(max(-np.pi / 2.0, theta_d), np.pi / 2.0)
+            converged = False
+            theta = theta_d
+            scale = 0.0
+            if abs(theta_d) > 1e-8:
+                for _ in range(10):
+                    t2 = theta * theta
+                    t4 = t2 * t2
+                    t6 = t4 * t2
+                    t8 = t6 * t2
+                    a, b, c, e = k0 * t2, k1 * t4, k2 * t6, k3 * t8
+                    fix = (theta * (1 + a + b + c + e) - theta_d) / (1 + 3 * a + 5 * b + 7 * c + 9 * e)
+                    theta = theta - fix
+                    if abs(fix) < 1e-8:
+                        converged = True
+                        break
+                scale = np.tan(theta) / theta_d
+            else:
+                converged = True
+            flipped = (theta_d < 0 and theta > 0) or (theta_d > 0 and theta < 0)
+            if converged and not flipped:
+                out[i] = pw0 * scale, pw1 * scale
+            else:
+                out[i] = -1000000.0, -1000000.0
+        return out.reshape(shape)
+
+    def project(self, p3d):
+        """cameras.py:384-390 -> cv2.fisheye.projectPoints(p, rvec, tvec, K, D)."""
+        X = np.asarray(p3d, dtype=np.float64).reshape(-1, 3)
+        R = rodrigues(self.rvec)
+        t = self.tvec
+        Y0 = R[0, 0] * X[:, 0] + R[0, 1] * X[:, 1] + R[0, 2] * X[:, 2] + t[0]
+        Y1 = R[1, 0] * X[:, 0] + R[1, 1] * X[:, 1] + R[1, 2] * X[:, 2] + t[1]
+        Y2 = R[2, 0] * X[:, 0] + R[2, 1] * X[:, 1] + R[2, 2] * X[:, 2] + t[2]
+        Y2 = np.where(np.abs(Y2) < np.finfo(np.float64).tiny, 1.0, Y2)
+        x0 = Y0 / Y2
+        x1 = Y1 / Y2
+        r = np.sqrt(x0 * x0 + x1 * x1)
+        th = np.arctan(r)
+        th2 = th * th
+        th3 = th2 * th
+        th4 = th2 * th2
+        th5 = th4 * th
+        th6 = th3 * th3
+        th7 = th6 * th
+        th8 = th4 * th4
+        th9 = th8 * th
+        k0, k1, k2, k3 = self.dist
+        theta_d = th + k0 * th3 + k1 * th5 + k2 * th7 + k3 * th9
+        big = r > 1e-8
+        with np.errstate(divide="ignore", invalid="ignore"):
+            cdist = np.where(big, theta_d * (1.0 / np.where(big, r, 1.0)), 1.0)
+        u = (x0 * cdist) * self.K[0, 0] + self.K[0, 2]
+        v = (x1 * cdist) * self.K[1, 1] + self.K[1, 2]
+        return np.stack([u, v], axis=-1)
+
+
+def make_cam(d):
+    """cameras.py:1972-1982: the model of each calibration dict (fisheye, else omnidir, else pinhole)."""
+    if isinstance(d, (OmnidirCam, PinholeCam)):
+        return d
+    if d.get("fisheye", False):
+        return FisheyeCam(d)
+    if d.get("omnidir", False):
+        return OmnidirCam(d)
+    return PinholeCam(d)
+
+
 def triangulate_simple(points, camera_mats):
     """cameras.py:20-32 -- homogeneous DLT, last right-singular vector of the 2k x 4 system."""
     num_cams = len(camera_mats)
@@ -144,7 +328,7 @@ class CameraGroupOracle:
     """cameras.py:557-783 CameraGroup hot-path methods."""
 
     def __init__(self, cam_dicts):
-        self.cameras = [c if isinstance(c, OmnidirCam) else OmnidirCam(c) for c in cam_dicts]
+        self.cameras = [make_cam(c) for c in cam_dicts]
 
     def subset(self, idx):
         g = CameraGroupOracle([])

@@ -1,6 +1,7 @@
-"""CPU: CameraGroup.from_dicts / load honour the camera model of each calibration dict
-(cameras.py:1972-1982).  Omnidir dicts build OmnidirCameras; fisheye and pinhole dicts raise
-instead of being pushed through the omnidir kernels (which would silently return garbage)."""
+"""CPU: CameraGroup.from_dicts / load build the camera model of each calibration dict
+(cameras.py:1972-1982: ``fisheye`` -> FisheyeCamera, ``omnidir`` -> OmnidirCamera, otherwise the
+pinhole Camera), and each model packs the 24-double camera row of include/mq_hip.h (slot 22 = model,
+slot 23 = the pinhole's k3).  No GPU call."""
 import numpy as np
 import pytest
 
@@ -15,29 +16,82 @@ def test_omnidir_dicts_build_omnidir_cameras():
     g = CameraGroup.from_dicts(_dicts())
     assert all(isinstance(c, OmnidirCamera) for c in g.cameras)
     assert g.get_names() == [d["name"] for d in _dicts()]
+    assert all(c.param_row()[22] == 0 for c in g.cameras)
 
 
-@pytest.mark.parametrize("flags,kind", [({"omnidir": False, "fisheye": False}, "pinhole"),
-                                        ({"fisheye": True}, "fisheye"),
-                                        ({}, "pinhole")])
-def test_non_omnidir_dicts_raise(flags, kind):
+@pytest.mark.parametrize("flags,cls", [({"omnidir": False, "fisheye": False}, "Camera"),
+                                       ({"fisheye": True}, "FisheyeCamera"),
+                                       ({"fisheye": True, "omnidir": True}, "FisheyeCamera"),
+                                       ({}, "Camera")])
+def test_model_follows_the_dict_flags(flags, cls):
+    from mqhip import geometry
     from mqhip.geometry import CameraGroup
     ds = _dicts()
     d = {k: v for k, v in ds[1].items() if k not in ("omnidir", "fisheye")}
+    d["distortions"] = np.zeros(4) if cls == "FisheyeCamera" else np.zeros(5)
     d.update(flags)
     ds[1] = d
-    with pytest.raises(NotImplementedError, match=kind):
-        CameraGroup.from_dicts(ds)
+    g = CameraGroup.from_dicts(ds)
+    assert type(g.cameras[1]) is getattr(geometry, cls)
+    assert type(g.cameras[0]) is geometry.OmnidirCamera
 
 
-def test_load_pinhole_calibration_toml_raises(tmp_path):
-    from mqhip import io as mqio
+def test_pinhole_row_layout():
+    from mqhip import synth
+    from mqhip.geometry import Camera, CameraGroup, rodrigues
+    d = synth.make_cameras_model(2, "pinhole")[1]
+    cam = CameraGroup.from_dicts([d]).cameras[0]
+    assert type(cam) is Camera
+    row = cam.param_row()
+    m = d["matrix"]
+    np.testing.assert_array_equal(row[:6], [m[0, 0], m[1, 1], 0.0, m[0, 2], m[1, 2], 0.0])  # skew unused by cv2
+    np.testing.assert_array_equal(row[6:10], d["distortions"][:4])
+    np.testing.assert_array_equal(row[10:19], rodrigues(d["rotation"]).ravel())
+    np.testing.assert_array_equal(row[19:22], d["translation"])
+    assert row[22] == 1 and row[23] == d["distortions"][4]
+    # 4 coefficients: k3 = 0; 8 with zero rational terms: accepted; non-zero rational terms: not implemented
+    assert Camera(matrix=m, dist=d["distortions"][:4]).param_row()[23] == 0
+    Camera(matrix=m, dist=np.r_[d["distortions"], np.zeros(3)]).param_row()
+    with pytest.raises(NotImplementedError, match="rational"):
+        Camera(matrix=m, dist=np.r_[d["distortions"], 0.1, 0, 0], name="x").param_row()
+
+
+def test_fisheye_row_layout():
+    from mqhip import synth
+    from mqhip.geometry import CameraGroup, FisheyeCamera
+    d = synth.make_cameras_model(2, "fisheye")[0]
+    cam = CameraGroup.from_dicts([d]).cameras[0]
+    assert type(cam) is FisheyeCamera
+    row = cam.param_row()
+    np.testing.assert_array_equal(row[6:10], d["distortions"])
+    assert row[2] == 0 and row[5] == 0 and row[22] == 2 and row[23] == 0
+    with pytest.raises(NotImplementedError, match="fisheye"):
+        FisheyeCamera(matrix=d["matrix"], dist=np.zeros(5)).param_row()
+
+
+def test_get_dict_flags_like_the_reference():
+    """cameras.py:191-199, 361-364, 479-485 (OmnidirCamera writes the capitalised 'Omnidir' key)."""
+    from mqhip import synth
     from mqhip.geometry import CameraGroup
-    calib = {f"cam_{i}": {"name": str(d["name"]), "size": [2048, 1536],
-                          "matrix": np.asarray(d["matrix"]).tolist(), "distortions": [0.0] * 5,
-                          "rotation": np.ravel(d["rvec"]).tolist(), "translation": np.ravel(d["tvec"]).tolist()}
-             for i, d in enumerate(_dicts())}
+    ds = synth.make_cameras(1) + synth.make_cameras_model(2, "pinhole")[1:] + synth.make_cameras_model(1, "fisheye")
+    out = CameraGroup.from_dicts(ds).get_dicts()
+    assert out[0]["Omnidir"] is True and "fisheye" not in out[1] and out[2]["fisheye"] is True
+    assert out[1]["distortions"] == list(ds[1]["distortions"])
+
+
+def test_load_pinhole_and_fisheye_calibration_toml(tmp_path):
+    from mqhip import io as mqio
+    from mqhip import synth
+    from mqhip.geometry import Camera, CameraGroup, FisheyeCamera
+    pin = synth.make_cameras_model(2, "pinhole")
+    fis = synth.make_cameras_model(2, "fisheye")
+    calib = {}
+    for i, d in enumerate([pin[0], fis[1]]):
+        calib[f"cam_{i}"] = {"name": str(d["name"]), "size": [2048, 1536], "matrix": np.asarray(d["matrix"]).tolist(),
+                             "distortions": np.ravel(d["distortions"]).tolist(), "rotation": np.ravel(d["rotation"]).tolist(),
+                             "translation": np.ravel(d["translation"]).tolist(), "fisheye": bool(d["fisheye"])}
     p = tmp_path / "calibration.toml"
     mqio.dump_toml(calib, str(p))
-    with pytest.raises(NotImplementedError, match="pinhole"):
-        CameraGroup.load(str(p))
+    g = CameraGroup.load(str(p))
+    assert [type(c) for c in g.cameras] == [Camera, FisheyeCamera]
+    np.testing.assert_array_equal(g.cameras[1].dist, fis[1]["distortions"])
