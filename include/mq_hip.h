@@ -24,7 +24,7 @@
  *        xi = skew = 0 (cv2.projectPoints / undistortPoints do not use the matrix's skew);
  *     2  FisheyeCamera (cameras.py:339-426): matrix, d0..d3 = distortions (k1..k4), xi = skew = d4 = 0.
  *   Every geometry entry point below (undistort, project, DLT, RANSAC, reprojection error,
- *   optim_points) runs the model of each row.
+ *   optim_points) runs the model of each row; any other model value gives NaN results.
  */
 #ifndef MQ_HIP_H
 #define MQ_HIP_H

@@ -17,7 +17,10 @@ namespace mq {
 
 enum CamModel { CAM_OMNIDIR = 0, CAM_PINHOLE = 1, CAM_FISHEYE = 2 };
 
-__device__ __forceinline__ int cam_model(const CamParams& cp) { return (int)cp.model; }
+// the row's model as an int; -1 (no model) for a non-integral slot
+__device__ __forceinline__ int cam_model(const CamParams& cp) {
+  return cp.model == (double)(int)cp.model ? (int)cp.model : -1;
+}
 
 // cv2.omnidir.undistortPoints(p, K, D, xi, R = I) restated (oracle/geometry.py OmnidirCam).
 __device__ __forceinline__ void omni_undistort(const CamParams& cp, double u, double v, double& ox, double& oy) {
@@ -159,19 +162,23 @@ __device__ __forceinline__ void fisheye_project(const CamParams& cp, double X, d
   v = (x1 * cdist) * cp.fy + cp.cy;
 }
 
+// A row whose model slot is none of the three (not a row the host packer writes) gives NaN: garbage in,
+// visibly invalid out, instead of a silently wrong model.
 __device__ __forceinline__ void cam_undistort(const CamParams& cp, double u, double v, double& ox, double& oy) {
   switch (cam_model(cp)) {
+    case CAM_OMNIDIR: omni_undistort(cp, u, v, ox, oy); break;
     case CAM_PINHOLE: pinhole_undistort(cp, u, v, ox, oy); break;
     case CAM_FISHEYE: fisheye_undistort(cp, u, v, ox, oy); break;
-    default: omni_undistort(cp, u, v, ox, oy); break;
+    default: ox = oy = __builtin_nan(""); break;
   }
 }
 
 __device__ __forceinline__ void cam_project(const CamParams& cp, double X, double Y, double Z, double& u, double& v) {
   switch (cam_model(cp)) {
+    case CAM_OMNIDIR: omni_project(cp, X, Y, Z, u, v); break;
     case CAM_PINHOLE: pinhole_project(cp, X, Y, Z, u, v); break;
     case CAM_FISHEYE: fisheye_project(cp, X, Y, Z, u, v); break;
-    default: omni_project(cp, X, Y, Z, u, v); break;
+    default: u = v = __builtin_nan(""); break;
   }
 }
 

@@ -214,9 +214,13 @@ __device__ __forceinline__ void fisheye_project_jac(const CamParams& cp, const d
 __device__ __forceinline__ void project_jac(const CamParams& cp, const double* X, double& u, double& v, double* Ju,
                                             double* Jv) {
   switch (cam_model(cp)) {
+    case CAM_OMNIDIR: omni_project_jac(cp, X, u, v, Ju, Jv); break;
     case CAM_PINHOLE: pinhole_project_jac(cp, X, u, v, Ju, Jv); break;
     case CAM_FISHEYE: fisheye_project_jac(cp, X, u, v, Ju, Jv); break;
-    default: omni_project_jac(cp, X, u, v, Ju, Jv); break;
+    default:  // not a row the host packer writes (camera.hpp)
+      u = v = __builtin_nan("");
+      for (int k = 0; k < 3; ++k) Ju[k] = Jv[k] = 0.0;
+      break;
   }
 }
 

@@ -210,3 +210,24 @@ def test_gpu_optim_points_matches_scipy(kind):
                                    args["scale_length"], args["scale_length_weak"], args["reproj_error_threshold"],
                                    "soft_l1", args["n_deriv_smooth"])
     assert 0.5 * np.sum(r ** 2) <= sa[2].cost * (1 + 1e-3), (0.5 * np.sum(r ** 2), sa[2].cost)
+
+
+@pytest.mark.gpu
+def test_gpu_unknown_model_row_gives_nan():
+    """A camera row whose model slot (include/mq_hip.h slot 22) is not 0, 1 or 2 yields NaN from every
+    geometry entry point instead of silently running another model."""
+    if not gpu_available():
+        pytest.skip("needs a HIP device")
+    import torch
+    from mqhip import synth
+    from mqhip.geometry import CameraGroup
+    cams = synth.make_cameras(3)
+    g = CameraGroup.from_dicts(cams)
+    rows = g.cams_tensor().clone()
+    rows[1, 22] = 7.0
+    g._cams_dev = rows
+    X = synth.make_skeletons(1, 2).reshape(-1, 3)
+    uv = g.project(X)
+    assert np.isfinite(uv[[0, 2]]).all() and np.isnan(uv[1]).all()
+    und = g.undistort_points(uv.copy())
+    assert np.isnan(und[1]).all() and np.isfinite(und[[0, 2]]).all()
