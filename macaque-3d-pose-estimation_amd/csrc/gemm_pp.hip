@@ -408,9 +408,6 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     srs[i] = gw[i] ? rsW : rsA;
     sdst[i] = (gw[i] ? S::OPA : 0) + grow[i] * 128;
   }
-#ifndef MQ_PP_DMAPRIO
-#define MQ_PP_DMAPRIO 0
-#endif
   auto issue = [&](int i, int slot) {
     char* dst = smem + slot * PP_STAGE + sdst[i];
     if (CONV && !gw[i]) {
@@ -511,11 +508,9 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
       for (int i = 0; i < QM; ++i)
         a[i][kk] = pp_frag(As, arow + i * 16 + frow, kk * 4 + fk);
     }
-    if constexpr (MQ_PP_DMAPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < S::C0; ++i) issue(i, slot ^ 1);
     issue_bias();
-    if constexpr (MQ_PP_DMAPRIO) __builtin_amdgcn_s_setprio(0);
     // retires the DMAs of the previous K-step's phase 2 (younger: its phase 3, this phase + bias)
     if (stores_pending)
       pp_wait_vm<S::N0 + EPI_OPS>();
@@ -530,10 +525,8 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
 #pragma unroll
       for (int j = 0; j < NB; ++j)
         b1[j][kk] = pp_frag(Ws, wcol + 16 * NA + j * 16 + frow, kk * 4 + fk);
-    if constexpr (MQ_PP_DMAPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = S::C0; i < S::C0 + S::C1; ++i) issue(i, slot ^ 1);
-    if constexpr (MQ_PP_DMAPRIO) __builtin_amdgcn_s_setprio(0);
     // retires the previous K-step's phase-3 DMAs (younger: phase 0 + bias, this phase)
     if (stores_pending)
       pp_wait_vm<S::N1 + EPI_OPS>();
@@ -549,18 +542,14 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
 #pragma unroll
       for (int i = 0; i < QM; ++i)
         a[i][kk] = pp_frag(As, arow + 16 * QM + i * 16 + frow, kk * 4 + fk);
-    if constexpr (MQ_PP_DMAPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = S::C0 + S::C1; i < S::C0 + S::C1 + S::C2; ++i) issue(i, slot ^ 1);
-    if constexpr (MQ_PP_DMAPRIO) __builtin_amdgcn_s_setprio(0);
     open_mfma();
     mfma_quadrant(1, b0, 0, NAc{});
     bar();
     // ---- phase 3: quadrant (M half 1, N part B)
-    if constexpr (MQ_PP_DMAPRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = S::C0 + S::C1 + S::C2; i < 8; ++i) issue(i, slot ^ 1);
-    if constexpr (MQ_PP_DMAPRIO) __builtin_amdgcn_s_setprio(0);
     advance();
     pp_wait_vm<S::N3>();  // phases 0-1 of this K-step (P0 of stage g+1) and the bias
     open_mfma();
