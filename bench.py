@@ -409,7 +409,8 @@ def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
             "ms_per_frame_with_tracker_and_id": round(ms, 3),
             "individuals_frames_per_s_with_tracker_and_id": round(N_ANIMALS / (ms * 1e-3), 2),
             "detector_ms_per_frame": round(det_ms, 3),
-            "id_classifier_ms_per_frame": round(id_ms, 3), "id_boxes_per_frame": round(sum(nid) / steps, 1),
+            "id_classifier_ms_per_frame": round(id_ms, 3), "id_classifier_boxes_timed": len(id_rows),
+            "id_boxes_per_frame": round(sum(nid) / steps, 1),
             "valid_box_slots": n_valid, "frames_timed": steps,
             "data": "random detector, pose and ID weights, random frames (the detector returns 100 boxes per view; "
                     "box selection and trackers at thresholds 0)"}
