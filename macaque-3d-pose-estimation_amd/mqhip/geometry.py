@@ -88,6 +88,50 @@ class Camera:
         M[:3, 3] = self.tvec
         return M
 
+    # cameras.py:214-299 accessors (host-side parameters; a CameraGroup re-packs its device rows after
+    # any of the setters through CameraGroup.invalidate(), which its own setters call)
+    def set_camera_matrix(self, matrix):
+        self.matrix = np.array(matrix, dtype=np.float64)
+
+    def set_focal_length(self, fx, fy=None):
+        self.matrix[0, 0] = fx
+        self.matrix[1, 1] = fx if fy is None else fy
+
+    def get_focal_length(self, both=False):
+        fx, fy = self.matrix[0, 0], self.matrix[1, 1]
+        return (fx, fy) if both else (fx + fy) / 2.0
+
+    def set_distortions(self, dist):
+        self.dist = np.array(dist, dtype=np.float64).ravel()
+
+    def set_rotation(self, rvec):
+        self.rvec = np.array(rvec, dtype=np.float64).ravel()
+        self.R = None
+
+    def set_translation(self, tvec):
+        self.tvec = np.array(tvec, dtype=np.float64).ravel()
+
+    def set_name(self, name):
+        self.name = str(name)
+
+    def set_size(self, size):
+        self.size = size
+
+    def get_size(self):
+        return self.size
+
+    def resize_camera(self, scale):
+        """cameras.py:269-277."""
+        size = self.get_size()
+        self.set_size((size[0] * scale, size[1] * scale))
+        m = self.get_camera_matrix() * scale
+        m[2, 2] = 1
+        self.set_camera_matrix(m)
+
+    def copy(self):
+        import copy as _copy
+        return _copy.deepcopy(self)
+
     def _extrinsic_rows(self, row):
         row[10:19] = (rodrigues(self.rvec) if self.R is None else self.R).ravel()
         row[19:22] = self.tvec[:3]
@@ -217,6 +261,63 @@ class CameraGroup:
 
     def get_names(self):
         return [c.get_name() for c in self.cameras]
+
+    # cameras.py:1849-1889, 1994-2017: host-side parameter access; setters invalidate the device rows
+    def invalidate(self):
+        """Re-pack the device camera rows on next use (after a camera's parameters were changed)."""
+        self._cams_dev = None
+
+    def copy(self):
+        import copy as _copy
+        return CameraGroup([c.copy() for c in self.cameras], _copy.copy(self.metadata), self.device)
+
+    def set_rotations(self, rvecs):
+        for cam, rvec in zip(self.cameras, rvecs):
+            cam.set_rotation(rvec)
+        self.invalidate()
+
+    def set_translations(self, tvecs):
+        for cam, tvec in zip(self.cameras, tvecs):
+            cam.set_translation(tvec)
+        self.invalidate()
+
+    def get_rotations(self):
+        return np.array([cam.get_rotation() for cam in self.cameras])
+
+    def get_translations(self):
+        return np.array([cam.get_translation() for cam in self.cameras])
+
+    def set_names(self, names):
+        for cam, name in zip(self.cameras, names):
+            cam.set_name(name)
+
+    def average_error(self, p2ds, median=False):
+        """cameras.py:1883-1889: mean (or median) per-point reprojection error of the DLT points."""
+        p3ds = self.triangulate(p2ds)
+        errors = self.reprojection_error(p3ds, p2ds, mean=True)
+        return np.median(errors) if median else np.mean(errors)
+
+    def load_dicts(self, arr):
+        """cameras.py:1994-1996: each camera reloads its parameters from a dict of its own model."""
+        for i, d in enumerate(arr):
+            self.cameras[i] = type(self.cameras[i]).from_dict(d)
+        self.invalidate()
+
+    def dump(self, fname):
+        """cameras.py:1998-2004: TOML with cam_<i> tables and the metadata.  As in the reference, an
+        OmnidirCamera's dict carries the key 'Omnidir' (cameras.py:479-485) while from_dicts tests 'omnidir',
+        so a dumped omnidir group loads back as pinhole cameras; the pipeline's own calibration.toml is
+        written by step 4 with 'omnidir = true'."""
+        from .io import dump_toml
+        dicts = self.get_dicts()
+        master = {f"cam_{i}": _toml_ready(d) for i, d in enumerate(dicts)}
+        master["metadata"] = self.metadata
+        dump_toml(master, fname)
+
+    def resize_cameras(self, scale):
+        for cam in self.cameras:
+            cam.resize_camera(scale)
+        self.invalidate()
 
     def subset_cameras(self, indices):
         return CameraGroup([self.cameras[i] for i in indices], self.metadata, self.device)
@@ -362,6 +463,21 @@ class CameraGroup:
                                  reproj_loss=reproj_loss, n_deriv_smooth=n_deriv_smooth, scores=scores,
                                  verbose=verbose, joint_len=joint_len, max_iter=14)
         return p3, joint_len
+
+
+def _toml_ready(d):
+    """numpy arrays / scalars of a camera dict as TOML-serialisable lists and floats."""
+    out = {}
+    for k, v in d.items():
+        if isinstance(v, np.ndarray):
+            out[k] = v.tolist()
+        elif isinstance(v, (np.floating, np.integer)):
+            out[k] = v.item()
+        elif v is None:
+            continue
+        else:
+            out[k] = v
+    return out
 
 
 def triangulate_pinv(cams: CameraGroup, und, frame_use):

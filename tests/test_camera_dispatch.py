@@ -95,3 +95,48 @@ def test_load_pinhole_and_fisheye_calibration_toml(tmp_path):
     g = CameraGroup.load(str(p))
     assert [type(c) for c in g.cameras] == [Camera, FisheyeCamera]
     np.testing.assert_array_equal(g.cameras[1].dist, fis[1]["distortions"])
+
+
+def test_group_parameter_accessors_and_device_rows():
+    """cameras.py:1849-1882: rotations / translations get and set; the setters re-pack the device rows."""
+    from mqhip import synth
+    from mqhip.geometry import CameraGroup, rodrigues
+    g = CameraGroup.from_dicts(synth.make_cameras_model(3, "pinhole"))
+    r = g.get_rotations()
+    t = g.get_translations()
+    assert r.shape == (3, 3) and t.shape == (3, 3)
+    g._cams_dev = "stale"               # stands in for packed device rows
+    g.set_rotations(r[::-1])
+    assert g._cams_dev is None          # re-packed on next use
+    np.testing.assert_array_equal(g.get_rotations(), r[::-1])
+    np.testing.assert_array_equal(g.cameras[0].param_row()[10:19], rodrigues(r[2]).ravel())
+    g.set_translations(t + 1.0)
+    np.testing.assert_array_equal(g.get_translations(), t + 1.0)
+    g.set_names(["a", "b", "c"])
+    assert g.get_names() == ["a", "b", "c"]
+    c = g.copy()
+    c.cameras[0].set_focal_length(5.0)
+    assert g.cameras[0].get_focal_length() != 5.0 and c.cameras[0].get_focal_length(both=True) == (5.0, 5.0)
+
+
+def test_resize_and_dump_load_round_trip(tmp_path):
+    """cameras.py:269-277, 1998-2017: resize scales matrix and size; dump -> load keeps pinhole and fisheye
+    cameras (an omnidir camera's 'Omnidir' key reloads as pinhole, as in the reference)."""
+    from mqhip import synth
+    from mqhip.geometry import Camera, CameraGroup, FisheyeCamera, OmnidirCamera
+    ds = synth.make_cameras_model(2, "pinhole")[:1] + synth.make_cameras_model(2, "fisheye")[1:] + \
+        synth.make_cameras(3)[2:]
+    g = CameraGroup.from_dicts(ds)
+    g.metadata = {"adjusted": True}
+    p = tmp_path / "calib.toml"
+    g.dump(str(p))
+    h = CameraGroup.load(str(p))
+    assert [type(c) for c in h.cameras] == [Camera, FisheyeCamera, Camera]
+    assert h.metadata == {"adjusted": True}
+    for a, b in zip(g.cameras[:2], h.cameras[:2]):
+        np.testing.assert_array_equal(a.param_row(), b.param_row())
+    m0 = g.cameras[0].get_camera_matrix().copy()
+    g.resize_cameras(0.5)
+    np.testing.assert_array_equal(g.cameras[0].get_camera_matrix()[:2], m0[:2] * 0.5)
+    assert g.cameras[0].get_camera_matrix()[2, 2] == 1 and tuple(g.cameras[0].get_size()) == (1024.0, 768.0)
+    assert isinstance(g.cameras[2], OmnidirCamera)
