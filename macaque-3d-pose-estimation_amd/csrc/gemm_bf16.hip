@@ -9,8 +9,8 @@
 // 128x128 ones (the ID classifier's stage-3/4 convolutions at a frame's dozen boxes, the detector's
 // late Swin stages).  Both accumulate every output in the same order (K ascending, 32 per MFMA), so
 // they agree bit for bit.  Tiles are staged HBM -> LDS with global_load_lds_dwordx4 (no VGPR
-// round trip), double buffered: the next K-tile's DMA is issued before the
-// current tile's MFMAs.  The LDS image is XOR-swizzled on the SOURCE address
+// round trip) through an NS-slot ring: the DMA of K-step t + NS - 1 is issued before step t's MFMAs,
+// and each step waits (counted vmcnt) only for its own stage.  The LDS image is XOR-swizzled on the SOURCE address
 // (16-B chunk c of row r lives at slot c ^ ((r >> 1) & 7)); the ds_read_b128
 // fragment reads are bank-conflict free under that swizzle.
 //
@@ -79,7 +79,7 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds_tile, int row, int c
   return *reinterpret_cast<const bf16x8*>(lds_tile + row * 128 + ((chunk ^ swz(row)) << 4));
 }
 
-template <int EPI, int WF, bool CONV = false>
+template <int EPI, int WF, bool CONV = false, int NS = 2>
 __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) {
   constexpr int TM = 32 * WF;                // tile rows = tile columns
   constexpr int TB = TM * BK * 2;            // bytes per operand tile
@@ -125,27 +125,34 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
       cy[i] = oy * p.conv_s - p.conv_p;
       cx[i] = ox * p.conv_s - p.conv_p;
     }
-    stage_conv_a<WF>(rsA, p, cbase, cy, cx, 0, smem, wave, lane);
-  } else {
-    stage_tile<WF>(p.A, p.lda, m0, p.M, 0, smem, wave, lane);
   }
-  stage_tile<WF>(p.W, p.ldw, n0, p.N, 0, smem + TB, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  // K-step t's A and W tiles -> ring slot t % NS (2 WF DMA instructions per wave)
+  auto issue = [&](int t) {
+    char* st = smem + (t % NS) * 2 * TB;
+    if constexpr (CONV)
+      stage_conv_a<WF>(rsA, p, cbase, cy, cx, t, st, wave, lane);
+    else
+      stage_tile<WF>(p.A, p.lda, m0, p.M, t * BK, st, wave, lane);
+    stage_tile<WF>(p.W, p.ldw, n0, p.N, t * BK, st + TB, wave, lane);
+  };
+  // NS-stage ring: K-steps t+1 .. t+NS-2 stay in flight while step t computes.  Each K-step waits for
+  // its own stage only (counted vmcnt, this wave's DMAs), then one barrier (every wave's part landed,
+  // every wave done reading the slot the next DMA overwrites), then issues stage t+NS-1 into the slot
+  // of step t-1.
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s);
 
   const int frow = lane & 15;
   const int fk = lane >> 4;
   for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nk) {
-      char* nxt = smem + (cur ^ 1) * 2 * TB;
-      if constexpr (CONV)
-        stage_conv_a<WF>(rsA, p, cbase, cy, cx, t + 1, nxt, wave, lane);
-      else
-        stage_tile<WF>(p.A, p.lda, m0, p.M, (t + 1) * BK, nxt, wave, lane);
-      stage_tile<WF>(p.W, p.ldw, n0, p.N, (t + 1) * BK, nxt + TB, wave, lane);
-    }
-    const char* As = smem + cur * 2 * TB;
+    if (t + NS - 2 < nk)
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * WF * (NS - 2)) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + NS - 1 < nk) issue(t + NS - 1);
+    const char* As = smem + (t % NS) * 2 * TB;
     const char* Bs = As + TB;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -160,7 +167,6 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_bf16_kernel(GemmArgs p) 
         for (int j = 0; j < WF; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
   }
 
   // Epilogue.  C layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
@@ -643,32 +649,35 @@ int deconv_subpixel_bf16(const GemmArgs& p, int epi, hipStream_t stream) {
   return gemm_pingpong_deconv(p, epi, g_num_cus, stream);
 }
 
+// 64x64 tiles: a 4-stage ring (64 KiB, still two workgroups per CU) keeps three K-steps of DMA in flight
+// under the short per-step MFMA work; 128x128 tiles: double buffered (64 KiB)
 template <int WF, bool CONV = false>
 static int launch_small(const GemmArgs& p, int epi, hipStream_t stream) {
   constexpr int TM = 32 * WF;
+  constexpr int NS = WF == 2 ? 4 : 2;
   const int tiles = ((p.M + TM - 1) / TM) * ((p.N + TM - 1) / TM);
   dim3 grid(tiles), block(GEMM_THREADS);
-  const size_t lds = 4 * (size_t)TM * BK * 2;
+  const size_t lds = (size_t)NS * 2 * TM * BK * 2;
   if constexpr (CONV) {
     switch (epi) {
-      case EPI_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_BF16, WF, true>), grid, block, lds, stream, p); break;
+      case EPI_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_BF16, WF, true, NS>), grid, block, lds, stream, p); break;
       case EPI_RELU_BF16:
-        hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RELU_BF16, WF, true>), grid, block, lds, stream, p);
+        hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RELU_BF16, WF, true, NS>), grid, block, lds, stream, p);
         break;
-      case EPI_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_F32, WF, true>), grid, block, lds, stream, p); break;
+      case EPI_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_F32, WF, true, NS>), grid, block, lds, stream, p); break;
       default: return -3;
     }
     return hipGetLastError() == hipSuccess ? 0 : -4;
   }
   switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_BF16, WF>), grid, block, lds, stream, p); break;
-    case EPI_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_GELU_BF16, WF>), grid, block, lds, stream, p); break;
-    case EPI_RELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RELU_BF16, WF>), grid, block, lds, stream, p); break;
-    case EPI_RESID_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RESID_F32, WF>), grid, block, lds, stream, p); break;
-    case EPI_POS_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_POS_F32, WF>), grid, block, lds, stream, p); break;
-    case EPI_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_F32, WF>), grid, block, lds, stream, p); break;
-    case EPI_NCHW_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_NCHW_F32, WF>), grid, block, lds, stream, p); break;
-    case EPI_RESID_RELU: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RESID_RELU, WF>), grid, block, lds, stream, p); break;
+    case EPI_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_BF16, WF, false, NS>), grid, block, lds, stream, p); break;
+    case EPI_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_GELU_BF16, WF, false, NS>), grid, block, lds, stream, p); break;
+    case EPI_RELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RELU_BF16, WF, false, NS>), grid, block, lds, stream, p); break;
+    case EPI_RESID_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RESID_F32, WF, false, NS>), grid, block, lds, stream, p); break;
+    case EPI_POS_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_POS_F32, WF, false, NS>), grid, block, lds, stream, p); break;
+    case EPI_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_F32, WF, false, NS>), grid, block, lds, stream, p); break;
+    case EPI_NCHW_F32: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_NCHW_F32, WF, false, NS>), grid, block, lds, stream, p); break;
+    case EPI_RESID_RELU: hipLaunchKernelGGL((gemm_bf16_kernel<EPI_RESID_RELU, WF, false, NS>), grid, block, lds, stream, p); break;
     default: return -3;
   }
   return hipGetLastError() == hipSuccess ? 0 : -4;

@@ -1,7 +1,7 @@
 """Time the Swin-S Mask R-CNN detector (BASELINE config 5's detection stage) on one MI355X:
 8 views of 1536x2048 uint8 frames per step, eager and hipGraph-replayed.
 
-python tools/bench_detector.py [--views 8] [--steps 10] [--graph]
+python tools/bench_detector.py [--views 8] [--steps 10] [--graph] [--lib PATH]
 """
 import argparse
 import json
@@ -19,7 +19,12 @@ def main():
     ap.add_argument("--views", type=int, default=8)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--graph", action="store_true")
+    ap.add_argument("--lib", default=None, help="time this build of libmq_hip.so (A/B of two builds)")
     args = ap.parse_args()
+    if args.lib:
+        import torch  # noqa: F401  (torch's HIP runtime first, as everywhere else)
+        from mqhip import _lib
+        _lib.load(os.path.abspath(args.lib))
     import numpy as np
     import torch
     from mqhip.detector import SwinDetectorHip
