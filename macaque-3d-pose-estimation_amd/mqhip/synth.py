@@ -345,10 +345,17 @@ def make_frames(n_views: int, kp2d_frame=None, seed: int = 4, height: int = IMG_
 
 
 def write_calibration_toml(cams, path):
-    """calibration.toml in the layout step4 writes (step4:101-138) for synthetic cameras."""
+    """calibration.toml in the layout step4 writes (step4:101-138) for synthetic cameras; pinhole / fisheye
+    dicts of make_cameras_model in aniposelib's Camera.get_dict layout (cameras.py:191-199, 361-364)."""
     from .io import dump_toml
     calib = {}
     for i, c in enumerate(cams):
+        if not c.get("omnidir", True):
+            calib[f"cam_{i}"] = {
+                "name": str(c["name"]), "size": list(c["size"]), "matrix": np.asarray(c["matrix"]).tolist(),
+                "distortions": np.ravel(c["distortions"]).tolist(), "rotation": np.ravel(c["rotation"]).tolist(),
+                "translation": np.ravel(c["translation"]).tolist(), "fisheye": bool(c["fisheye"])}
+            continue
         calib[f"cam_{i}"] = {
             "name": str(c["name"]), "size": list(c["size"]), "matrix": np.asarray(c["matrix"]).tolist(),
             "distortions": np.ravel(c["distortions"]).tolist(), "rotation": np.ravel(c["rvec"]).tolist(),

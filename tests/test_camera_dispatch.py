@@ -140,3 +140,18 @@ def test_resize_and_dump_load_round_trip(tmp_path):
     np.testing.assert_array_equal(g.cameras[0].get_camera_matrix()[:2], m0[:2] * 0.5)
     assert g.cameras[0].get_camera_matrix()[2, 2] == 1 and tuple(g.cameras[0].get_size()) == (1024.0, 768.0)
     assert isinstance(g.cameras[2], OmnidirCamera)
+
+
+def test_synthetic_mixed_calibration_toml_round_trip(tmp_path):
+    """synth.write_calibration_toml writes pinhole / fisheye dicts in Camera.get_dict's layout next to the
+    omnidir ones (the step-4 GPU test's mixed calibration); CameraGroup.load gives the same camera rows."""
+    from mqhip import synth
+    from mqhip.geometry import Camera, CameraGroup, FisheyeCamera, OmnidirCamera
+    cams = synth.make_cameras(8)[:2] + synth.make_cameras_model(8, "pinhole")[2:5] + \
+        synth.make_cameras_model(8, "fisheye")[5:]
+    p = tmp_path / "calibration.toml"
+    synth.write_calibration_toml(cams, str(p))
+    g = CameraGroup.load(str(p))
+    assert [type(c) for c in g.cameras] == [OmnidirCamera] * 2 + [Camera] * 3 + [FisheyeCamera] * 3
+    for a, b in zip(g.cameras, CameraGroup.from_dicts(cams).cameras):
+        np.testing.assert_array_equal(a.param_row(), b.param_row())

@@ -21,10 +21,19 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="n
 TRI = dict(scale_smooth=3, scale_length=5, scale_length_weak=2, n_deriv_smooth=2, reproj_error_threshold=3)
 
 
-def _results_dir(tmp_path, A=2, F=36):
+def _cams(kind):
+    from mqhip import synth
+    if kind == "omnidir":
+        return synth.make_cameras(8)
+    # mixed: 2 omnidir, 3 pinhole, 3 fisheye cameras in one calibration.toml (cameras.py:1972-1982)
+    return (synth.make_cameras(8)[:2] + synth.make_cameras_model(8, "pinhole")[2:5] +
+            synth.make_cameras_model(8, "fisheye")[5:])
+
+
+def _results_dir(tmp_path, A=2, F=36, kind="omnidir"):
     from mqhip import io as mqio
     from mqhip import synth
-    cams = synth.make_cameras(8)
+    cams = _cams(kind)
     skel = synth.make_skeletons(A, F)
     kp2d = synth.make_kp2d(cams, skel, noise_px=2.0, drop=0.1)       # (A,F,C,J,3)
     rd = tmp_path / "results" / "demo"
@@ -38,13 +47,16 @@ def _results_dir(tmp_path, A=2, F=36):
     return cams, kp2d, str(tmp_path / "results"), str(cal / "config.yaml")
 
 
-def test_step4_proc_matches_oracle(tmp_path):
+@pytest.mark.parametrize("kind", ["omnidir", "mixed"])
+def test_step4_proc_matches_oracle(tmp_path, kind):
+    """step 4 end to end; "mixed": a calibration.toml holding omnidir, pinhole and fisheye cameras, loaded
+    through CameraGroup.load into the three models."""
     from mqhip import io as mqio
     from mqhip import synth
     from oracle.geometry import CameraGroupOracle, optim_points
     from oracle.viterbi import step4_filter
     from src.pipeline import step4_aniposefiltering as step4
-    cams, kp2d, root, cfg = _results_dir(tmp_path)
+    cams, kp2d, root, cfg = _results_dir(tmp_path, kind=kind)
     data = step4.proc("demo", root, cfg, 17, redo=True)
     rd = os.path.join(root, "demo")
     got = mqio.load_array_pickle(os.path.join(rd, "kp3d.pickle"))
