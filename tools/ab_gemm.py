@@ -22,6 +22,7 @@ def open_lib(path):
     lib.mq_create.argtypes = [i32, C.POINTER(vp)]
     lib.mq_gemm_bf16.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]
     lib.mq_attention_bf16.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp]
+    lib.mq_layernorm.argtypes = [vp, vp, vp, vp, vp, i32, i32, C.c_float, i32, vp]
     ctx = vp()
     assert lib.mq_create(0, C.byref(ctx)) == 0
     return lib, ctx
@@ -35,6 +36,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--attention", action="store_true")
+    ap.add_argument("--layernorm", action="store_true", help="also time mq_layernorm (ViT-H rows, bf16 and f32 out)")
     args = ap.parse_args()
     import torch
     libs = {"A": open_lib(args.a), "B": open_lib(args.b)}
@@ -43,7 +45,7 @@ def main():
     P = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
     g = torch.Generator(device=dev)
     g.manual_seed(0)
-    for name in args.shape.split(","):
+    for name in [n for n in args.shape.split(",") if n]:
         M, N, K, epi = SHAPES[name]
         a = torch.randn((M, K), generator=g, device=dev).to(torch.bfloat16)
         w = (torch.randn((N, K), generator=g, device=dev) / K ** 0.5).to(torch.bfloat16)
@@ -84,6 +86,34 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 print(f"attention {key} r={rnd}: {e0.elapsed_time(e1) / args.iters * 1e3:.1f} us", flush=True)
+
+    if args.layernorm:
+        rows, dim = 64 * 192, 1280
+        x = torch.randn((rows, dim), generator=g, device=dev) * 3 + 0.5
+        gam = torch.randn((dim,), generator=g, device=dev)
+        bet = torch.randn((dim,), generator=g, device=dev)
+        for out_f32 in (0, 1):
+            outs = {}
+            for rnd in range(args.rounds):
+                for key, (lib, ctx) in libs.items():
+                    y = torch.empty((rows, dim), device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
+                    run = lambda: lib.mq_layernorm(ctx, P(x), P(gam), P(bet), P(y), rows, dim, 1e-6, out_f32, s)  # noqa: E731
+                    for _ in range(3):
+                        assert run() == 0
+                    torch.cuda.synchronize()
+                    outs.setdefault(key, y.clone())
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(args.iters):
+                        run()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    us = e0.elapsed_time(e1) / args.iters * 1e3
+                    nbytes = rows * dim * (4 + (4 if out_f32 else 2))
+                    print(f"layernorm out_f32={out_f32} {key} r={rnd}: {us:.2f} us  {nbytes / (us * 1e-6) / 1e12:.2f} TB/s",
+                          flush=True)
+            print(f"layernorm out_f32={out_f32}: A and B bit-identical = {bool(torch.equal(outs['A'], outs['B']))}",
+                  flush=True)
 
 
 if __name__ == "__main__":
