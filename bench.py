@@ -595,7 +595,10 @@ def main():
     backend = os.environ.get("MQ_BENCH_BACKEND", "nccl")
     if os.environ.get("MQ_BENCH_SHARE_GPU") == "1":
         local = local % torch.cuda.device_count()
-    if world > 1:
+    # MQ_BENCH_DIST=1 (never set by the driver): the process group, the keypoint all-gather and the
+    # max-over-ranks timing also at world 1 -- an RCCL rehearsal of the N > 1 code on a one-GPU box
+    dist_on = world > 1 or os.environ.get("MQ_BENCH_DIST") == "1"
+    if dist_on:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
@@ -649,7 +652,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     timing = not args.graph
@@ -660,18 +663,18 @@ def main():
         step(args.warmup + i, log_slot=i)
     # the one exchange step: every rank's per-view 2D keypoints, in frame order (mqhip.shard)
     per_frame = kp_log.view(args.steps, FPS, N_VIEWS, N_ANIMALS, cfg.n_joints, 3).flatten(0, 1)
-    if world > 1:
+    if dist_on:
         gathered = gather_keypoints(per_frame.to(xdev), world * args.steps * FPS, world)
     else:
         gathered = per_frame
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     if timing:
         _lib.check(lib.mq_vitpose_timing(model.handle, 0), "timing")
-    if world > 1:
+    if dist_on:
         t = torch.tensor([dt], device=xdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -759,7 +762,7 @@ def main():
         result["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 
