@@ -49,8 +49,8 @@ def n_joints_of(pose_model, default=17):
 
 def _all_gather(buf, world, group=None):
     import torch.distributed as dist
-    if world == 1:
-        return [buf]
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
+        return [buf]  # no process group (a process group of one, e.g. an RCCL rehearsal, still gathers)
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
     return parts

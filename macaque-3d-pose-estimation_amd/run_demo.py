@@ -59,7 +59,8 @@ def proc(data_name, fps, results_dir_root, device_str, config_path, raw_data_dir
 def _dist_from_env(backend=None):
     """torch.distributed.run environment -> (world, rank, local_rank, group, gather_device).  Backend
     "nccl" (RCCL over xGMI, one GPU per rank) unless MQ_DIST_BACKEND=gloo (host tensors: a rehearsal
-    of several ranks on one GPU, MQ_SHARE_GPU=1)."""
+    of several ranks on one GPU, MQ_SHARE_GPU=1).  MQ_DIST_FORCE=1 builds the process group also at world
+    size 1 (an RCCL rehearsal of the gather on a one-GPU box; never needed for a real run)."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -69,7 +70,7 @@ def _dist_from_env(backend=None):
     if os.environ.get("MQ_SHARE_GPU") == "1":
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
-    if world == 1:
+    if world == 1 and os.environ.get("MQ_DIST_FORCE") != "1":
         return 1, 0, local, None, None
     if backend == "nccl":
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -85,11 +85,12 @@ def main():
     if rank == 0:
         print(json.dumps({"config": "BASELINE config 3 (+ step 4 of config 4's path: Viterbi, DLT, optim_points)",
                           "frames": a.frames, "views": a.views, "individuals": a.animals, "model": a.model,
-                          "world": world, "backend": os.environ.get("MQ_DIST_BACKEND", "nccl") if world > 1 else None,
+                          "world": world,
+                          "backend": os.environ.get("MQ_DIST_BACKEND", "nccl") if dist.is_initialized() else None,
                           "id_classifier": not a.no_id, "seconds": {k: round(v, 4) for k, v in times.items()},
                           "total_s": round(total, 4),
                           "individuals_frames_per_s": round(a.animals * a.frames / total, 2)}), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 
