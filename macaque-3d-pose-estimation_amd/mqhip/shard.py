@@ -75,8 +75,7 @@ def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, 
     plans, jobs = s1.plan_jobs(stores, T, kp_params, tracks)
     n_steps, C = len(T), len(stores)
     s0, e0 = frame_block(n_steps, world, rank)
-    raw = s1.run_pose(pose_model, stores, jobs, range(s0, e0), steps_per_batch)
-    id_raw = None if id_model is None else s1.run_id(id_model, stores, jobs, range(s0, e0), steps_per_batch)
+    raw, id_raw = s1.run_pose_id(pose_model, id_model, stores, jobs, range(s0, e0), steps_per_batch)
     # the buffer shape must agree on every rank, also on a rank whose block holds no pose job:
     # take J from the model, never from this rank's results
     J = n_joints_of(pose_model)

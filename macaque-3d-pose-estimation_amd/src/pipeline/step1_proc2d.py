@@ -429,6 +429,68 @@ def run_id(id_model, stores, jobs, steps, steps_per_batch=8):
     return out
 
 
+_PINNED = {}
+
+
+def _pinned_frames(shape, device_index):
+    """A reusable page-locked host buffer of at least ``shape`` (n, H, W, 3) u8 for the frame uploads."""
+    import torch
+    n = int(np.prod(shape))
+    buf = _PINNED.get(device_index)
+    if buf is None or buf.numel() < n:
+        buf = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+        _PINNED[device_index] = buf
+    return buf[:n].view(*shape)
+
+
+def run_pose_id(pose_model, id_model, stores, jobs, steps, steps_per_batch=8):
+    """``run_pose`` and ``run_id`` over the same batches with every frame of a batch read and uploaded
+    once: the images go through one page-locked buffer into one device tensor per image size, and the
+    pose crops and the ID patches are cut from that copy (the separate passes stacked and uploaded the
+    frames twice).  Batches, their order and their box order are the two passes' own, so the results
+    are theirs bit for bit.  Returns (raw, id_raw); id_raw is None without an ``id_model``."""
+    if getattr(pose_model, "device_index", None) is None:  # a stand-in model (host tests): the two passes
+        return (run_pose(pose_model, stores, jobs, steps, steps_per_batch),
+                None if id_model is None else run_id(id_model, stores, jobs, steps, steps_per_batch))
+    import torch
+    models = None if id_model is None else (
+        id_model if isinstance(id_model, (list, tuple)) else [id_model] * len(stores))
+    steps = [k for k in steps if k in jobs]
+    dev = torch.device("cuda", pose_model.device_index)
+    raw, id_raw = {}, (None if models is None else {})
+    for b0 in range(0, len(steps), steps_per_batch):
+        by_shape = {}
+        for k in steps[b0:b0 + steps_per_batch]:
+            for (c, fn, boxes, _, bb) in jobs[k]:
+                img = stores[c].image(fn)
+                by_shape.setdefault(img.shape, []).append(((k, c), img, boxes, bb))
+        for shape, items in by_shape.items():
+            host = _pinned_frames((len(items),) + tuple(shape), pose_model.device_index)
+            for i, (_, img, _, _) in enumerate(items):
+                host[i].numpy()[...] = img
+            frames = host.to(dev, non_blocking=True)
+            out = inference_topdown_batch(pose_model, frames, [bb for _, _, _, bb in items])
+            for (key, _, _, _), r in zip(items, out):
+                kp = np.stack([np.asarray(x.pred_instances.keypoints[0], dtype=np.float64) for x in r])
+                sc = np.stack([np.asarray(x.pred_instances.keypoint_scores[0], dtype=np.float32) for x in r])
+                raw[key] = (kp, sc)
+            if models is not None:
+                # run_id's grouping: per (model, image size), items in step / camera order
+                groups = {}
+                for i, ((k, c), _, boxes, _) in enumerate(items):
+                    if models[c] is None:
+                        id_raw[(k, c)] = [{"pred_label": -1, "pred_score": 0.0} for _ in boxes]
+                    else:
+                        groups.setdefault(id(models[c]), (models[c], []))[1].append(i)
+                for model, idx in groups.values():
+                    sel = set(idx)
+                    preds = model.classify(frames, [items[i][2] if i in sel else [] for i in range(len(items))])
+                    for i in idx:
+                        id_raw[items[i][0]] = preds[i]
+            torch.cuda.current_stream(dev).synchronize()  # the pinned buffer is refilled next
+    return raw, id_raw
+
+
 def _as_results(kp, sc):
     from types import SimpleNamespace
     return [SimpleNamespace(pred_instances=SimpleNamespace(keypoints=kp[i][None], keypoint_scores=sc[i][None]))
@@ -473,8 +535,7 @@ def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8
     frame).  With ``id_model`` the tracked boxes are classified on the GPU the same way (else the stores'
     ID predictions, if any).  Returns per camera (alldata rows per kept frame, frame numbers)."""
     plans, jobs = plan_jobs(stores, T, kp_params, tracks)
-    raw = run_pose(pose_model, stores, jobs, range(len(T)), steps_per_batch)
-    id_raw = None if id_model is None else run_id(id_model, stores, jobs, range(len(T)), steps_per_batch)
+    raw, id_raw = run_pose_id(pose_model, id_model, stores, jobs, range(len(T)), steps_per_batch)
     return assemble_rows(stores, T, plans, jobs, raw, kp_params, id_raw)
 
 

@@ -145,3 +145,27 @@ def test_config3_two_ranks_shared_gpu_equals_single_process(clip, single):
     info = json.loads(line)
     assert info["world"] == 2 and info["frames"] == N_FRAMES
     _assert_same_outputs(single[0], res, camera_ids(cfg))
+
+
+def test_run_pose_id_equals_separate_passes(clip, pose):
+    """step 1's single-upload batch loop (run_pose_id: each batch's frames uploaded once, pose crops and
+    ID patches cut from that copy) gives run_pose's keypoints / scores and run_id's predictions bit for bit
+    on the first 24 time steps of the clip (3 batches, 8 cameras, each camera's ID variant)."""
+    import glob
+
+    from mqhip.io import FrameStore
+    from src.pipeline import step1_proc2d as s1
+    root, raw_dir, cfg = clip
+    stores = [FrameStore(os.path.dirname(p)) for p in sorted(glob.glob(os.path.join(raw_dir, "clip.*", "metadata.yaml")))]
+    md0 = stores[0].get_frame_metadata()
+    T = np.arange(md0["frame_time"][0], md0["frame_time"][-1], 1.0 / 24)
+    _, jobs = s1.plan_jobs(stores, T)
+    ids = s1.resolve_id_models(stores, "auto", "cuda:0")
+    steps = range(24)
+    raw_a = s1.run_pose(pose, stores, jobs, steps, 8)
+    id_a = s1.run_id(ids, stores, jobs, steps, 8)
+    raw_b, id_b = s1.run_pose_id(pose, ids, stores, jobs, steps, 8)
+    assert raw_a.keys() == raw_b.keys() and len(raw_a) > 0
+    for k in raw_a:
+        assert np.array_equal(raw_a[k][0], raw_b[k][0]) and np.array_equal(raw_a[k][1], raw_b[k][1]), k
+    assert id_a == id_b and len(id_a) == len(raw_a)
