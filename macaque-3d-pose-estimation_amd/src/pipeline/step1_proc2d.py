@@ -430,64 +430,137 @@ def run_id(id_model, stores, jobs, steps, steps_per_batch=8):
 
 
 _PINNED = {}
+_SIDE = {}
 
 
-def _pinned_frames(shape, device_index):
-    """A reusable page-locked host buffer of at least ``shape`` (n, H, W, 3) u8 for the frame uploads."""
+def _pinned_frames(shape, key):
+    """A reusable page-locked host buffer of at least ``shape`` (n, H, W, 3) u8 per ``key``."""
     import torch
     n = int(np.prod(shape))
-    buf = _PINNED.get(device_index)
+    buf = _PINNED.get(key)
     if buf is None or buf.numel() < n:
         buf = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-        _PINNED[device_index] = buf
+        _PINNED[key] = buf
     return buf[:n].view(*shape)
 
 
+def _to_host(t):
+    """Device -> page-locked host copy, queued on the current stream (read it after the batch's event)."""
+    import torch
+    h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    h.copy_(t, non_blocking=True)
+    return h
+
+
 def run_pose_id(pose_model, id_model, stores, jobs, steps, steps_per_batch=8):
-    """``run_pose`` and ``run_id`` over the same batches with every frame of a batch read and uploaded
-    once: the images go through one page-locked buffer into one device tensor per image size, and the
-    pose crops and the ID patches are cut from that copy (the separate passes stacked and uploaded the
-    frames twice).  Batches, their order and their box order are the two passes' own, so the results
-    are theirs bit for bit.  Returns (raw, id_raw); id_raw is None without an ``id_model``."""
+    """``run_pose`` and ``run_id`` over the same batches, pipelined: every frame of a batch is read once
+    into a page-locked buffer (two, alternating) and uploaded once on a side stream; the pose crops and the
+    ID patches are cut from that device copy; the outputs come back by queued copies, and the host reads
+    batch b - 1's results while the GPU runs batch b (the two passes stacked and uploaded every frame twice
+    and waited on each batch).  Batches, their order and their box order are the two passes' own, so the
+    results are theirs bit for bit.  Returns (raw, id_raw); id_raw is None without an ``id_model``."""
     if getattr(pose_model, "device_index", None) is None:  # a stand-in model (host tests): the two passes
         return (run_pose(pose_model, stores, jobs, steps, steps_per_batch),
                 None if id_model is None else run_id(id_model, stores, jobs, steps, steps_per_batch))
     import torch
+    from mqhip.apis import _sample
+    from mqhip.resnet_id import patch_bounds
     models = None if id_model is None else (
         id_model if isinstance(id_model, (list, tuple)) else [id_model] * len(stores))
     steps = [k for k in steps if k in jobs]
-    dev = torch.device("cuda", pose_model.device_index)
+    di = pose_model.device_index
+    dev = torch.device("cuda", di)
+    cs = torch.cuda.current_stream(dev)
+    xs = _SIDE.get(di)
+    if xs is None:
+        xs = _SIDE[di] = torch.cuda.Stream(device=dev)
     raw, id_raw = {}, (None if models is None else {})
-    for b0 in range(0, len(steps), steps_per_batch):
+
+    def launch(items, key):
+        host = _pinned_frames((len(items),) + tuple(items[0][1].shape), key)
+        for i, (_, img, _, _) in enumerate(items):
+            host[i].numpy()[...] = img
+        with torch.cuda.stream(xs):
+            frames = host.to(dev, non_blocking=True)
+            up = torch.cuda.Event()
+            up.record(xs)
+        cs.wait_event(up)
+        frames.record_stream(cs)
+        # pose: inference_topdown_batch's batch, outputs left on the device
+        boxes, owner = [], []
+        for i, (_, _, _, bb) in enumerate(items):
+            b = np.asarray(bb, dtype=np.float32).reshape(-1, 4)
+            boxes.append(b)
+            owner += [i] * len(b)
+        pose_out = None
+        if owner:
+            allb = np.concatenate(boxes)
+            kp, score, _ = pose_model.net.topdown(frames, torch.from_numpy(allb).to(dev),
+                                                  torch.tensor(owner, dtype=torch.int32, device=dev),
+                                                  flip_test=pose_model.flip_test)
+            pose_out = (allb, owner, _to_host(kp), _to_host(score))
+        # ID: run_id's grouping (per model, items in step / camera order) and classify's box order
+        id_out = []
+        if models is not None:
+            groups = {}
+            for i, ((k, c), _, bxs, _) in enumerate(items):
+                if models[c] is None:
+                    id_raw[(k, c)] = [{"pred_label": -1, "pred_score": 0.0} for _ in bxs]
+                else:
+                    groups.setdefault(id(models[c]), (models[c], []))[1].append(i)
+            for model, idx in groups.values():
+                res = {i: [{"pred_label": -1, "pred_score": 0.0} for _ in range(len(items[i][2]))] for i in idx}
+                rows, where = [], []
+                for i in idx:
+                    for j, b in enumerate(np.asarray(items[i][2]).reshape(-1, 4)):
+                        pb = patch_bounds(frames.shape[1:3], b)
+                        if pb is not None:
+                            y0, y1, x0, x1 = pb
+                            rows.append((i, x0, y0, x1, y1))
+                            where.append((i, j))
+                probs = None
+                if rows:
+                    x, _ = model.preprocess(frames, rows)
+                    probs = _to_host(model.forward(x)[1])
+                id_out.append((res, where, probs))
+        return items, pose_out, id_out
+
+    def finish(batch, ev):
+        ev.synchronize()
+        for items, pose_out, id_out in batch:
+            per = [[] for _ in items]
+            if pose_out is not None:
+                allb, owner, kp, score = pose_out
+                kp, score = kp.numpy(), score.numpy()
+                for k, i in enumerate(owner):
+                    per[i].append(_sample(kp[k], score[k], allb[k]))
+            for (key, _, _, _), r in zip(items, per):
+                kpa = np.stack([np.asarray(x.pred_instances.keypoints[0], dtype=np.float64) for x in r])
+                sca = np.stack([np.asarray(x.pred_instances.keypoint_scores[0], dtype=np.float32) for x in r])
+                raw[key] = (kpa, sca)
+            for res, where, probs in id_out:
+                if probs is not None:
+                    p = probs.numpy()
+                    for (i, j), pr in zip(where, p):
+                        res[i][j] = {"pred_label": int(np.argmax(pr)), "pred_score": float(np.max(pr))}
+                for i, r in res.items():
+                    id_raw[items[i][0]] = r
+
+    pending = None
+    for bi, b0 in enumerate(range(0, len(steps), steps_per_batch)):
         by_shape = {}
         for k in steps[b0:b0 + steps_per_batch]:
-            for (c, fn, boxes, _, bb) in jobs[k]:
+            for (c, fn, bxs, _, bb) in jobs[k]:
                 img = stores[c].image(fn)
-                by_shape.setdefault(img.shape, []).append(((k, c), img, boxes, bb))
-        for shape, items in by_shape.items():
-            host = _pinned_frames((len(items),) + tuple(shape), pose_model.device_index)
-            for i, (_, img, _, _) in enumerate(items):
-                host[i].numpy()[...] = img
-            frames = host.to(dev, non_blocking=True)
-            out = inference_topdown_batch(pose_model, frames, [bb for _, _, _, bb in items])
-            for (key, _, _, _), r in zip(items, out):
-                kp = np.stack([np.asarray(x.pred_instances.keypoints[0], dtype=np.float64) for x in r])
-                sc = np.stack([np.asarray(x.pred_instances.keypoint_scores[0], dtype=np.float32) for x in r])
-                raw[key] = (kp, sc)
-            if models is not None:
-                # run_id's grouping: per (model, image size), items in step / camera order
-                groups = {}
-                for i, ((k, c), _, boxes, _) in enumerate(items):
-                    if models[c] is None:
-                        id_raw[(k, c)] = [{"pred_label": -1, "pred_score": 0.0} for _ in boxes]
-                    else:
-                        groups.setdefault(id(models[c]), (models[c], []))[1].append(i)
-                for model, idx in groups.values():
-                    sel = set(idx)
-                    preds = model.classify(frames, [items[i][2] if i in sel else [] for i in range(len(items))])
-                    for i in idx:
-                        id_raw[items[i][0]] = preds[i]
-            torch.cuda.current_stream(dev).synchronize()  # the pinned buffer is refilled next
+                by_shape.setdefault(img.shape, []).append(((k, c), img, bxs, bb))
+        batch = [launch(items, (di, bi & 1, gi)) for gi, items in enumerate(by_shape.values())]
+        ev = torch.cuda.Event()
+        ev.record(cs)
+        if pending is not None:
+            finish(*pending)
+        pending = (batch, ev)
+    if pending is not None:
+        finish(*pending)
     return raw, id_raw
 
 
