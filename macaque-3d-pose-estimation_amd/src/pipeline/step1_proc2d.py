@@ -317,7 +317,7 @@ def process_single_cam(frames, tracks, out_dir, pose_model, frame_numbers=None, 
         fnums.append(fn)
     np.save(Path(out_dir) / "frame_num.npy", np.array(fnums, dtype=np.int32))
     with open(Path(out_dir) / "alldata.json", "w") as fp:
-        json.dump(results, fp)
+        fp.write(json.dumps(results))  # same text as json.dump, C encoder
     return results
 
 
@@ -662,7 +662,7 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
         os.makedirs(out_dirs[i], exist_ok=True)
         np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))
         with open(Path(out_dirs[i]) / "alldata.json", "w") as fp:
-            json.dump(rows, fp)
+            fp.write(json.dumps(rows))  # the C encoder (json.dump streams through the Python one): same text
 
 
 def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0, pose_model=None, detector=None,
