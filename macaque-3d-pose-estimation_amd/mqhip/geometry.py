@@ -61,6 +61,15 @@ class Camera:
         return cls(matrix=d.get("matrix"), dist=d.get("distortions"), size=d.get("size"),
                    rvec=d.get("rotation", d.get("rvec")), tvec=d.get("translation", d.get("tvec")), name=d.get("name"))
 
+    def load_dict(self, d):
+        """cameras.py:201-207: reload this camera's parameters in place from a dict."""
+        self.set_camera_matrix(d['matrix'])
+        self.set_rotation(d['rotation'])
+        self.set_translation(d['translation'])
+        self.set_distortions(d['distortions'])
+        self.set_name(d['name'])
+        self.set_size(d['size'])
+
     def get_dict(self):
         """cameras.py:191-199."""
         return {"name": self.get_name(), "size": list(self.size) if self.size is not None else None,
@@ -88,8 +97,8 @@ class Camera:
         M[:3, 3] = self.tvec
         return M
 
-    # cameras.py:214-299 accessors (host-side parameters; a CameraGroup re-packs its device rows after
-    # any of the setters through CameraGroup.invalidate(), which its own setters call)
+    # cameras.py:214-299 accessors (host-side parameters; a CameraGroup re-packs its rows on every call and
+    # re-uploads them when they changed, so any setter -- on the camera or on a group -- takes effect)
     def set_camera_matrix(self, matrix):
         self.matrix = np.array(matrix, dtype=np.float64)
 
@@ -205,6 +214,31 @@ class OmnidirCamera(Camera):
                              rvec=d.get("rotation", d.get("rvec")), tvec=d.get("translation", d.get("tvec")),
                              xi=d.get("xi"), K=d.get("K"), D=d.get("D"), name=d.get("name"))
 
+    def load_dict(self, d):
+        """cameras.py:442-451."""
+        super().load_dict(d)
+        self.set_xi(d['xi'])
+        self.set_K(d['K'])
+        self.set_D(d['D'])
+
+    def get_xi(self):
+        return self.xi
+
+    def set_xi(self, xi):
+        self.xi = np.array(xi, dtype=np.float64).ravel()
+
+    def get_K(self):
+        return self.K
+
+    def set_K(self, K):
+        self.K = np.array(K, dtype=np.float64)
+
+    def get_D(self):
+        return self.D
+
+    def set_D(self, D):
+        self.D = np.array(D, dtype=np.float64).ravel()
+
     def get_dict(self):
         d = super().get_dict()
         d.update({"Omnidir": True, "xi": self.xi, "K": self.K, "D": self.D})
@@ -224,6 +258,7 @@ class CameraGroup:
         self.metadata = {} if metadata is None else metadata
         self.device = device
         self._cams_dev = None
+        self._cams_host = None
 
     # ------------------------------------------------------------------ construction
     @staticmethod
@@ -264,8 +299,9 @@ class CameraGroup:
 
     # cameras.py:1849-1889, 1994-2017: host-side parameter access; setters invalidate the device rows
     def invalidate(self):
-        """Re-pack the device camera rows on next use (after a camera's parameters were changed)."""
+        """Drop the cached device rows (cams_tensor re-packs on every call anyway)."""
         self._cams_dev = None
+        self._cams_host = None
 
     def copy(self):
         import copy as _copy
@@ -298,9 +334,10 @@ class CameraGroup:
         return np.median(errors) if median else np.mean(errors)
 
     def load_dicts(self, arr):
-        """cameras.py:1994-1996: each camera reloads its parameters from a dict of its own model."""
-        for i, d in enumerate(arr):
-            self.cameras[i] = type(self.cameras[i]).from_dict(d)
+        """cameras.py:1994-1996: each camera reloads its parameters in place (subset groups and outside
+        references to the camera objects see the new values)."""
+        for cam, d in zip(self.cameras, arr):
+            cam.load_dict(d)
         self.invalidate()
 
     def dump(self, fname):
@@ -337,9 +374,13 @@ class CameraGroup:
         return torch.device("cuda", self.device)
 
     def cams_tensor(self):
-        if self._cams_dev is None:
-            rows = np.stack([c.param_row() for c in self.cameras])
-            self._cams_dev = torch.from_numpy(rows).to(self._dev())
+        """The (C, 24) f64 device rows.  Re-packed from the cameras on every call (the reference reads the
+        parameters on every call too; C x 24 doubles is cheap) and re-uploaded only when they changed, so a
+        setter on a camera, on this group or on a group sharing the camera objects is never missed."""
+        rows = np.stack([c.param_row() for c in self.cameras])
+        if self._cams_dev is None or self._cams_host is None or rows.tobytes() != self._cams_host.tobytes():
+            self._cams_host = rows
+            self._cams_dev = torch.from_numpy(rows.copy()).to(self._dev())
         return self._cams_dev
 
     def _ctx(self):

@@ -118,10 +118,12 @@ def detect_stores(detector, stores, T, score_thr=SCORE_THR):
     return out
 
 
-def init_id_model(device: str = "cuda:0", id_variant: str = "normal", weights=None):
+def init_id_model(device: str = "cuda:0", id_variant: str = "normal", weights=None, random_weights=False):
     """step1:125-136: the ResNet-152 ID classifier of ``id_variant`` (None for an unknown variant, as
-    there).  The checkpoint is read with torch.load(weights_only=True) when it exists (mmpretrain keys
-    under 'state_dict'); otherwise seeded random weights (no checkpoint ships with the reference)."""
+    there).  The checkpoint is read with torch.load(weights_only=True) (mmpretrain keys under
+    'state_dict').  A missing checkpoint raises FileNotFoundError, as the reference's init_model does,
+    unless ``random_weights`` asks for seeded random weights (tests and bench only: no checkpoint ships
+    with the reference)."""
     from mqhip.resnet_id import ResNetIdHip, make_random_weights
     if ID_CONFIGS.get(id_variant) is None or ID_CKPTS.get(id_variant) is None:
         return None
@@ -132,8 +134,10 @@ def init_id_model(device: str = "cuda:0", id_variant: str = "normal", weights=No
             import torch
             sd = torch.load(ck, map_location="cpu", weights_only=True)
             weights = {k: v.float() for k, v in sd.get("state_dict", sd).items()}
-        else:  # one seed per variant, so a camera's variant shows in its (random-weight) predictions
+        elif random_weights:  # one seed per variant, so a camera's variant shows in its predictions
             weights = make_random_weights(152, seed={"normal": 0, "mff1y": 1}[id_variant])
+        else:
+            raise FileNotFoundError(f"ID checkpoint of variant {id_variant!r} not found: {ck}")
     return ResNetIdHip(weights, depth=152, device=dev)
 
 
@@ -386,18 +390,29 @@ def id_variant_of(store):
 def resolve_id_models(stores, id_model, device_str="cuda:0"):
     """One ID model (or None) per store.  ``id_model``: None (no classification: the stores' own ID
     predictions, if any); ``"auto"`` -- the reference's rule, ``init_id_model(device, id_variant_of(store))``
-    per camera (step1:424-427), each variant built once; a dict {variant: model}; or one model for every
-    camera."""
+    per camera (step1:424-427), each variant built once; a variant whose checkpoint is missing warns and
+    keeps the stores' own predictions (None) instead of classifying with random weights;
+    ``"random"`` -- the same per-variant models with seeded random weights (tests and bench only);
+    a dict {variant: model}; or one model for every camera."""
     if id_model is None:
         return None
     if isinstance(id_model, str):
-        if id_model != "auto":
-            raise ValueError(f"id_model must be None, 'auto', a dict or a model, not {id_model!r}")
+        if id_model not in ("auto", "random"):
+            raise ValueError(f"id_model must be None, 'auto', 'random', a dict or a model, not {id_model!r}")
         cache = {}
         for st in stores:
             v = id_variant_of(st)
-            if v not in cache:
+            if v in cache:
+                continue
+            if id_model == "random":
+                cache[v] = init_id_model(device_str, v, random_weights=True)
+                continue
+            try:
                 cache[v] = init_id_model(device_str, v)
+            except FileNotFoundError as e:
+                import warnings
+                warnings.warn(f"{e}; cameras of variant {v!r} keep their stores' ID predictions")
+                cache[v] = None
         return [cache[id_variant_of(st)] for st in stores]
     if isinstance(id_model, dict):
         return [id_model.get(id_variant_of(st)) for st in stores]

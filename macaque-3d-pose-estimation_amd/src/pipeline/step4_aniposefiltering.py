@@ -82,24 +82,47 @@ def correct_coordinate_frame(config, all_points_3d, bodyparts):
     return adj - center, M, center
 
 
+# configs/calibration_tmpl.toml of the reference: eight omnidir entries cam_0..cam_7 named "1".."8",
+# zero intrinsics / extrinsics; step4:106 loads it and overwrites the fields of the listed cameras.
+N_CALIB_TEMPLATE_CAMS = 8
+
+
+def calibration_template(n_cams=N_CALIB_TEMPLATE_CAMS):
+    """The reference's calibration template as a dict (key order = the template's)."""
+    return {f'cam_{i}': {'name': str(i + 1), 'size': [2048, 1536], 'matrix': [[0.0] * 3 for _ in range(3)],
+                         'distortions': [0.0] * 4, 'rotation': [0, 0, 0], 'translation': [0, 0, 0],
+                         'fisheye': False, 'omnidir': True} for i in range(n_cams)}
+
+
 def write_calibration(config_path, result_dir, cam_ids):
-    """step4:101-138: calibration.toml from the h5 intrinsics/extrinsics (needs h5py)."""
+    """step4:101-138: calibration.toml from the h5 intrinsics / extrinsics (needs h5py).
+
+    Same semantics as the reference: start from the 8-camera template, then per listed camera
+    matrix = mtx with its first two rows halved (the h5 intrinsics are at 2x resolution),
+    distortions / xi / D raveled, K as stored, name = the camera id; rotation / translation
+    = the raveled rvec / tvec of cam_extrinsic_optim.h5.  Template entries past len(cam_ids)
+    keep their zeros (step 4 subsets the group by name afterwards); a camera index past the
+    template raises KeyError, as the reference's ``calib['cam_'+str(i_cam)]`` does."""
     import h5py  # absent in this image; only reached when the h5 files exist
     base = os.path.dirname(config_path)
-    calib = {}
+    calib = calibration_template()
     with h5py.File(os.path.join(base, 'cam_intrinsic.h5'), 'r') as f:
         for i, k in enumerate(cam_ids):
-            mtx = f[k]['mtx'][()]
+            mtx = np.array(f[k]['mtx'][()])
             mtx[:2, :] /= 2
-            calib[f'cam_{i}'] = {
-                'name': k, 'size': [2048, 1536], 'matrix': mtx.tolist(),
-                'distortions': f[k]['dist'][()].ravel().tolist(), 'xi': f[k]['xi'][()].ravel().tolist(),
-                'K': f[k]['K'][()].tolist(), 'D': f[k]['D'][()].ravel().tolist(),
-                'fisheye': False, 'omnidir': True}
+            ent = calib[f'cam_{i}']
+            ent['matrix'] = mtx.tolist()
+            ent['distortions'] = np.asarray(f[k]['dist'][()]).ravel().tolist()
+            ent['name'] = k
+            ent['xi'] = np.asarray(f[k]['xi'][()]).ravel().tolist()
+            ent['K'] = np.asarray(f[k]['K'][()]).tolist()
+            ent['D'] = np.asarray(f[k]['D'][()]).ravel().tolist()
     with h5py.File(os.path.join(base, 'cam_extrinsic_optim.h5'), 'r') as f:
         for i, k in enumerate(cam_ids):
-            calib[f'cam_{i}']['rotation'] = f[k]['rvec'][()].ravel().tolist()
-            calib[f'cam_{i}']['translation'] = f[k]['tvec'][()].ravel().tolist()
+            ent = calib[f'cam_{i}']
+            ent['rotation'] = np.asarray(f[k]['rvec'][()]).ravel().tolist()
+            ent['translation'] = np.asarray(f[k]['tvec'][()]).ravel().tolist()
+            ent['name'] = k
     mqio.dump_toml(calib, os.path.join(result_dir, 'calibration.toml'))
 
 

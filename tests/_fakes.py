@@ -45,3 +45,58 @@ def open_stores(root):
     import glob
     from mqhip import io as mqio
     return [mqio.FrameStore(d) for d in sorted(glob.glob(f"{root}/demo.*"))]
+
+
+# ----------------------------------------------------------------------------- h5py stand-in
+class _H5Dataset:
+    """``f[cam][key][()]`` returns a fresh copy, as h5py reads a dataset into a new array."""
+
+    def __init__(self, a):
+        self._a = np.asarray(a)
+
+    def __getitem__(self, key):
+        assert key == (), "the reference reads whole datasets only (step4:118-135)"
+        return self._a.copy()
+
+
+class _H5File:
+    def __init__(self, store, path, mode="r"):
+        assert mode == "r"
+        self._groups = {k: {kk: _H5Dataset(vv) for kk, vv in v.items()} for k, v in store[str(path)].items()}
+
+    def __getitem__(self, k):
+        return self._groups[k]
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def install_fake_h5py(monkeypatch, store):
+    """Put a module named h5py into sys.modules whose File(path) serves ``store[path]`` =
+    {camera id: {dataset name: array}}; h5py itself is absent in this image."""
+    import sys
+    import types
+    mod = types.ModuleType("h5py")
+    mod.File = lambda path, mode="r": _H5File(store, path, mode)
+    monkeypatch.setitem(sys.modules, "h5py", mod)
+    return mod
+
+
+def calibration_h5_store(cams, base):
+    """The two h5 files step 4 reads (step4:107-108) for synthetic omnidir cameras, in the shapes
+    OpenCV's omnidir calibration stores: mtx at twice the image resolution (the first two rows are
+    halved on read), dist (1, 4), xi (1, 1), K (3, 3), D (1, 4), rvec / tvec (3, 1)."""
+    import os
+    intr, extr = {}, {}
+    for c in cams:
+        k = str(c["name"])
+        mtx = np.asarray(c["matrix"], dtype=np.float64).copy()
+        mtx[:2, :] *= 2
+        intr[k] = {"mtx": mtx, "dist": np.ravel(c["distortions"])[:4].reshape(1, 4),
+                   "xi": np.ravel(c["xi"]).reshape(1, 1), "K": np.asarray(c["K"], dtype=np.float64),
+                   "D": np.ravel(c["D"]).reshape(1, 4)}
+        extr[k] = {"rvec": np.ravel(c["rvec"]).reshape(3, 1), "tvec": np.ravel(c["tvec"]).reshape(3, 1)}
+    return {os.path.join(base, "cam_intrinsic.h5"): intr, os.path.join(base, "cam_extrinsic_optim.h5"): extr}

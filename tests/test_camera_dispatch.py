@@ -155,3 +155,63 @@ def test_synthetic_mixed_calibration_toml_round_trip(tmp_path):
     assert [type(c) for c in g.cameras] == [OmnidirCamera] * 2 + [Camera] * 3 + [FisheyeCamera] * 3
     for a, b in zip(g.cameras, CameraGroup.from_dicts(cams).cameras):
         np.testing.assert_array_equal(a.param_row(), b.param_row())
+
+
+def test_device_rows_follow_camera_setters_and_shared_subsets(monkeypatch):
+    """cams_tensor re-packs the rows on every call, so a setter on a camera object (not only the
+    group's setters), on an OmnidirCamera's K / xi / D, or through a parent group that shares the camera
+    objects with a subset group, is never answered with stale rows; load_dicts updates the cameras in place
+    (cameras.py:1994-1996), so subset groups see the reloaded values.  Device rows on the CPU here."""
+    import torch
+    from mqhip import synth
+    from mqhip.geometry import CameraGroup
+    g = CameraGroup.from_dicts(synth.make_cameras(3))
+    sub = g.subset_cameras([2, 0])
+    for grp in (g, sub):
+        monkeypatch.setattr(grp, "_dev", lambda: torch.device("cpu"))
+    r0 = g.cams_tensor().clone()
+    assert g.cams_tensor() is g.cams_tensor()                        # unchanged rows: no re-upload
+    g.cameras[0].set_K(np.asarray(g.cameras[0].K) * 2.0)
+    np.testing.assert_array_equal(g.cams_tensor()[0, 0].item(), 2.0 * r0[0, 0].item())
+    np.testing.assert_array_equal(sub.cams_tensor()[1].numpy(), g.cams_tensor()[0].numpy())
+    g.cameras[2].set_rotation([0.1, 0.2, 0.3])
+    np.testing.assert_array_equal(sub.cams_tensor()[0].numpy(), g.cameras[2].param_row())
+    d = synth.make_cameras(3, seed_ext=7)
+    g.load_dicts([{**c, "rotation": c["rvec"], "translation": c["tvec"]} for c in d])
+    assert sub.cameras[0] is g.cameras[2]
+    np.testing.assert_array_equal(sub.cams_tensor()[0, 19:22].numpy(), np.ravel(d[2]["tvec"]))
+    assert not np.array_equal(sub.cams_tensor().numpy(), r0[[2, 0]].numpy())
+
+
+def test_integration_stub_cam_rows_runs_and_matches_the_library_rows():
+    """INTEGRATION.md's Option-B stub packs camera rows through mqhip.geometry (no cv2).
+    Its ``_cam_rows`` is executed here on reference-style camera objects (get_dict() as cameras.py:191-199,
+    361-364, 479-485) with torch's .cuda() stubbed, and must equal synth.camera_array."""
+    import os
+    import re
+    from types import SimpleNamespace
+    from mqhip import geometry as mq
+    from mqhip import synth
+    text = open(os.path.join(os.path.dirname(__file__), "..", "INTEGRATION.md")).read()
+    block = re.search(r"```python\n(.*?)```", text, re.S).group(1)
+    src = block[block.index("def _cam_rows"):block.index("def triangulate")]
+    fake_torch = SimpleNamespace(from_numpy=lambda a: SimpleNamespace(cuda=lambda: a))
+    ns = {"np": np, "torch": fake_torch, "_mq": mq}
+    exec(src, ns)
+
+    class RefStyle:                                   # what the reference's OmnidirCamera.get_dict returns
+        def __init__(self, c):
+            self.c = c
+
+        def get_dict(self):
+            c = self.c
+            return {"name": c["name"], "size": list(c["size"]), "matrix": np.asarray(c["matrix"]).tolist(),
+                    "distortions": np.ravel(c["distortions"]).tolist(), "rotation": np.ravel(c["rvec"]).tolist(),
+                    "translation": np.ravel(c["tvec"]).tolist(), "Omnidir": True, "xi": c["xi"], "K": c["K"],
+                    "D": c["D"]}
+
+    cams = synth.make_cameras(4)
+    np.testing.assert_array_equal(ns["_cam_rows"]([RefStyle(c) for c in cams]), synth.camera_array(cams))
+    pin = synth.make_cameras_model(2, "pinhole")
+    ref = np.stack([mq.Camera.from_dict(d).param_row() for d in pin])
+    np.testing.assert_array_equal(ns["_cam_rows"]([mq.Camera.from_dict(d) for d in pin]), ref)

@@ -63,7 +63,7 @@ def single(clip, pose):
     root, raw, cfg = clip
     res = _results(root, "res_single")
     data = run_demo.proc("clip", 24, res, "cuda:0", cfg, raw, 17, n_animal=N_ANIMALS, pose_model=pose,
-                         id_model="auto")
+                         id_model="random")
     return res, data
 
 
@@ -114,7 +114,7 @@ def test_config3_world1_sharded_equals_single_process(clip, single, pose):
     from src.pipeline.step3_crossframematching import camera_ids
     root, raw, cfg = clip
     res = _results(root, "res_world1")
-    run_demo.proc("clip", 24, res, "cuda:0", cfg, raw, 17, n_animal=N_ANIMALS, pose_model=pose, id_model="auto",
+    run_demo.proc("clip", 24, res, "cuda:0", cfg, raw, 17, n_animal=N_ANIMALS, pose_model=pose, id_model="random",
                   world=1, rank=0, sharded=True)
     _assert_same_outputs(single[0], res, camera_ids(cfg))
 
@@ -160,7 +160,7 @@ def test_run_pose_id_equals_separate_passes(clip, pose):
     md0 = stores[0].get_frame_metadata()
     T = np.arange(md0["frame_time"][0], md0["frame_time"][-1], 1.0 / 24)
     _, jobs = s1.plan_jobs(stores, T)
-    ids = s1.resolve_id_models(stores, "auto", "cuda:0")
+    ids = s1.resolve_id_models(stores, "random", "cuda:0")
     steps = range(24)
     raw_a = s1.run_pose(pose, stores, jobs, steps, 8)
     id_a = s1.run_id(ids, stores, jobs, steps, 8)

@@ -319,3 +319,27 @@ def test_step4_proc_fixed_joint_lengths(tmp_path):
         _, s3, err = _oracle_scores_errors(o, kp[a], got["kp3d"][a])
         np.testing.assert_array_equal(got["kp3d_score"][a], s3)
         np.testing.assert_allclose(got["kp3d_err"][a], err, rtol=0, atol=1e-6)
+
+
+def test_step4_proc_from_h5_calibration(tmp_path, monkeypatch):
+    """step4.proc with cam_intrinsic.h5 / cam_extrinsic_optim.h5 next to config.yaml (read through a
+    stand-in h5py module; h5py is absent here) rebuilds calibration.toml from them (step4:101-138) and
+    gives the same kp3d, bit for bit, as the run on the synthetic calibration.toml of the same cameras."""
+    import shutil
+    from _fakes import calibration_h5_store, install_fake_h5py
+    from mqhip import io as mqio
+    from src.pipeline import step4_aniposefiltering as step4
+    cams, kp2d, root, cfg = _results_dir(tmp_path, A=2, F=24)
+    step4.proc("demo", root, cfg, 17, redo=True)
+    ref = mqio.load_array_pickle(os.path.join(root, "demo", "kp3d.pickle"))
+    store = calibration_h5_store(cams, os.path.dirname(cfg))
+    install_fake_h5py(monkeypatch, store)
+    for path in store:
+        open(path, "wb").close()
+    os.remove(os.path.join(root, "demo", "calibration.toml"))
+    shutil.rmtree(os.path.join(root, "demo", "kp2d_f.pickle"), ignore_errors=True)
+    step4.proc("demo", root, cfg, 17, redo=True)
+    got = mqio.load_array_pickle(os.path.join(root, "demo", "kp3d.pickle"))
+    assert os.path.exists(os.path.join(root, "demo", "calibration.toml"))
+    for k in ("kp3d", "kp3d_score", "kp3d_err"):
+        np.testing.assert_array_equal(got[k], ref[k])

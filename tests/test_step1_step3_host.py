@@ -210,3 +210,22 @@ def test_default_track_map_follows_the_track_ids_present():
     Trk, Cid = s3.known_assignment(T, 4)
     assert sorted(Trk) == [1, 2, 3, 4] and Trk[2].tolist() == [[2, 2]] and Cid[4].tolist() == [3]
     assert s3.default_track_map([[[]]], 2) == {0: 0, 1: 1}
+
+
+def test_auto_id_model_without_checkpoint_warns_and_keeps_store_ids(tmp_path, monkeypatch):
+    """"auto" never classifies with random weights.  A missing checkpoint raises in
+    init_id_model (the reference's init_model fails loudly); resolve_id_models("auto") warns and keeps
+    the stores' own ID predictions (None) for that variant; "random" is the explicit opt-in."""
+    import pytest
+    from src.pipeline import step1_proc2d as s1
+    monkeypatch.setattr(s1, "ID_CKPTS", {"normal": str(tmp_path / "missing.pth"), "mff1y": str(tmp_path / "m2.pth")})
+    with pytest.raises(FileNotFoundError):
+        s1.init_id_model("cuda:0", "normal")
+    stores = _stores(tmp_path, n_cams=2)
+    with pytest.warns(UserWarning, match="keep their stores' ID predictions"):
+        assert s1.resolve_id_models(stores, "auto") == [None, None]
+    built = []
+    monkeypatch.setattr(s1, "init_id_model", lambda dev, v, random_weights=False: built.append((v, random_weights)) or v)
+    assert s1.resolve_id_models(stores, "random") == ["normal", "normal"] and built == [("normal", True)]
+    with pytest.raises(ValueError):
+        s1.resolve_id_models(stores, "bogus")

@@ -69,7 +69,7 @@ def main():
     w = synth.confident_head(make_random_weights(cfg, seed=0, device=torch.device("cuda", local)))
     pose = PoseModelHip(cfg, w, local)
     del w
-    id_model = None if a.no_id else "auto"
+    id_model = None if a.no_id else "random"
     times = {}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
