@@ -56,8 +56,32 @@ def _all_gather(buf, world, group=None):
     return parts
 
 
+def camera_shard(n_cams: int, world: int, rank: int):
+    """The cameras whose post-process (KP_THR / EMA, alldata.json, step 3's kp2d slice) rank owns:
+    c = rank (mod world)."""
+    return list(range(rank, n_cams, world))
+
+
+def gather_cameras(part, n_cams: int, world: int, group=None, device=None):
+    """kp2d slices (A, F, C_own, J, 3) of every rank's ``camera_shard`` -> the whole (A, F, C, J, 3) on every
+    rank: ONE all-gather of fixed-size buffers (padded to the largest shard; ~2 MB for a 300-frame clip)."""
+    import numpy as np
+    per = len(camera_shard(n_cams, world, 0))
+    A, F, _, J, D = part.shape
+    buf = torch.zeros((A, F, per, J, D), dtype=torch.float64)
+    buf[:, :, :part.shape[2]] = torch.from_numpy(np.ascontiguousarray(part))
+    if device is not None:
+        buf = buf.to(device)
+    parts = _all_gather(buf, world, group)
+    out = np.zeros((A, F, n_cams, J, D))
+    for r in range(world):
+        own = camera_shard(n_cams, world, r)
+        out[:, :, own] = parts[r][:, :, :len(own)].cpu().numpy()
+    return out
+
+
 def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, steps_per_batch=8,
-                      kp_params=None, device=None, id_model=None, tracks=None):
+                      kp_params=None, device=None, id_model=None, tracks=None, cams=None, with_ids=False, timings=None):
     """BASELINE config 3: the step-1 pose slice of a clip, time steps sharded across ranks.
 
     Every rank walks the same per-camera time grid (``step1_proc2d.plan_jobs``); rank r runs the
@@ -68,7 +92,10 @@ def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, 
     is recursive in time per track, so it runs after the gather and the result equals the single-GPU
     ``process_stores`` exactly.  ``device``: where the gathered buffers live (a CUDA device for RCCL;
     None = host tensors, gloo).  ``world == 1`` needs no process group.  Returns what ``process_stores``
-    returns (per camera: rows per kept frame, frame numbers)."""
+    returns (per camera: rows per kept frame, frame numbers); with ``cams`` only for those cameras (the
+    post-process of the other cameras is left to their owning ranks, ``camera_shard``), aligned with
+    ``cams``; ``with_ids`` adds every camera's kept-frame track ids (``step1_proc2d.kept_track_ids``); ``timings``
+    (dict) receives ``gather_end``, the perf_counter at which the all-gather completed."""
     import numpy as np
     from src.pipeline import step1_proc2d as s1
     kp_params = s1.KP_PARAMS if kp_params is None else kp_params
@@ -92,15 +119,26 @@ def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, 
     if device is not None:
         buf = buf.to(device)
     parts = _all_gather(buf, world, group)
+    if timings is not None:
+        import time
+        if device is not None:
+            torch.cuda.synchronize(device)
+        timings["gather_end"] = time.perf_counter()
     allraw, allid = {}, ({} if id_model is not None else None)
+    keep = set(range(C) if cams is None else cams)
     for r in range(world):
         s, e = frame_block(n_steps, world, r)
         part = parts[r].cpu().numpy()
         for k in range(s, e):
             for (c, _, boxes, _, _) in jobs.get(k, []):
+                if c not in keep:
+                    continue
                 v = part[k - s, c, :len(boxes)]
                 kp = v[:, :J * 3].reshape(len(boxes), J, 3)
                 allraw[(k, c)] = (kp[..., :2].copy(), kp[..., 2].astype(np.float32))
                 if allid is not None:
                     allid[(k, c)] = [{"pred_label": int(lab), "pred_score": float(scr)} for lab, scr in v[:, J * 3:]]
-    return s1.assemble_rows(stores, T, plans, jobs, allraw, kp_params, allid)
+    out = s1.assemble_rows(stores, T, plans, jobs, allraw, kp_params, allid, cams=cams)
+    if with_ids:
+        return out, s1.kept_track_ids(stores, T, plans, jobs)
+    return out

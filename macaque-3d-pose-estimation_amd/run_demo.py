@@ -37,22 +37,51 @@ def proc(data_name, fps, results_dir_root, device_str, config_path, raw_data_dir
          sharded=False, gather_device=None, timings=None):
     """run_demo.py:21-30: step 1 -> (known assignment) -> step 4; returns step 4's kp3d dict (on rank 0;
     None on the other ranks of a sharded run).  ``timings``: optional dict filled with wall seconds per
-    stage."""
+    stage.
+
+    Steps 3-4 take step 1's rows in memory (the files are still written, by a background thread joined
+    before returning).  On a sharded run (``world`` > 1 or ``sharded``) rank r post-processes and writes
+    the cameras c = r (mod world) and assembles their kp2d slices; one all-gather of the slices gives
+    rank 0 step 3's array, and rank 0 alone writes kp2d.pickle and runs step 4 (Viterbi, DLT / RANSAC,
+    optim_points: tens of ms of GPU work for a 300-frame clip).  When step 1 had nothing to do (files
+    present) steps 3-4 read the files, as the reference does."""
     import time
     device = int(device_str.split(':')[1]) if ':' in device_str else 0
     t0 = time.perf_counter()
-    step1.proc(data_name, results_dir_root, raw_data_dir, device_str, fps, pose_model=pose_model, id_model=id_model,
-               world=world, rank=rank, group=group, sharded=sharded, gather_device=gather_device)
+    s1out = step1.proc(data_name, results_dir_root, raw_data_dir, device_str, fps, pose_model=pose_model,
+                       id_model=id_model, world=world, rank=rank, group=group, sharded=sharded,
+                       gather_device=gather_device, background_writes=True, timings=timings)
     t1 = time.perf_counter()
-    if rank != 0:
-        return None
-    step3.proc_known_assignment(data_name, results_dir_root, config_path, n_animal=n_animal, n_kp=n_kp,
-                                track_to_animal=track_to_animal)
-    t2 = time.perf_counter()
-    out = step4.proc(data_name, results_dir_root, config_path, n_kp, redo=True, device=device)
-    t3 = time.perf_counter()
+    try:
+        kp2d = step3.kp2d_from_step1(s1out, step3.camera_ids(config_path), n_animal=n_animal, n_kp=n_kp,
+                                     track_to_animal=track_to_animal, world=world if (world > 1 or sharded) else 1,
+                                     group=group if (world > 1 or sharded) else None,
+                                     device=gather_device if (world > 1 or sharded) else None)
+        t2 = time.perf_counter()
+        if rank != 0:
+            return None
+        result_dir = os.path.join(results_dir_root, data_name)
+        if kp2d is None:
+            if s1out is not None:
+                s1out.wait()               # the files are the input of the file path
+            kp2d = step3.proc_known_assignment(data_name, results_dir_root, config_path, n_animal=n_animal,
+                                               n_kp=n_kp, track_to_animal=track_to_animal)
+        else:
+            from mqhip import io as mqio
+            os.makedirs(result_dir, exist_ok=True)
+            mqio.dump_pickle(kp2d, os.path.join(result_dir, "kp2d.pickle"))
+        t3 = time.perf_counter()
+        out = step4.proc(data_name, results_dir_root, config_path, n_kp, redo=True, device=device, kp2d=kp2d)
+        t4 = time.perf_counter()
+    finally:
+        if s1out is not None:
+            s1out.wait()
+    t5 = time.perf_counter()
     if timings is not None:
-        timings.update(step1_s=t1 - t0, step3_s=t2 - t1, step4_s=t3 - t2)
+        timings.update(step1_s=t1 - t0, step3_s=t3 - t1, step4_s=t4 - t3, kp2d_gather_s=t2 - t1,
+                       after_step1_s=t4 - t1, files_join_s=t5 - t4)
+        if "gather_end" in timings:   # the sharded path: rank 0's timeline after the keypoint all-gather
+            timings["after_gather_s"] = t4 - timings.pop("gather_end")
     return out
 
 
@@ -61,6 +90,8 @@ def _dist_from_env(backend=None):
     "nccl" (RCCL over xGMI, one GPU per rank) unless MQ_DIST_BACKEND=gloo (host tensors: a rehearsal
     of several ranks on one GPU, MQ_SHARE_GPU=1).  MQ_DIST_FORCE=1 builds the process group also at world
     size 1 (an RCCL rehearsal of the gather on a one-GPU box; never needed for a real run)."""
+    import datetime
+
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -72,10 +103,13 @@ def _dist_from_env(backend=None):
     torch.cuda.set_device(local)
     if world == 1 and os.environ.get("MQ_DIST_FORCE") != "1":
         return 1, 0, local, None, None
+    # rank 0 runs step 4 alone after the last collective while the others wait in the closing barrier:
+    # a timeout well past any clip's step 4
+    timeout = datetime.timedelta(seconds=float(os.environ.get("MQ_DIST_TIMEOUT_S", "7200")))
     if backend == "nccl":
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
         return world, rank, local, None, torch.device("cuda", local)
-    dist.init_process_group(backend)
+    dist.init_process_group(backend, timeout=timeout)
     return world, rank, local, None, None
 
 

@@ -234,44 +234,75 @@ class KeypointSmoother:
         self.buffers.clear()
 
     def update(self, tid, frame_number, kpt_xy, kpt_score):
+        return self.update_many([tid], frame_number, np.asarray(kpt_xy)[None], np.asarray(kpt_score)[None])[0]
+
+    def update_many(self, tids, frame_number, kpt_xy, kpt_score):
+        """``update`` for the n boxes of one frame at once (n, J, 2) / (n, J) -> (n, J, 3): the same
+        element-wise float64 / float32 arithmetic, vectorised over the boxes.  Boxes sharing a track id
+        within the frame (the second one smooths against the first) take the sequential path."""
+        tids = [int(t) for t in tids]
+        if len(set(tids)) != len(tids):
+            return np.stack([self.update_many([t], frame_number, np.asarray(kpt_xy)[i:i + 1],
+                                              np.asarray(kpt_score)[i:i + 1])[0] for i, t in enumerate(tids)])
         xy = np.array(kpt_xy, dtype=np.float64, copy=True)
         sc = np.array(kpt_score, dtype=np.float32, copy=True)
         low = sc < self.p["kp_thr"]
-        xy[low, :2] = np.nan
+        xy[low] = np.nan
         sc[low] = 0.0
-        kp = np.concatenate([xy, sc.reshape(-1, 1)], axis=1)
-        buf = self.buffers.setdefault(int(tid), deque(maxlen=5))
-        buf.append((frame_number, kp.copy()))
-        if len(buf) >= 2:
-            (_, prev), (fc, cur) = buf[-2], buf[-1]
-            both = ~np.isnan(prev[:, 0]) & ~np.isnan(cur[:, 0])
-            disp = np.zeros(prev.shape[0], dtype=np.float32)
+        kp = np.concatenate([xy, sc[..., None]], axis=-1)                    # (n, J, 3)
+        hist = []
+        for i, t in enumerate(tids):
+            buf = self.buffers.setdefault(t, deque(maxlen=5))
+            if buf:
+                hist.append(i)
+        if hist:
+            prev = np.stack([self.buffers[tids[i]][-1][1] for i in hist])     # (h, J, 3) smoothed previous
+            cur = kp[hist]
+            both = ~np.isnan(prev[..., 0]) & ~np.isnan(cur[..., 0])
+            disp = np.zeros(both.shape, dtype=np.float32)
             if both.any():
-                disp[both] = np.linalg.norm(cur[both, :2] - prev[both, :2], axis=1)
+                disp[both] = np.linalg.norm(cur[both][:, :2] - prev[both][:, :2], axis=1)
             sm = (disp < self.p["disp_thr"]) & both
             a = self.p["ema_alpha"]
-            cur[sm, :2] = a * prev[sm, :2] + (1 - a) * cur[sm, :2]
-            buf[-1] = (fc, cur)
-        return buf[-1][1]
+            cur[sm, :2] = a * prev[sm][:, :2] + (1 - a) * cur[sm][:, :2]
+            kp[hist] = cur
+        for i, t in enumerate(tids):
+            self.buffers[t].append((frame_number, kp[i].copy()))
+        return kp
 
 
 def _rows(pose_results, boxes, tids, smoother, frame_number, id_preds, kp_params):
-    rows = []
-    for i, pr in enumerate(pose_results):
+    n = len(pose_results)
+    if n == 0:
+        return []
+    kps, scs = [], []
+    for pr in pose_results:
         kp = pr.pred_instances.keypoints[0]
         try:
             sc = pr.pred_instances.keypoint_scores[0]
         except AttributeError:
             sc = np.ones(kp.shape[0], dtype=np.float32)
-        sm = smoother.update(int(tids[i]), frame_number, kp, sc)
+        kps.append(np.asarray(kp, dtype=np.float64))
+        scs.append(np.asarray(sc, dtype=np.float32))
+    return _rows_arrays(np.stack(kps), np.stack(scs), boxes, tids, smoother, frame_number, id_preds, kp_params)
+
+
+def _rows_arrays(kp, sc, boxes, tids, smoother, frame_number, id_preds, kp_params):
+    """alldata rows [tid, x1, y1, x2, y2, [[x, y, s] x J], assigned_id, id_score] (step1:345-362) of the
+    n boxes of one frame from their keypoints (n, J, 2) float64 and scores (n, J) float32."""
+    n = len(kp)
+    if n == 0:
+        return []
+    sm = smoother.update_many([int(tids[i]) for i in range(n)], frame_number, kp, sc).tolist()
+    bx = np.asarray(boxes[:n], dtype=np.float64).tolist()
+    rows = []
+    for i in range(n):
         if id_preds is None:
             label, score = -1, 0.0
         else:
             label, score = int(id_preds[i]["pred_label"]), float(id_preds[i]["pred_score"])
         assigned = label if score >= kp_params["id_conf_thr"] else -1
-        x1, y1, x2, y2 = boxes[i]
-        rows.append([int(tids[i]), float(x1), float(y1), float(x2), float(y2),
-                     [[float(x), float(y), float(s)] for (x, y, s) in sm], assigned, score])
+        rows.append([int(tids[i])] + bx[i] + [sm[i], assigned, score])
     return rows
 
 
@@ -579,38 +610,57 @@ def run_pose_id(pose_model, id_model, stores, jobs, steps, steps_per_batch=8):
     return raw, id_raw
 
 
-def _as_results(kp, sc):
-    from types import SimpleNamespace
-    return [SimpleNamespace(pred_instances=SimpleNamespace(keypoints=kp[i][None], keypoint_scores=sc[i][None]))
-            for i in range(len(kp))]
-
-
-def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS, id_raw=None):
+def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS, id_raw=None, cams=None):
     """KP_THR, the recursive per-track EMA and the alldata rows (step1:300-370), per camera in time
     order, from the pose results of ``run_pose``.  Returns per camera (rows per kept frame, frame
-    numbers) after the reference's "valid frames only" filter."""
-    smoothers = [KeypointSmoother(kp_params) for _ in stores]
-    results = [[] for _ in stores]
-    fnums = [[] for _ in stores]
-    for k in range(len(T)):
-        job_of = {c: j for j in jobs.get(k, []) for c in (j[0],)}
-        for c, st in enumerate(stores):
+    numbers) after the reference's "valid frames only" filter.  ``cams``: only these cameras (the EMA
+    state is per camera, so a subset gives the same rows; ``raw`` needs entries for them only); the
+    result is then aligned with ``cams``."""
+    cams = list(range(len(stores))) if cams is None else list(cams)
+    out = []
+    for c in cams:
+        st = stores[c]
+        smoother = KeypointSmoother(kp_params)
+        results, fnums = [], []
+        for k in range(len(T)):
             fn, rep = plans[c][k]
+            job = next((j for j in jobs.get(k, ()) if j[0] == c), None)
             if rep:
-                results[c].append(results[c][-1] if results[c] else [])
-            elif c not in job_of:  # no tracks / only degenerate boxes in this frame (step1:229-265)
-                results[c].append([])
+                results.append(results[-1] if results else [])
+            elif job is None:  # no tracks / only degenerate boxes in this frame (step1:229-265)
+                results.append([])
             else:
-                _, _, boxes, tids, _ = job_of[c]
+                _, _, boxes, tids, _ = job
                 kp, sc = raw[(k, c)]
                 ids = id_raw[(k, c)] if id_raw is not None else st.id_preds_of(fn)
-                results[c].append(_rows(_as_results(kp, sc), boxes, tids, smoothers[c], fn, ids, kp_params))
-            fnums[c].append(fn)
-    out = []
-    for c, st in enumerate(stores):  # "Save valid frames only" (step1:364-370)
-        valid = set(int(x) for x in st.get_frame_metadata()["frame_number"])
-        keep = [(r, f) for r, f in zip(results[c], fnums[c]) if f in valid]
+                results.append(_rows_arrays(np.asarray(kp, dtype=np.float64), np.asarray(sc, dtype=np.float32),
+                                            boxes, tids, smoother, fn, ids, kp_params))
+            fnums.append(fn)
+        valid = set(int(x) for x in st.get_frame_metadata()["frame_number"])  # "Save valid frames only" (:364-370)
+        keep = [(r, f) for r, f in zip(results, fnums) if f in valid]
         out.append(([r for r, _ in keep], [f for _, f in keep]))
+    return out
+
+
+def kept_track_ids(stores, T, plans, jobs):
+    """Per camera, per kept frame of ``assemble_rows``, the track ids of its rows -- from the frame plan
+    alone (no pose results): what step 3's known assignment needs from the cameras a rank does not
+    assemble itself."""
+    out = []
+    for c, st in enumerate(stores):
+        ids, fnums = [], []
+        for k in range(len(T)):
+            fn, rep = plans[c][k]
+            job = next((j for j in jobs.get(k, ()) if j[0] == c), None)
+            if rep:
+                ids.append(ids[-1] if ids else [])
+            elif job is None:
+                ids.append([])
+            else:
+                ids.append([int(t) for t in job[3]])
+            fnums.append(fn)
+        valid = set(int(x) for x in st.get_frame_metadata()["frame_number"])
+        out.append([i for i, f in zip(ids, fnums) if f in valid])
     return out
 
 
@@ -627,19 +677,63 @@ def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8
     return assemble_rows(stores, T, plans, jobs, raw, kp_params, id_raw)
 
 
+class Step1Output:
+    """What step 1 computed in this call, for steps 3-4 in memory (run_demo): per processed camera (store
+    index) its alldata rows and kept frame numbers -- on a sharded rank only the cameras it owns
+    (``mqhip.shard.camera_shard``) -- and every camera's kept-frame track ids; ``wait()`` joins the
+    background writer of the alldata.json / frame_num.npy files."""
+
+    def __init__(self, names, todo, rows, fnums, ids, writer):
+        self.names = names            # camera id (results sub-directory) per store, in store order
+        self.todo = todo              # store indices processed in this call
+        self.rows = rows              # {store index: rows per kept frame}
+        self.fnums = fnums            # {store index: kept frame numbers}
+        self.ids = ids                # per store (every camera): per kept frame, the rows' track ids
+        self._writer = writer
+
+    @property
+    def complete(self):
+        return len(self.todo) == len(self.names)
+
+    def wait(self):
+        if self._writer is not None:
+            self._writer.join()
+            self._writer = None
+        err = getattr(self, "_error", None)
+        if err is not None:
+            self._error = None
+            raise err
+
+
+def _write_step1_files(out_dirs, items, into):
+    try:
+        for i, rows, fn in items:
+            os.makedirs(out_dirs[i], exist_ok=True)
+            np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))
+            with open(Path(out_dirs[i]) / "alldata.json", "w") as fp:
+                fp.write(json.dumps(rows))  # the C encoder (json.dump streams through the Python one): same text
+    except BaseException as e:  # re-raised by Step1Output.wait()
+        into._error = e
+
+
 def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None, redo=False, pose_model=None,
                         device_str="cuda:0", steps_per_batch=8, id_model=None, detector=None, world=1, rank=0,
-                        group=None, sharded=False, gather_device=None):
+                        group=None, sharded=False, gather_device=None, background_writes=False, timings=None):
     """step1_proc2d.py:389-447 with the frame stores of ``mqhip.io.FrameStore`` and the tracker
     rows they carry (or, with ``detector``, the detector -> tracker chain).  ``id_model``: see
     ``resolve_id_models`` ("auto" = the reference's per-camera variant).  Writes
-    <results_root>/<data_name>/<cam>/alldata.json and frame_num.npy.
+    <results_root>/<data_name>/<cam>/alldata.json and frame_num.npy, and returns a ``Step1Output``
+    (None when every camera was already done).
 
     Multi-GPU (BASELINE config 3; ``world`` > 1, or ``sharded`` at world 1): every rank calls this with
     its ``rank``; the clip's time steps are sharded over the ranks (``mqhip.shard.pose_clip_sharded``:
     one all-gather of the raw keypoints over ``group``, buffers on ``gather_device`` -- the rank's GPU for
-    RCCL, None for gloo) and rank 0 writes the files, which equal the single-process ones bit for bit."""
+    RCCL, None for gloo); then rank r post-processes (KP_THR / EMA) and writes the cameras
+    c = r (mod world) only.  The files equal the single-process ones bit for bit.
+    ``background_writes``: the files are written by a thread (``Step1Output.wait()`` joins it) while the
+    caller goes on with the rows in memory."""
     import glob
+    import threading
     from mqhip.io import FrameStore
     meta_paths = sorted(glob.glob(os.path.join(raw_root, f"{data_name}.*", "metadata.yaml")))
     if not meta_paths:
@@ -653,31 +747,44 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
         t_start, t_end = t0 + t_intv[0], t0 + t_intv[1]
     T = np.arange(t_start, t_end, 1.0 / fps)
     suffix = "" if t_intv is None else f".{int(t_intv[0]):04d}-{int(t_intv[1]):04d}"
-    out_dirs = [os.path.join(results_root, data_name + suffix, os.path.basename(st.filename).split(".")[-1])
-                for st in stores]
+    names = [os.path.basename(st.filename).split(".")[-1] for st in stores]
+    out_dirs = [os.path.join(results_root, data_name + suffix, n) for n in names]
     todo = [i for i, d in enumerate(out_dirs)
             if redo or not (os.path.exists(os.path.join(d, "alldata.json"))
                             and os.path.exists(os.path.join(d, "frame_num.npy")))]
     if not todo:
-        return
+        return None
     if pose_model is None:
         pose_model = init_pose_model(device=device_str)
     sel = [stores[i] for i in todo]
     tracks = None if detector is None else track_stores(detector, sel, T)
     id_models = resolve_id_models(sel, id_model, device_str)
+    ids_sel = None
     if world > 1 or sharded:
-        from mqhip.shard import pose_clip_sharded
-        res = pose_clip_sharded(pose_model, sel, T, world, rank, group=group, steps_per_batch=steps_per_batch,
-                                device=gather_device, id_model=id_models, tracks=tracks)
-        if rank != 0:
-            return
+        from mqhip.shard import camera_shard, pose_clip_sharded
+        own = camera_shard(len(sel), world, rank)
+        res, ids_sel = pose_clip_sharded(pose_model, sel, T, world, rank, group=group,
+                                         steps_per_batch=steps_per_batch, device=gather_device, id_model=id_models,
+                                         tracks=tracks, cams=own, with_ids=True, timings=timings)
+        done = [todo[j] for j in own]
     else:
         res = process_stores(pose_model, sel, T, steps_per_batch=steps_per_batch, id_model=id_models, tracks=tracks)
-    for i, (rows, fn) in zip(todo, res):
-        os.makedirs(out_dirs[i], exist_ok=True)
-        np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))
-        with open(Path(out_dirs[i]) / "alldata.json", "w") as fp:
-            fp.write(json.dumps(rows))  # the C encoder (json.dump streams through the Python one): same text
+        done = list(todo)
+    items = [(i, rows, fn) for i, (rows, fn) in zip(done, res)]
+    out = Step1Output(names, todo, {i: r for i, r, _ in items}, {i: f for i, _, f in items}, None, None)
+    if ids_sel is None:
+        from src.pipeline.step3_crossframematching import track_ids
+        ids_sel = track_ids([out.rows[i] for i in todo])
+    out.ids = [None] * len(stores)
+    for j, i in enumerate(todo):
+        out.ids[i] = ids_sel[j]
+    if background_writes:
+        out._writer = threading.Thread(target=_write_step1_files, args=(out_dirs, items, out), daemon=False)
+        out._writer.start()
+    else:
+        _write_step1_files(out_dirs, items, out)
+        out.wait()
+    return out
 
 
 def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0, pose_model=None, detector=None,
@@ -687,5 +794,5 @@ def proc(data_name, results_root, raw_root, device_str="cuda:0", fps=24.0, pose_
     reference's rule (every camera classified by the ID model of its variant, step1:424-427); None keeps
     the stores' own ID predictions (``resolve_id_models``).  Unlike the reference (which hard-codes cuda:1,
     step1:50,421) the device argument is honoured."""
-    step1_proc2d_custom(data_name, results_root, raw_root, fps=fps, pose_model=pose_model, device_str=device_str,
-                        detector=detector, id_model=id_model, **shard)
+    return step1_proc2d_custom(data_name, results_root, raw_root, fps=fps, pose_model=pose_model,
+                               device_str=device_str, detector=detector, id_model=id_model, **shard)

@@ -209,8 +209,9 @@ def reconstruct_3d(kp2d_f, cgroup, config, bodyparts=BODYPARTS, joint_len_median
     return kp3d, S, E, joint_len
 
 
-def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int = 0, verbose=False):
-    """step4_aniposefiltering.proc (step4:89)."""
+def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int = 0, verbose=False, kp2d=None):
+    """step4_aniposefiltering.proc (step4:89).  ``kp2d``: step 3's (A, F, C, J, 3) array in memory (as
+    written to kp2d.pickle) instead of reading the file back."""
     result_dir = results_dir_root + '/' + data_name
     fixed = os.path.exists(os.path.dirname(config_path) + '/joint_len.npy')
     out_name = 'kp3d_fxdJointLen.pickle' if fixed else 'kp3d.pickle'
@@ -232,7 +233,9 @@ def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int
 
     # ---- 2D filtering (step4:140-170)
     print('##### 2D filtering....', flush=True)
-    kp2d = np.asarray(mqio.load_array_pickle(result_dir + '/kp2d.pickle'), dtype=np.float64)
+    if kp2d is None:
+        kp2d = mqio.load_array_pickle(result_dir + '/kp2d.pickle')
+    kp2d = np.asarray(kp2d, dtype=np.float64)
     kp2d_f = filter_2d(kp2d, device=device)
     mqio.dump_pickle(kp2d_f, result_dir + '/kp2d_f.pickle')
 

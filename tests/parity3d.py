@@ -1,0 +1,255 @@
+"""End-to-end 2D -> 3D parity: the HIP chain against the oracle chain from identical frames and weights.
+
+Test infrastructure, shared by tests/test_gpu_parity3d.py and bench.py's parity leg.
+The scene is BASELINE config 2 per frame (8 synthetic omnidir views at 2048 x 1536, 4 individuals,
+17 joints, boxes around the projected skeletons) over ``n_frames`` consecutive frames (config 4's
+clip, sliced).  Weights: seeded random ViTPose-H with ``synth.confident_head`` (no real checkpoint is
+distributable), identical in both chains.
+
+HIP chain (the product path, reference call sites in brackets):
+  step 1 ``process_frame_multiview`` [step1_proc2d.py:294-343]: UDP crop -> ViTPose-H bf16 flip test ->
+  UDP/DARK decode -> KP_THR + recursive EMA -> alldata rows; step 3 ``create_kp2dfile`` with the known
+  track -> individual map [step3:872-915]; step 4 ``filter_2d`` (Viterbi) + ``reconstruct_3d`` (DLT ->
+  optim_points, the reference's default ``ransac = false, optim = true``) [step4:140-331].
+
+Oracle chain (oracle/, CPU restatements; the ViT forward is the fp32 PyTorch restatement run on the GPU
+with TF32 off): oracle crop (cv2 fixed-point warp) -> fp32 ViT-H flip test -> oracle decode -> oracle
+KP_THR / EMA smoother -> the same kp2d assembly -> oracle batched Viterbi -> oracle DLT -> scipy
+least_squares optim_points (ftol 1e-3, cameras.py:1116-1190) per individual.
+
+Definitions (per crop c and joint j, on the ORACLE's flip-averaged fp32 heatmap H):
+  clear   -- top-2 margin (H_max - H_second) / max|H| > 5e-2;
+  taylor  -- the oracle's DARK Newton step stays within half a heatmap cell of its argmax cell (the
+             step is ill-conditioned on near-singular Hessians of noise-like random-weight heatmaps);
+  a 3D point (individual, frame, joint) is ALL-CLEAR when every view that passes step 4's score
+  threshold in the oracle chain is clear and taylor there, and both chains keep the same views.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (ROOT, os.path.join(ROOT, "macaque-3d-pose-estimation_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+MARGIN = 5e-2          # top-2 margin of max|H| that makes a joint "clear" 
+KP_TOL_PX = 0.5        # keypoint tolerance on clear, Taylor-regime joints
+
+
+def make_scene(n_frames=1, n_views=8, n_animals=4, seed=7):
+    from mqhip import synth
+    cams = synth.make_cameras(n_views)
+    skel = synth.make_skeletons(n_animals, max(n_frames, 2), seed=seed)[:, :n_frames]
+    truth = synth.make_kp2d(cams, skel, noise_px=0.0, drop=0.0)          # (A, F, C, J, 3)
+    tracks = []
+    for f in range(n_frames):
+        boxes = synth.boxes_from_kp2d(truth[:, f].transpose(1, 0, 2, 3))   # (C, A, 4) int32
+        tracks.append([[[float(b[0]), float(b[1]), float(b[2]), float(b[3]), float(a), 0.95]
+                        for a, b in enumerate(boxes[c])] for c in range(n_views)])
+    return {"cams": cams, "skel": skel, "truth": truth, "tracks": tracks, "n_frames": n_frames,
+            "n_views": n_views, "n_animals": n_animals, "seed": seed}
+
+
+def scene_frames(scene, f):
+    from mqhip import synth
+    return synth.make_frames(scene["n_views"], scene["truth"][:, f].transpose(1, 0, 2, 3), seed=1000 + f)
+
+
+def make_weights(device="cuda", seed=11):
+    from mqhip import synth
+    from mqhip.weights import VIT_H, make_random_weights
+    return synth.confident_head(make_random_weights(VIT_H, seed=seed, device=device))
+
+
+def _kp2d_from_rows(T, n_animals):
+    from src.pipeline import step3_crossframematching as step3
+    Trk, Cid = step3.known_assignment(T, n_animals, {a: a for a in range(n_animals)})
+    with tempfile.TemporaryDirectory() as d:
+        return step3.create_kp2dfile(d, T, Trk, Cid, n_animal=n_animals)
+
+
+def hip_chain(scene, w, config):
+    """Product path: returns kp2d (A,F,C,J,3), per-frame (kp, score, argmax) of the crops, step-4 outputs."""
+    import torch
+    from mqhip.apis import PoseModelHip
+    from mqhip.geometry import CameraGroup
+    from mqhip.weights import VIT_H
+    from src.pipeline import step1_proc2d as s1
+    from src.pipeline import step4_aniposefiltering as step4
+    model = PoseModelHip(VIT_H, w, 0)
+    C, A = scene["n_views"], scene["n_animals"]
+    smoothers = [s1.KeypointSmoother() for _ in range(C)]
+    T = [[] for _ in range(C)]
+    per_frame = []
+    for f in range(scene["n_frames"]):
+        fr = torch.from_numpy(scene_frames(scene, f)).cuda()
+        rows = s1.process_frame_multiview(model, fr, scene["tracks"][f], smoothers, f)
+        for c in range(C):
+            T[c].append(rows[c])
+        # the crops' raw outputs (same batch as step 1's) for the 2D checks
+        bbs = np.concatenate([s1.expand_boxes(s1.filter_tracks(t)[0]) for t in scene["tracks"][f]])
+        owner = np.repeat(np.arange(C, dtype=np.int32), [len(s1.filter_tracks(t)[0]) for t in scene["tracks"][f]])
+        kp, sc, am = model.net.topdown(fr, torch.from_numpy(bbs).cuda(), torch.from_numpy(owner).cuda())
+        per_frame.append((kp.cpu().numpy().astype(np.float64), sc.cpu().numpy(), am.cpu().numpy(), bbs, owner))
+        del fr
+    kp2d = _kp2d_from_rows(T, A)
+    kp2d_f = step4.filter_2d(kp2d)
+    cg = CameraGroup.from_dicts(scene["cams"])
+    kp3d, S, E, _ = step4.reconstruct_3d(kp2d_f, cg, config)
+    torch.cuda.synchronize()
+    return {"kp2d": kp2d, "kp2d_f": kp2d_f, "per_frame": per_frame, "kp3d": kp3d, "S": S, "E": E}
+
+
+def oracle_chain(scene, w, config):
+    """Oracle path (see the module docstring)."""
+    import torch
+    from mqhip.weights import VIT_H
+    from oracle.crop import preprocess, topdown_crop
+    from oracle.decode import decode_batch
+    from oracle.geometry import CameraGroupOracle, optim_points
+    from oracle.postprocess import Smoother, expand_boxes, filter_tracks, frame_rows
+    from oracle.viterbi import step4_filter_batched
+    from oracle.vitpose import forward_flip_test
+    C, A, J = scene["n_views"], scene["n_animals"], 17
+    smoothers = [Smoother() for _ in range(C)]
+    T = [[] for _ in range(C)]
+    per_frame = []
+    prev = (torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    torch.backends.cudnn.allow_tf32 = False
+    try:
+        for f in range(scene["n_frames"]):
+            frames = scene_frames(scene, f)
+            crops, cs, ss, owner, boxes_all, tids_all = [], [], [], [], [], []
+            for c in range(C):
+                boxes, tids = filter_tracks(scene["tracks"][f][c])
+                bb = expand_boxes(boxes)
+                for i in range(len(bb)):
+                    c_u8, ctr, scl = topdown_crop(frames[c], bb[i])
+                    crops.append(preprocess(c_u8))
+                    cs.append(ctr)
+                    ss.append(scl)
+                    owner.append(c)
+                boxes_all.append(boxes)
+                tids_all.append(tids)
+            x = torch.from_numpy(np.stack(crops)).cuda()
+            with torch.no_grad():
+                hm = forward_flip_test(x, w, VIT_H)[0].float().cpu().numpy()
+            del x
+            cs, ss = np.stack(cs), np.stack(ss)
+            rkp, rsc, ram = decode_batch(hm, cs, ss)
+            flat = hm.reshape(hm.shape[0], J, -1)
+            top2 = np.sort(flat, axis=-1)[..., -2:]
+            clear = (top2[..., 1] - top2[..., 0]) / np.abs(flat).max(axis=-1) > MARGIN
+            # DARK step of at most half a heatmap cell (input-space cell = scale / heatmap size)
+            cell = np.stack([ram % 48 / 47.0, ram // 48 / 63.0], axis=-1) * ss[:, None] + cs[:, None] - 0.5 * ss[:, None]
+            taylor = np.abs(rkp - cell).max(axis=-1) <= 0.5 * ss.max(axis=-1)[:, None] / 63.0
+            per_frame.append((rkp, rsc, ram, clear, taylor, np.array(owner)))
+            k = 0
+            for c in range(C):
+                n = len(boxes_all[c])
+                T[c].append(frame_rows(rkp[k:k + n], rsc[k:k + n], boxes_all[c], tids_all[c], smoothers[c], f))
+                k += n
+    finally:
+        torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = prev
+    kp2d = _kp2d_from_rows(T, A)
+    kp2d_f = step4_filter_batched(kp2d)
+    tri = config["triangulation"]
+    o = CameraGroupOracle(scene["cams"])
+    kp = kp2d_f.transpose((2, 4, 0, 1, 3))                                  # (A, C, F, J, 3)
+    F = kp.shape[2]
+    kp3d = np.zeros((A, F, J, 3))
+    good_views = np.zeros((A, C, F, J), bool)
+    # the same constraint pairs step 4 reads from the config (step4:40-49)
+    from src.pipeline.step4_aniposefiltering import BODYPARTS, load_constraints
+    cons = load_constraints(config, BODYPARTS)
+    weak = load_constraints(config, BODYPARTS, "constraints_weak")
+    for a in range(A):
+        p2 = kp[a, ..., :2].copy()
+        p2[kp[a, ..., 2] < tri["score_threshold"]] = np.nan
+        good_views[a] = ~np.isnan(p2[..., 0])
+        init = o.triangulate(p2.reshape(C, -1, 2)).reshape(F, J, 3)
+        if tri["optim"] and np.sum(np.isfinite(init[..., 0])) >= 20:
+            kp3d[a] = optim_points(o, p2, init, cons, weak, scale_smooth=tri["scale_smooth"],
+                                   scale_length=tri["scale_length"], scale_length_weak=tri["scale_length_weak"],
+                                   reproj_error_threshold=tri["reproj_error_threshold"],
+                                   n_deriv_smooth=tri["n_deriv_smooth"], ftol=1e-3)[0]
+        else:
+            kp3d[a] = init
+    return {"kp2d": kp2d, "kp2d_f": kp2d_f, "per_frame": per_frame, "kp3d": kp3d, "good_views": good_views}
+
+
+def compare(scene, hip, ora, score_threshold=0.5):
+    """The parity figures (see the module docstring for the definitions)."""
+    C, A, J = scene["n_views"], scene["n_animals"], 17
+    am_eq, n_clear, n_all, dkp, n_kp = [], 0, 0, [], 0
+    clear_cj = np.zeros((A, scene["n_frames"], C, J), bool)
+    for f, (h, o) in enumerate(zip(hip["per_frame"], ora["per_frame"])):
+        kp, sc, am = h[0], h[1], h[2]
+        rkp, rsc, ram, clear, taylor, owner = o
+        n_all += clear.size
+        n_clear += int(clear.sum())
+        am_eq.append(am[clear] == ram[clear])
+        ok = clear & taylor & (sc >= 0.3) & (rsc >= 0.3)
+        n_kp += int(ok.sum())
+        if ok.any():
+            dkp.append(np.abs(kp[ok] - rkp[ok]).max(axis=-1))
+        # crop k of view owner[k] is individual (k - first crop of the view): boxes are per individual in order
+        first = {c: int(np.argmax(owner == c)) for c in range(C)}
+        for k in range(len(owner)):
+            clear_cj[k - first[owner[k]], f, owner[k]] = clear[k] & taylor[k]
+    am_eq = np.concatenate([x.ravel() for x in am_eq]) if am_eq else np.zeros(0, bool)
+    dkp = np.concatenate(dkp) if dkp else np.zeros(0)
+    # 3D: views that pass the score threshold after the Viterbi filter, per (a, f, j)
+    def views(kp2d_f):
+        kp = kp2d_f.transpose((2, 4, 0, 1, 3))                               # (A, C, F, J, 3)
+        return kp[..., 2] >= score_threshold
+    vh, vo = views(hip["kp2d_f"]), views(ora["kp2d_f"])
+    same_views = (vh == vo).all(axis=1)                                      # (A, F, J)
+    n_views = vo.sum(axis=1)
+    all_clear = same_views & (n_views >= 2) & np.all(~vo | clear_cj.transpose(0, 2, 1, 3), axis=1)
+    finite = np.isfinite(hip["kp3d"][..., 0]) & np.isfinite(ora["kp3d"][..., 0])
+    d3 = np.linalg.norm(hip["kp3d"] - ora["kp3d"], axis=-1)
+    sel = all_clear & finite
+    every = finite & (n_views >= 2)
+    q = lambda x, p: float(np.percentile(x, p)) if x.size else float("nan")
+    return {
+        "crops_joints": int(n_all),
+        "clear_fraction": n_clear / max(1, n_all),
+        "argmax_equal_on_clear": float(am_eq.mean()) if am_eq.size else float("nan"),
+        "n_clear_taylor_scored": n_kp,
+        "kp_max_abs_px": float(dkp.max()) if dkp.size else float("nan"),
+        "kp_p99_abs_px": q(dkp, 99),
+        "points": int(every.sum()),
+        "all_clear_points": int(sel.sum()),
+        "all_clear_fraction": float(sel.sum()) / max(1, int(every.sum())),
+        "kp3d_mm_all_clear_median": q(d3[sel], 50),
+        "kp3d_mm_all_clear_p99": q(d3[sel], 99),
+        "kp3d_mm_all_clear_max": float(d3[sel].max()) if sel.any() else float("nan"),
+        "kp3d_mm_every_point_median": q(d3[every], 50),
+        "kp3d_mm_every_point_p99": q(d3[every], 99),
+        "same_views_fraction": float(same_views.mean()),
+    }
+
+
+def load_config(optim=True, ransac=False):
+    from mqhip import io as mqio
+    from src.pipeline import step4_aniposefiltering as step4
+    conf = mqio.load_toml(step4.CONFIG_TMPL)
+    conf["triangulation"].update(optim=optim, ransac=ransac)
+    return conf
+
+
+def run(n_frames=1, optim=True, seed=7, weights=None):
+    """Both chains on one scene -> (figures, hip, oracle)."""
+    scene = make_scene(n_frames=n_frames, seed=seed)
+    w = make_weights() if weights is None else weights
+    config = load_config(optim=optim)
+    hip = hip_chain(scene, w, config)
+    ora = oracle_chain(scene, w, config)
+    return compare(scene, hip, ora, config["triangulation"]["score_threshold"]), hip, ora

@@ -114,9 +114,16 @@ def test_config3_world1_sharded_equals_single_process(clip, single, pose):
     from src.pipeline.step3_crossframematching import camera_ids
     root, raw, cfg = clip
     res = _results(root, "res_world1")
+    times = {}
     run_demo.proc("clip", 24, res, "cuda:0", cfg, raw, 17, n_animal=N_ANIMALS, pose_model=pose, id_model="random",
-                  world=1, rank=0, sharded=True)
+                  world=1, rank=0, sharded=True, timings=times)
     _assert_same_outputs(single[0], res, camera_ids(cfg))
+    # steps 3-4 took step 1's rows in memory: the kp2d.pickle they wrote equals step 3 run on the files
+    from mqhip import io as mqio
+    from src.pipeline import step3_crossframematching as step3
+    mem = mqio.load_array_pickle(os.path.join(res, "clip", "kp2d.pickle"))
+    np.testing.assert_array_equal(step3.proc_known_assignment("clip", res, cfg, n_animal=N_ANIMALS), mem)
+    print("config-3 world-1 sharded timings:", times)
 
 
 def _free_port():
