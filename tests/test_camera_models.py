@@ -231,3 +231,39 @@ def test_gpu_unknown_model_row_gives_nan():
     assert np.isfinite(uv[[0, 2]]).all() and np.isnan(uv[1]).all()
     und = g.undistort_points(uv.copy())
     assert np.isnan(und[1]).all() and np.isfinite(und[[0, 2]]).all()
+
+
+@pytest.mark.gpu
+def test_gpu_closed_forms_without_the_oracle():
+    """the GPU camera models against closed forms that do not go through oracle/geometry.py (so a
+    misreading of OpenCV shared by the oracle and the kernels cannot pass): zero-distortion pinhole = the
+    pinhole projection fx X/Z + cx; zero-distortion fisheye = equidistant f atan(r) / r; undistort(project(X))
+    = X / Z for distorted models; the pinhole icdist < 0 exit returns the undistorted seed ((u - cx) / fx, 0)
+    and the fisheye non-convergence sentinel is (-1e6, -1e6)."""
+    if not gpu_available():
+        pytest.skip("needs a HIP device")
+    from mqhip.geometry import CameraGroup
+    X = np.array([[100.0, -50.0, 1500.0], [0.0, 0.0, 800.0], [-300.0, 220.0, 2100.0], [1.0, 0.0, 1.0]])
+    g = CameraGroup.from_dicts([_cam_frame_dict("pinhole", np.zeros(5)), _cam_frame_dict("fisheye", np.zeros(4))])
+    uv = g.project(X)
+    f, fy, cx, cy = 1000.0, 1010.0, 1000.0, 750.0
+    np.testing.assert_allclose(uv[0, :, 0], f * X[:, 0] / X[:, 2] + cx, rtol=1e-15, atol=1e-9)
+    np.testing.assert_allclose(uv[0, :, 1], fy * X[:, 1] / X[:, 2] + cy, rtol=1e-15, atol=1e-9)
+    r = np.hypot(X[:, 0], X[:, 1]) / X[:, 2]
+    sc = np.where(r > 0, np.arctan(r) / np.where(r > 0, r, 1.0), 1.0)
+    np.testing.assert_allclose(uv[1, :, 0], f * sc * X[:, 0] / X[:, 2] + cx, rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(uv[1, 3], [f * np.pi / 4 + cx, cy], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(g.undistort_points(uv), np.broadcast_to(X[:, :2] / X[:, 2:], (2, 4, 2)), rtol=0,
+                               atol=1e-12)
+    # distorted round trips
+    gd = CameraGroup.from_dicts([_cam_frame_dict("pinhole", [-0.08, 0.02, 1e-3, -2e-3, 0.004]),
+                                 _cam_frame_dict("fisheye", [0.02, -0.004, 1e-3, -5e-4])])
+    rng = np.random.default_rng(5)
+    xy = rng.uniform(-0.3, 0.3, (64, 2))
+    Xd = np.c_[xy * 1000.0, np.full(64, 1000.0)]
+    np.testing.assert_allclose(gd.undistort_points(gd.project(Xd)), np.broadcast_to(xy, (2, 64, 2)), rtol=0, atol=1e-9)
+    # the two exit branches, by their defining values
+    ge = CameraGroup.from_dicts([_cam_frame_dict("pinhole", [-50.0, 0, 0, 0, 0]), _cam_frame_dict("fisheye", [-0.6, 0, 0, 0])])
+    und = ge.undistort_points(np.array([[[1400.0, 750.0]], [[2200.0, 750.0]]]))
+    np.testing.assert_allclose(und[0, 0], [0.4, 0.0], rtol=0, atol=1e-15)
+    np.testing.assert_array_equal(und[1, 0], [-1e6, -1e6])
