@@ -188,6 +188,38 @@ def parity_check(w, x, hm_cpu, cfg, batch):
                     f"{batch}-crop batch holding those crops, same weights"}
 
 
+def parity_3d(device, slice_frames=8):
+    """End-to-end 2D -> 3D parity of the headline path (tests/parity3d.py, the same
+    harness as tests/test_gpu_parity3d.py): the HIP chain (step 1 crop -> ViTPose-H bf16 -> decode -> KP_THR
+    / EMA, step 3 kp2d, step 4 Viterbi -> DLT [-> optim_points]) against the oracle chain (oracle crop -> fp32
+    ViT-H on the GPU, TF32 off -> oracle decode / smoother / Viterbi / DLT -> scipy optim_points) from the same
+    frames and weights: config 2 (one 8-view x 4-individual frame) and a ``slice_frames``-frame clip slice.
+    Figures per case: clear fraction, argmax agreement on clear joints, max keypoint deviation on clear
+    Taylor-regime joints, kp3d deviation (mm) on all-clear points and on every point."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import parity3d
+    out = {"tolerances": {"argmax": "bit-exact on clear joints (top-2 margin > 5e-2 max|H|)",
+                          "keypoint_px": parity3d.KP_TOL_PX,
+                          "kp3d_mm_all_clear": {"median": parity3d.KP3D_MM_MEDIAN, "p99": parity3d.KP3D_MM_P99}}}
+    w = parity3d.make_weights(device=torch_device(device))
+    for name, nf in (("config2_frame", 1), ("clip_slice", slice_frames)):
+        t0 = time.perf_counter()
+        fig, _, _ = parity3d.run(n_frames=nf, weights=w)
+        fig = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in fig.items()}
+        fig["frames"] = nf
+        fig["seconds"] = round(time.perf_counter() - t0, 1)
+        out[name] = fig
+        log(f"parity 3D {name}: {fig}")
+    del w
+    return out
+
+
+def torch_device(i):
+    import torch
+    return torch.device("cuda", i)
+
+
 def detector_cpu(reps=3):
     """Config-5 detection stage on the CPU port (oracle/swin_det.py, torch fp32): resize +
     normalise + Swin-S + FPN + RPN head convolutions of ONE 1536x2048 view, x8 views.  The RPN
@@ -754,6 +786,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_config5:
         result["config5"] = config5_gpu(local, model, frames[:, :N_VIEWS] if frames.dim() == 5 else frames, cams_dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["parity_3d_mm"] = parity_3d(local)
         result["cpu_baseline"] = cpu_baseline(cams_np)
         if "lift_config4" in result:
             result["lift_config4"]["speedup_vs_cpu_port"] = round(

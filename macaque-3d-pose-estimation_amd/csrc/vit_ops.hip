@@ -141,6 +141,51 @@ __device__ __forceinline__ int att_item(int H) {
 //                 step and a v_permlane16_swap pairs neighbouring d runs into 16-B row stores.
 constexpr int ATT2_KCH = 10;  // K image row stride in 16-B chunks (DH <= 80)
 
+// one 16-B LDS read in inline asm with an immediate offset: the QK^T loop below keeps its own ring of K
+// fragments in flight and counts them with explicit lgkmcnt waits (the compiler, left to itself at <= 128
+// VGPRs, kept one read ahead of each MFMA)
+template <int OFF>
+__device__ __forceinline__ bf16x8 att_ds_read16(unsigned addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+// K fragment of key block tb: row tb * 16 + l16 of the K image = base + tb * 16 rows * KCH * 16 B
+__device__ __forceinline__ bf16x8 att_read_kfrag(unsigned base, int tb) {
+  constexpr int R = 16 * ATT2_KCH * 16;
+  switch (tb) {
+    case 0: return att_ds_read16<0>(base);
+    case 1: return att_ds_read16<1 * R>(base);
+    case 2: return att_ds_read16<2 * R>(base);
+    case 3: return att_ds_read16<3 * R>(base);
+    case 4: return att_ds_read16<4 * R>(base);
+    case 5: return att_ds_read16<5 * R>(base);
+    case 6: return att_ds_read16<6 * R>(base);
+    case 7: return att_ds_read16<7 * R>(base);
+    case 8: return att_ds_read16<8 * R>(base);
+    case 9: return att_ds_read16<9 * R>(base);
+    case 10: return att_ds_read16<10 * R>(base);
+    default: return att_ds_read16<11 * R>(base);
+  }
+}
+template <int N>
+__device__ __forceinline__ void att_wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+// a count known after unrolling (the switch folds)
+__device__ __forceinline__ void att_wait_lgkm_n(int n) {
+  switch (n) {
+    case 0: att_wait_lgkm<0>(); break;
+    case 1: att_wait_lgkm<1>(); break;
+    case 2: att_wait_lgkm<2>(); break;
+    case 3: att_wait_lgkm<3>(); break;
+    case 4: att_wait_lgkm<4>(); break;
+    case 5: att_wait_lgkm<5>(); break;
+    case 6: att_wait_lgkm<6>(); break;
+    default: att_wait_lgkm<7>(); break;
+  }
+}
+
 template <int DH, int TT = 0>
 __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t* __restrict__ qkv,
                                                                      bf16_t* __restrict__ out, int T_rt, int D,
@@ -212,19 +257,43 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
   for (int u = 0; u < 2; ++u)
 #pragma unroll
     for (int tb = 0; tb < MAXT / 16; ++tb) S[u][tb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // one k-step's K fragments are all read before its MFMAs, so the reads overlap each other and the
-  // matrix products instead of each MFMA waiting on its own read
+  // QK^T: the NKS x ntb K fragments (t = ks * ntb + tb) stream through a ring of KR registers, KD reads in
+  // flight ahead of the MFMA that uses them (the read of fragment t + KD is issued right after MFMA t - (KR - KD),
+  // the last reader of its ring slot); each MFMA waits by a counted lgkmcnt for its own fragment only.  At the
+  // full 192 tokens the sequence is static (36 MFMAs); other token counts take the compiler-scheduled loop.
   auto qk = [&](int u) {
+    if constexpr (TT == MAXT) {
+      constexpr int NTB = MAXT / 16, NF = NKS * NTB, KD = 6, KR = 8;
+      unsigned kbase[NKS];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const int chunk = (HALF && ks == NKS - 1) ? 4 * ks + (g & 1) : 4 * ks + g;
-      bf16x8 kf[MAXT / 16];
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int chunk = (HALF && ks == NKS - 1) ? 4 * ks + (g & 1) : 4 * ks + g;
+        kbase[ks] = (unsigned)(uintptr_t)MQ_LDS_LOCAL(Kimg + l16 * (KCH * 16) + chunk * 16);
+      }
+      bf16x8 ring[KR];
 #pragma unroll
-      for (int tb = 0; tb < MAXT / 16; ++tb)
-        if (tb < ntb) kf[tb] = *reinterpret_cast<const bf16x8*>(Kimg + (tb * 16 + l16) * (KCH * 16) + chunk * 16);
+      for (int t = 0; t < KD; ++t) ring[t] = att_read_kfrag(kbase[t / NTB], t % NTB);
 #pragma unroll
-      for (int tb = 0; tb < MAXT / 16; ++tb)
-        if (tb < ntb) S[u][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[tb], qf[u][ks], S[u][tb], 0, 0, 0);
+      for (int t = 0; t < NF; ++t) {
+        // reads issued after fragment t: min(t + KD, NF) - (t + 1)
+        att_wait_lgkm_n(NF - 1 - t < KD - 1 ? NF - 1 - t : KD - 1);
+        __builtin_amdgcn_sched_barrier(0);
+        S[u][t % NTB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[t % KR], qf[u][t / NTB], S[u][t % NTB], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + KD < NF) ring[(t + KD) % KR] = att_read_kfrag(kbase[(t + KD) / NTB], (t + KD) % NTB);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int chunk = (HALF && ks == NKS - 1) ? 4 * ks + (g & 1) : 4 * ks + g;
+        bf16x8 kf[MAXT / 16];
+#pragma unroll
+        for (int tb = 0; tb < MAXT / 16; ++tb)
+          if (tb < ntb) kf[tb] = *reinterpret_cast<const bf16x8*>(Kimg + (tb * 16 + l16) * (KCH * 16) + chunk * 16);
+#pragma unroll
+        for (int tb = 0; tb < MAXT / 16; ++tb)
+          if (tb < ntb) S[u][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[tb], qf[u][ks], S[u][tb], 0, 0, 0);
+      }
     }
   };
   // softmax over the tokens of query l16: registers hold tokens tb*16 + 4 g + e.  The row max and
@@ -311,21 +380,11 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
       }
     }
   };
-  qk(0);
-  softmax(0);
-  pv(0);
-  if (has1) {
-    __builtin_amdgcn_sched_barrier(0);
-    qk(1);
-    softmax(1);
-    pv(1);
-  }
   // O^T C-layout: column = query l16, rows 4 g + e = d within the 16-block dt.  Pairs (dt, dt+1):
   // after v_permlane16_swap even groups hold d 16 dt + 4 g + 0..7, odd groups 16 (dt+1) + 4 (g-1) + 0..7.
+  // Block 0 is stored before block 1 runs, so its 20 O registers are free during block 1's QK^T ring.
   const bool odd = g & 1;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    if (u == 1 && !has1) break;
+  auto store = [&](int u) {
     const int q = (wave + u * ATT_WAVES) * 16 + l16;
     bf16_t* orow = out + (row0 + q) * D + h * DH;
     const float inv = linv[u];
@@ -351,6 +410,17 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
                                  pack_bf16x2(O[u][dt][2] * inv, O[u][dt][3] * inv));
       *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * g) = o;
     }
+  };
+  qk(0);
+  softmax(0);
+  pv(0);
+  store(0);
+  if (has1) {
+    __builtin_amdgcn_sched_barrier(0);
+    qk(1);
+    softmax(1);
+    pv(1);
+    store(1);
   }
 }
 

@@ -39,6 +39,10 @@ for _p in (ROOT, os.path.join(ROOT, "macaque-3d-pose-estimation_amd")):
 
 MARGIN = 5e-2          # top-2 margin of max|H| that makes a joint "clear" 
 KP_TOL_PX = 0.5        # keypoint tolerance on clear, Taylor-regime joints
+KP3D_MM_MEDIAN = 0.5   # kp3d tolerance on all-clear points (stated after measurement)
+KP3D_MM_P99 = 2.0
+CLEAR_MIN = 0.3        # share of joints with a clear top-2 margin (random-weight heatmaps)
+ALL_CLEAR_MIN = 4      # all-clear 3D points a case must contain
 
 
 def make_scene(n_frames=1, n_views=8, n_animals=4, seed=7):

@@ -1,0 +1,40 @@
+"""GPU: the end-to-end tolerance north_star asks for -- 3D joints of the HIP chain against the oracle chain
+from identical frames and weights (tests/parity3d.py has the two chains and the definitions).
+
+Cases: BASELINE config 2 (one frame, 8 views x 4 individuals, ViTPose-H, DLT: optim_points needs >= 20
+points per individual, step4:242-245) and a 24-frame slice of the config-4 clip through the reference's
+default step 4 (Viterbi -> DLT -> optim_points, ``ransac = false``).  Stated tolerances:
+  * argmax bit-exact on every clear joint (top-2 margin > 5e-2 max|H|);
+  * the clear fraction is at least CLEAR_MIN (random-weight heatmaps have flat tops; the figure is the
+    share of joints the bit-exact statement covers);
+  * keypoints within 0.5 px on clear, Taylor-regime joints;
+  * kp3d within KP3D_MM_MEDIAN (median) / KP3D_MM_P99 (p99) mm on all-clear points, with at least
+    ALL_CLEAR_MIN of them.
+"""
+import json
+
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+
+@pytest.fixture(scope="module")
+def weights():
+    import parity3d
+    return parity3d.make_weights()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n_frames", [1, 24])
+def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames):
+    import parity3d
+    fig, hip, ora = parity3d.run(n_frames=n_frames, weights=weights)
+    print("parity3d", json.dumps(fig))
+    assert fig["argmax_equal_on_clear"] == 1.0
+    assert fig["clear_fraction"] >= parity3d.CLEAR_MIN
+    assert fig["n_clear_taylor_scored"] > 0 and fig["kp_max_abs_px"] <= parity3d.KP_TOL_PX
+    assert fig["all_clear_points"] >= parity3d.ALL_CLEAR_MIN
+    assert fig["kp3d_mm_all_clear_median"] <= parity3d.KP3D_MM_MEDIAN
+    assert fig["kp3d_mm_all_clear_p99"] <= parity3d.KP3D_MM_P99
