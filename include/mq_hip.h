@@ -43,8 +43,9 @@ extern "C" {
  *        mq_det_topk_boxes (config-5 capturable box selection) and mq_optim_prepare (host initialisation) added.
  *   3 -- camera rows carry a model (slot 22: 0 omnidir, 1 pinhole, 2 fisheye) and a fifth distortion
  *        coefficient (slot 23); rows written for ABI 1-2 (zeros there) keep the omnidir meaning.
- *        mq_camera_undistort / mq_camera_project added (mq_omnidir_* are the same functions). */
-#define MQ_ABI_VERSION 3
+ *        mq_camera_undistort / mq_camera_project added (mq_omnidir_* are the same functions).
+ *   4 -- mq_alldata_json (host: step 1's alldata.json text from row arrays) added. */
+#define MQ_ABI_VERSION 4
 
 typedef struct mq_ctx mq_ctx;
 typedef struct mq_vitpose mq_vitpose;
@@ -376,6 +377,15 @@ int mq_attention_bf16(mq_ctx* ctx, const uint16_t* qkv, uint16_t* out, int n_img
  * summation orders).  constraints: int32 (n_strong + n_weak, 2) joint pairs.  One host thread per animal. */
 int mq_optim_prepare(const double* p3ds, int B, int F, int J, const int32_t* constraints, int n_strong, int n_weak,
                      double scale_smooth, double* x0, double* scale_smooth_full);
+
+/* step 1's alldata.json text (step1_proc2d.py:345-375: json.dump of the per-frame row lists
+ * [track id, x1, y1, x2, y2, [[x, y, score] x J], assigned id, id score]) from the rows as HOST arrays (no
+ * HIP call): nrows int32 (n_frames) rows per frame; tid / assigned int64 (n); box float64 (n, 4); kp
+ * float64 (n, J, 3); score float64 (n), n = sum(nrows).  Writes the text, byte for byte Python's
+ * json.dumps of those lists (float repr, NaN, ", " separators), into out[cap] and its length into *len;
+ * -2 if cap is too small.  Replaces the interpreter-bound json.dumps of step 1's writer. */
+int mq_alldata_json(int n_frames, const int32_t* nrows, const int64_t* tid, const double* box, const double* kp,
+                    int J, const int64_t* assigned, const double* score, char* out, int64_t cap, int64_t* len);
 
 /* CameraGroup.optim_points (cameras.py:1116-1190) and optim_points_jointlenfix (:1192-1415) for
  * B animals at once.  Replaces scipy least_squares(trf, 2-point sparse Jacobian) with

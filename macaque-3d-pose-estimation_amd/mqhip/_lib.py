@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmq_hip.so"))
-ABI_VERSION = 3  # include/mq_hip.h MQ_ABI_VERSION
+ABI_VERSION = 4  # include/mq_hip.h MQ_ABI_VERSION
 
 EXPORTED = [
     "mq_abi_version", "mq_last_error", "mq_set_tuning", "mq_get_tuning", "mq_create", "mq_destroy",
@@ -22,7 +22,7 @@ EXPORTED = [
     "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_camera_undistort", "mq_camera_project", "mq_triangulate_dlt", "mq_reproj_error",
     "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_geometry_affinity", "mq_match_svt", "mq_viterbi_filter",
     "mq_det_resize_patch", "mq_layernorm", "mq_window_attention", "mq_patch_merge_gather", "mq_upsample_add",
-    "mq_im2col3x3", "mq_conv3x3_bf16", "mq_gemm_resid_relu_bf16", "mq_id_conv_bf16", "mq_deconv_subpixel_pack", "mq_deconv_subpixel_bf16", "mq_f32_to_bf16", "mq_subsample2", "mq_nms", "mq_rpn_proposals", "mq_roi_align", "mq_rcnn_post", "mq_det_topk_boxes", "mq_optim_prepare", "mq_optim_points", "mq_attention_bf16",
+    "mq_im2col3x3", "mq_conv3x3_bf16", "mq_gemm_resid_relu_bf16", "mq_id_conv_bf16", "mq_deconv_subpixel_pack", "mq_deconv_subpixel_bf16", "mq_f32_to_bf16", "mq_subsample2", "mq_nms", "mq_rpn_proposals", "mq_roi_align", "mq_rcnn_post", "mq_det_topk_boxes", "mq_optim_prepare", "mq_optim_points", "mq_attention_bf16", "mq_alldata_json",
     "mq_id_crop_resize", "mq_id_preprocess", "mq_id_im2col", "mq_id_maxpool", "mq_id_relu_bf16", "mq_id_head",
 ]
 
@@ -42,6 +42,7 @@ f32 = C.c_float
 
 _SIGS = {
     "mq_abi_version": (i32, []),
+    "mq_alldata_json": (i32, [i32, vp, vp, vp, vp, i32, vp, vp, vp, i64, C.POINTER(i64)]),
     "mq_last_error": (C.c_char_p, []),
     "mq_set_tuning": (i32, [i32, i32]),
     "mq_get_tuning": (i32, [i32]),

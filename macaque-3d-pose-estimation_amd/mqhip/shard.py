@@ -81,7 +81,7 @@ def gather_cameras(part, n_cams: int, world: int, group=None, device=None):
 
 
 def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, steps_per_batch=8,
-                      kp_params=None, device=None, id_model=None, tracks=None, cams=None, with_ids=False, timings=None):
+                      kp_params=None, device=None, id_model=None, tracks=None, cams=None, with_ids=False, timings=None, records=False):
     """BASELINE config 3: the step-1 pose slice of a clip, time steps sharded across ranks.
 
     Every rank walks the same per-camera time grid (``step1_proc2d.plan_jobs``); rank r runs the
@@ -94,7 +94,8 @@ def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, 
     None = host tensors, gloo).  ``world == 1`` needs no process group.  Returns what ``process_stores``
     returns (per camera: rows per kept frame, frame numbers); with ``cams`` only for those cameras (the
     post-process of the other cameras is left to their owning ranks, ``camera_shard``), aligned with
-    ``cams``; ``with_ids`` adds every camera's kept-frame track ids (``step1_proc2d.kept_track_ids``); ``timings``
+    ``cams``; ``with_ids`` adds every camera's kept-frame track ids (``step1_proc2d.kept_track_ids``); ``records``
+    returns ``step1_proc2d.CameraRows`` per camera instead of row lists; ``timings``
     (dict) receives ``gather_end``, the perf_counter at which the all-gather completed."""
     import numpy as np
     from src.pipeline import step1_proc2d as s1
@@ -138,7 +139,10 @@ def pose_clip_sharded(pose_model, stores, T, world: int, rank: int, group=None, 
                 allraw[(k, c)] = (kp[..., :2].copy(), kp[..., 2].astype(np.float32))
                 if allid is not None:
                     allid[(k, c)] = [{"pred_label": int(lab), "pred_score": float(scr)} for lab, scr in v[:, J * 3:]]
-    out = s1.assemble_rows(stores, T, plans, jobs, allraw, kp_params, allid, cams=cams)
+    if records:  # step1_proc2d.CameraRows (arrays) instead of the nested row lists
+        out = s1.assemble_records(stores, T, plans, jobs, allraw, kp_params, allid, cams=cams)
+    else:
+        out = s1.assemble_rows(stores, T, plans, jobs, allraw, kp_params, allid, cams=cams)
     if with_ids:
         return out, s1.kept_track_ids(stores, T, plans, jobs)
     return out

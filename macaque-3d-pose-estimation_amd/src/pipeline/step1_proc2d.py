@@ -240,7 +240,7 @@ class KeypointSmoother:
         """``update`` for the n boxes of one frame at once (n, J, 2) / (n, J) -> (n, J, 3): the same
         element-wise float64 / float32 arithmetic, vectorised over the boxes.  Boxes sharing a track id
         within the frame (the second one smooths against the first) take the sequential path."""
-        tids = [int(t) for t in tids]
+        tids = [t if isinstance(t, tuple) else int(t) for t in tids]   # (camera, track) keys: several cameras
         if len(set(tids)) != len(tids):
             return np.stack([self.update_many([t], frame_number, np.asarray(kpt_xy)[i:i + 1],
                                               np.asarray(kpt_score)[i:i + 1])[0] for i, t in enumerate(tids)])
@@ -294,6 +294,12 @@ def _rows_arrays(kp, sc, boxes, tids, smoother, frame_number, id_preds, kp_param
     if n == 0:
         return []
     sm = smoother.update_many([int(tids[i]) for i in range(n)], frame_number, kp, sc).tolist()
+    return _rows_smoothed(sm, boxes, tids, id_preds, kp_params)
+
+
+def _rows_smoothed(sm, boxes, tids, id_preds, kp_params):
+    """alldata rows from the smoothed keypoints ``sm`` (n lists of J [x, y, s])."""
+    n = len(sm)
     bx = np.asarray(boxes[:n], dtype=np.float64).tolist()
     rows = []
     for i in range(n):
@@ -610,36 +616,131 @@ def run_pose_id(pose_model, id_model, stores, jobs, steps, steps_per_batch=8):
     return raw, id_raw
 
 
-def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS, id_raw=None, cams=None):
-    """KP_THR, the recursive per-track EMA and the alldata rows (step1:300-370), per camera in time
-    order, from the pose results of ``run_pose``.  Returns per camera (rows per kept frame, frame
-    numbers) after the reference's "valid frames only" filter.  ``cams``: only these cameras (the EMA
-    state is per camera, so a subset gives the same rows; ``raw`` needs entries for them only); the
-    result is then aligned with ``cams``."""
+class CameraRows:
+    """One camera's alldata rows (step1:345-375) as arrays: per kept frame ``nrows[f]`` rows; per row the
+    track id, the int box (as float), the smoothed keypoints (J, 3) [x, y, score], the assigned ID and its
+    score.  ``rows()`` gives the reference's nested lists (what json.dump writes), ``json_text()`` the file
+    text (libmq_hip's formatter, byte for byte json.dumps of those lists, run without the interpreter lock)."""
+
+    def __init__(self, nrows, tid, box, kp, assigned, score, fnums):
+        self.nrows = np.asarray(nrows, dtype=np.int32)
+        self.tid = np.asarray(tid, dtype=np.int64)
+        self.box = np.asarray(box, dtype=np.float64).reshape(-1, 4)
+        self.kp = np.asarray(kp, dtype=np.float64)
+        self.assigned = np.asarray(assigned, dtype=np.int64)
+        self.score = np.asarray(score, dtype=np.float64)
+        self.fnums = list(fnums)
+        self.offsets = np.concatenate([[0], np.cumsum(self.nrows)]).astype(np.int64)
+
+    def __len__(self):
+        return len(self.nrows)
+
+    def frame(self, f):
+        """(first row, row count) of kept frame f."""
+        return int(self.offsets[f]), int(self.nrows[f])
+
+    def track_ids(self):
+        t = self.tid.tolist()
+        return [t[self.offsets[f]:self.offsets[f + 1]] for f in range(len(self.nrows))]
+
+    def rows(self):
+        tid, box, kp = self.tid.tolist(), self.box.tolist(), self.kp.tolist()
+        assigned, score = self.assigned.tolist(), self.score.tolist()
+        out = []
+        for f in range(len(self.nrows)):
+            a, b = self.offsets[f], self.offsets[f + 1]
+            out.append([[tid[r]] + box[r] + [kp[r], assigned[r], score[r]] for r in range(a, b)])
+        return out
+
+    def json_text(self):
+        import ctypes
+        from mqhip import _lib
+        try:
+            lib = _lib.load()
+        except _lib.MqError:  # no library: the Python encoder (same text)
+            return json.dumps(self.rows())
+        J = self.kp.shape[1] if self.kp.ndim == 3 and len(self.kp) else 17
+        cap = len(self.tid) * ((5 + 3 * J) * 26 + 64) + len(self.nrows) * 4 + 16
+        buf = ctypes.create_string_buffer(cap)
+        n = ctypes.c_int64()
+        c = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        arrs = [np.ascontiguousarray(x) for x in (self.nrows, self.tid, self.box, self.kp, self.assigned, self.score)]
+        _lib.check(lib.mq_alldata_json(len(self.nrows), c(arrs[0]), c(arrs[1]), c(arrs[2]), c(arrs[3]), J, c(arrs[4]),
+                                       c(arrs[5]), buf, cap, ctypes.byref(n)), "mq_alldata_json")
+        return buf.raw[:n.value].decode()
+
+
+def assemble_records(stores, T, plans, jobs, raw, kp_params=KP_PARAMS, id_raw=None, cams=None):
+    """KP_THR, the recursive per-track EMA and the alldata rows (step1:300-370), per camera in time order,
+    from the pose results of ``run_pose``, as ``CameraRows`` (after the reference's "valid frames only"
+    filter).  ``cams``: only these cameras (the EMA state is per camera, so a subset gives the same rows;
+    ``raw`` needs entries for them only); the result is aligned with ``cams``."""
     cams = list(range(len(stores))) if cams is None else list(cams)
-    out = []
-    for c in cams:
-        st = stores[c]
-        smoother = KeypointSmoother(kp_params)
-        results, fnums = [], []
-        for k in range(len(T)):
+    job_at = {(k, j[0]): j for k, js in jobs.items() for j in js}
+    thr = kp_params["id_conf_thr"]
+    # one smoother for the cameras, keyed (camera, track): the cameras' EMA states are independent, and every
+    # time step's boxes of all cameras go through ONE vectorised update (same element-wise arithmetic)
+    smoother = KeypointSmoother(kp_params)
+    frames = {c: [] for c in cams}       # per camera, per time step: (tid, box, kp, assigned, score) arrays
+    fnums = {c: [] for c in cams}
+    empty = None
+    for k in range(len(T)):
+        batch = []
+        for c in cams:
             fn, rep = plans[c][k]
-            job = next((j for j in jobs.get(k, ()) if j[0] == c), None)
+            fnums[c].append(fn)
+            job = job_at.get((k, c))
             if rep:
-                results.append(results[-1] if results else [])
+                frames[c].append(frames[c][-1] if frames[c] else empty)
             elif job is None:  # no tracks / only degenerate boxes in this frame (step1:229-265)
-                results.append([])
+                frames[c].append(empty)
             else:
-                _, _, boxes, tids, _ = job
-                kp, sc = raw[(k, c)]
-                ids = id_raw[(k, c)] if id_raw is not None else st.id_preds_of(fn)
-                results.append(_rows_arrays(np.asarray(kp, dtype=np.float64), np.asarray(sc, dtype=np.float32),
-                                            boxes, tids, smoother, fn, ids, kp_params))
-            fnums.append(fn)
-        valid = set(int(x) for x in st.get_frame_metadata()["frame_number"])  # "Save valid frames only" (:364-370)
-        keep = [(r, f) for r, f in zip(results, fnums) if f in valid]
-        out.append(([r for r, _ in keep], [f for _, f in keep]))
+                batch.append((c, fn, job))
+                frames[c].append(None)
+        if not batch:
+            continue
+        keys, kps, scs = [], [], []
+        for c, fn, (_, _, boxes, tids, _) in batch:
+            kp, sc = raw[(k, c)]
+            keys += [(c, int(t)) for t in tids[:len(kp)]]
+            kps.append(np.asarray(kp, dtype=np.float64))
+            scs.append(np.asarray(sc, dtype=np.float32))
+        sm = smoother.update_many(keys, k, np.concatenate(kps), np.concatenate(scs))
+        o = 0
+        for (c, fn, (_, _, boxes, tids, _)), kp in zip(batch, kps):
+            n = len(kp)
+            ids = id_raw[(k, c)] if id_raw is not None else stores[c].id_preds_of(fn)
+            if ids is None:
+                lab, scr = np.full(n, -1, np.int64), np.zeros(n)
+            else:
+                lab = np.array([int(ids[i]["pred_label"]) for i in range(n)], dtype=np.int64)
+                scr = np.array([float(ids[i]["pred_score"]) for i in range(n)], dtype=np.float64)
+            frames[c][-1] = (np.asarray(tids[:n], dtype=np.int64), np.asarray(boxes[:n], dtype=np.float64),
+                             sm[o:o + n], np.where(scr >= thr, lab, -1), scr)
+            o += n
+    out = []
+    J = None
+    for c in cams:
+        valid = set(int(x) for x in stores[c].get_frame_metadata()["frame_number"])  # "valid frames only" (:364-370)
+        keep = [(fr, f) for fr, f in zip(frames[c], fnums[c]) if f in valid]
+        parts = [fr for fr, _ in keep if fr is not None]
+        if J is None:
+            J = next((p[2].shape[1] for ps in frames.values() for p in ps if p is not None), 17)
+        out.append(CameraRows(
+            [0 if fr is None else len(fr[0]) for fr, _ in keep],
+            np.concatenate([p[0] for p in parts]) if parts else np.zeros(0, np.int64),
+            np.concatenate([p[1] for p in parts]) if parts else np.zeros((0, 4)),
+            np.concatenate([p[2] for p in parts]) if parts else np.zeros((0, J, 3)),
+            np.concatenate([p[3] for p in parts]) if parts else np.zeros(0, np.int64),
+            np.concatenate([p[4] for p in parts]) if parts else np.zeros(0),
+            [f for _, f in keep]))
     return out
+
+
+def assemble_rows(stores, T, plans, jobs, raw, kp_params=KP_PARAMS, id_raw=None, cams=None):
+    """``assemble_records`` as the reference's nested row lists: per camera (rows per kept frame, frame
+    numbers)."""
+    return [(cr.rows(), cr.fnums) for cr in assemble_records(stores, T, plans, jobs, raw, kp_params, id_raw, cams)]
 
 
 def kept_track_ids(stores, T, plans, jobs):
@@ -664,7 +765,8 @@ def kept_track_ids(stores, T, plans, jobs):
     return out
 
 
-def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8, id_model=None, tracks=None):
+def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8, id_model=None, tracks=None,
+                   records=False):
     """Pose half of step1_proc2d_custom / process_single_cam (step1_proc2d.py:166-447) for every
     camera at once.  Per camera the reference's time-grid walk, degenerate-box filter, margin
     expansion, KP_THR and recursive EMA are kept exactly (the EMA state is per camera and runs in
@@ -674,19 +776,21 @@ def process_stores(pose_model, stores, T, kp_params=KP_PARAMS, steps_per_batch=8
     ID predictions, if any).  Returns per camera (alldata rows per kept frame, frame numbers)."""
     plans, jobs = plan_jobs(stores, T, kp_params, tracks)
     raw, id_raw = run_pose_id(pose_model, id_model, stores, jobs, range(len(T)), steps_per_batch)
+    if records:  # CameraRows per camera (arrays) instead of (rows, frame numbers)
+        return assemble_records(stores, T, plans, jobs, raw, kp_params, id_raw)
     return assemble_rows(stores, T, plans, jobs, raw, kp_params, id_raw)
 
 
 class Step1Output:
     """What step 1 computed in this call, for steps 3-4 in memory (run_demo): per processed camera (store
-    index) its alldata rows and kept frame numbers -- on a sharded rank only the cameras it owns
+    index) its alldata rows as ``CameraRows`` -- on a sharded rank only the cameras it owns
     (``mqhip.shard.camera_shard``) -- and every camera's kept-frame track ids; ``wait()`` joins the
     background writer of the alldata.json / frame_num.npy files."""
 
     def __init__(self, names, todo, rows, fnums, ids, writer):
         self.names = names            # camera id (results sub-directory) per store, in store order
         self.todo = todo              # store indices processed in this call
-        self.rows = rows              # {store index: rows per kept frame}
+        self.rows = rows              # {store index: CameraRows}
         self.fnums = fnums            # {store index: kept frame numbers}
         self.ids = ids                # per store (every camera): per kept frame, the rows' track ids
         self._writer = writer
@@ -707,11 +811,11 @@ class Step1Output:
 
 def _write_step1_files(out_dirs, items, into):
     try:
-        for i, rows, fn in items:
+        for i, rec in items:
             os.makedirs(out_dirs[i], exist_ok=True)
-            np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(fn, dtype=np.int32))
+            np.save(Path(out_dirs[i]) / "frame_num.npy", np.array(rec.fnums, dtype=np.int32))
             with open(Path(out_dirs[i]) / "alldata.json", "w") as fp:
-                fp.write(json.dumps(rows))  # the C encoder (json.dump streams through the Python one): same text
+                fp.write(rec.json_text())  # json.dumps' text of the rows, formatted natively (GIL released)
     except BaseException as e:  # re-raised by Step1Output.wait()
         into._error = e
 
@@ -765,16 +869,16 @@ def step1_proc2d_custom(data_name, results_root, raw_root, fps=24.0, t_intv=None
         own = camera_shard(len(sel), world, rank)
         res, ids_sel = pose_clip_sharded(pose_model, sel, T, world, rank, group=group,
                                          steps_per_batch=steps_per_batch, device=gather_device, id_model=id_models,
-                                         tracks=tracks, cams=own, with_ids=True, timings=timings)
+                                         tracks=tracks, cams=own, with_ids=True, timings=timings, records=True)
         done = [todo[j] for j in own]
     else:
-        res = process_stores(pose_model, sel, T, steps_per_batch=steps_per_batch, id_model=id_models, tracks=tracks)
+        res = process_stores(pose_model, sel, T, steps_per_batch=steps_per_batch, id_model=id_models, tracks=tracks,
+                             records=True)
         done = list(todo)
-    items = [(i, rows, fn) for i, (rows, fn) in zip(done, res)]
-    out = Step1Output(names, todo, {i: r for i, r, _ in items}, {i: f for i, _, f in items}, None, None)
+    items = list(zip(done, res))
+    out = Step1Output(names, todo, {i: r for i, r in items}, {i: r.fnums for i, r in items}, None, None)
     if ids_sel is None:
-        from src.pipeline.step3_crossframematching import track_ids
-        ids_sel = track_ids([out.rows[i] for i in todo])
+        ids_sel = [out.rows[i].track_ids() for i in todo]
     out.ids = [None] * len(stores)
     for j, i in enumerate(todo):
         out.ids[i] = ids_sel[j]

@@ -102,6 +102,31 @@ def kp2d_of_camera(rows_c, Trk, Cid, i_cam, n_frame, n_animal=4, n_kp=17):
     return out
 
 
+def kp2d_of_camera_rows(cr, Trk, Cid, i_cam, n_frame, n_animal=4, n_kp=17):
+    """``kp2d_of_camera`` from a camera's rows as arrays (``step1_proc2d.CameraRows``): the same selection --
+    per frame and track (Trk order) the last row carrying the track's box id -- on the arrays, bit for bit."""
+    out = np.zeros([n_animal, n_frame, n_kp, 3])
+    is_done = np.zeros([n_animal, n_frame], dtype=bool)
+    tid = cr.tid
+    for i_frame in range(min(n_frame, len(cr))):
+        a0, n = cr.frame(i_frame)
+        if n == 0:
+            continue
+        ft = tid[a0:a0 + n]
+        for k in Trk.keys():
+            i_animal = Cid[k][i_frame]
+            if i_animal < 0:
+                continue
+            trk = Trk[k][i_frame, :]
+            if np.sum(trk >= 0) == 0 or is_done[i_animal, i_frame]:
+                continue
+            hit = np.nonzero(ft == trk[i_cam])[0]
+            if len(hit):
+                out[i_animal, i_frame] = cr.kp[a0 + hit[-1]]
+                is_done[i_animal, i_frame] = True
+    return out
+
+
 def assemble_kp2d(T, Trk, Cid, n_animal=4, n_kp=17):
     """create_kp2dfile's (A, F, C, J, 3) array without writing it."""
     n_cam = len(T)
@@ -140,7 +165,7 @@ def kp2d_from_step1(s1out, cam_ids, n_animal=4, n_kp=17, track_to_animal=None, w
     part = np.zeros((n_animal, n_frame, len(own), n_kp, 3))
     for j, i in enumerate(own):
         if i in pos:
-            part[:, :, j] = kp2d_of_camera(s1out.rows[i], Trk, Cid, pos[i], n_frame, n_animal, n_kp)
+            part[:, :, j] = kp2d_of_camera_rows(s1out.rows[i], Trk, Cid, pos[i], n_frame, n_animal, n_kp)
     if len(own) == n_st and world == 1 and group is None:
         full = part
     else:

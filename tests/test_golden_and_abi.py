@@ -114,7 +114,7 @@ def test_library_exports_every_header_symbol(lib):
     for s in syms:
         assert hasattr(lib, s), f"libmq_hip.so does not export {s}"
     assert sorted(_lib.EXPORTED) == syms
-    assert lib.mq_abi_version() == 3
+    assert lib.mq_abi_version() == 4
 
 
 def test_library_is_gfx950_code_object(lib):
