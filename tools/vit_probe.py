@@ -30,6 +30,7 @@ def main():
         for name in list(_lib._SIGS):
             if not hasattr(probe, name):
                 del _lib._SIGS[name]
+        _lib.ABI_VERSION = probe.mq_abi_version()  # an A/B build may predate the current ABI
         _lib.load(os.path.abspath(args.lib))  # first load wins: every later load() returns this build
     from mqhip.pose import VitPoseHip
     from mqhip.weights import VIT_H, make_random_weights
