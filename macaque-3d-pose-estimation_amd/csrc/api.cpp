@@ -513,17 +513,27 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
   mq::GemmArgs g{};
   g = mq::GemmArgs{m->A0, m->w_patch, m->X, m->b_patch, m->pos, rows, D, KP, KP, KP, D, T};
   K_TRY(mq::gemm_bf16(g, mq::EPI_POS_F32, s));
+  // Residual updates: proj and fc2 write their branch output (bias included) as bf16 into P, and the next
+  // LayerNorm adds it to the f32 residual stream X in the same pass (x += p; X written back; y = LN(x)).
+  // The f32 read-modify-write of X in the GEMM epilogue, which every CU ran at once at the end of proj's /
+  // fc2's single tile round, is gone; the LayerNorm pass reads 31 MB more and writes X.  P lives in the QKV
+  // buffer: qkv is consumed by the attention before proj writes P, and the next qkv GEMM runs after the
+  // LayerNorm that consumed fc2's P.
+  unsigned short* P = m->QKV;
   for (int l = 0; l < m->L; ++l) {
     const Layer& ly = m->layers[l];
-    K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
+    if (l == 0)
+      K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
+    else
+      K_TRY(mq::add_layernorm_f32_bf16(m->X, P, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
     // qkv written head-major (each head's Q / K / V rows contiguous) for the attention's loads
     g = mq::GemmArgs{m->Hn, ly.wqkv, m->QKV, ly.bqkv, nullptr, rows, 3 * D, D, D, D, 3 * D, 0};
     g.head_dim = g_qkv_head_major ? D / m->H : 0;
     K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
     K_TRY(mq::attention_bf16(m->QKV, m->O, F, T, D, m->H, s, g_qkv_head_major != 0));
-    g = mq::GemmArgs{m->O, ly.wproj, m->X, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
-    K_TRY(mq::gemm_bf16(g, mq::EPI_RESID_F32, s));
-    K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
+    g = mq::GemmArgs{m->O, ly.wproj, P, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
+    K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+    K_TRY(mq::add_layernorm_f32_bf16(m->X, P, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
     g = mq::GemmArgs{m->Hn, ly.wfc1, m->G, ly.bfc1, nullptr, rows, FF, D, D, D, FF, 0};
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (m->timing) {
@@ -539,10 +549,13 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
     }
     K_TRY(mq::gemm_bf16(g, mq::EPI_GELU_BF16, s));
     if (m->timing) HIP_TRY(hipEventRecord(e1, s));
-    g = mq::GemmArgs{m->G, ly.wfc2, m->X, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0};
-    K_TRY(mq::gemm_bf16(g, mq::EPI_RESID_F32, s));
+    g = mq::GemmArgs{m->G, ly.wfc2, P, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0};
+    K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
   }
-  K_TRY(mq::layernorm_f32_bf16(m->X, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
+  if (m->L > 0)
+    K_TRY(mq::add_layernorm_f32_bf16(m->X, P, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
+  else
+    K_TRY(mq::layernorm_f32_bf16(m->X, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
   // head: deconv1 (GEMM + col2im + BN + ReLU)
   unsigned short* cols1 = m->G;
   g = mq::GemmArgs{m->Hn, m->w_dc1, cols1, nullptr, nullptr, rows, 16 * dc, D, D, D, 16 * dc, 0};

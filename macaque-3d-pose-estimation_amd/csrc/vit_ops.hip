@@ -8,25 +8,43 @@ namespace mq {
 
 // ---------------------------------------------------------------- LayerNorm
 // One wave per row: fp32 in, bf16 (GEMM operand) or f32 (residual stream) out.
-template <int MAXIT, bool OUT_F32>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ g,
-                                                         const float* __restrict__ b, void* __restrict__ yv,
-                                                         int rows, int dim, float eps) {
+// ADD: the residual update of a pre-norm block fused in front of the next LayerNorm -- x += p (p = the
+// branch output, bf16, bias included, as the proj / fc2 GEMMs write it), x written back, then normalised.
+template <int MAXIT, bool OUT_F32, bool ADD>
+__global__ __launch_bounds__(256) void layernorm_kernel(float* __restrict__ x, const bf16_t* __restrict__ p,
+                                                         const float* __restrict__ g, const float* __restrict__ b,
+                                                         void* __restrict__ yv, int rows, int dim, float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const float* xr = x + (size_t)row * dim;
+  float* xr = x + (size_t)row * dim;
   float4 v[MAXIT], gg[MAXIT], bb[MAXIT];
-  // gamma / beta are loaded together with the row (one memory round trip per wave, not two)
+  uint2 pp[MAXIT];
+  // gamma / beta (and the branch output) are loaded together with the row (one memory round trip per wave)
 #pragma unroll
   for (int it = 0; it < MAXIT; ++it) {
     const int i = it * 256 + lane * 4;
     if (i < dim) {
       v[it] = *reinterpret_cast<const float4*>(xr + i);
+      if constexpr (ADD) pp[it] = *reinterpret_cast<const uint2*>(p + (size_t)row * dim + i);
       gg[it] = *reinterpret_cast<const float4*>(g + i);
       bb[it] = *reinterpret_cast<const float4*>(b + i);
     } else {
       v[it] = gg[it] = bb[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      pp[it] = make_uint2(0u, 0u);
+    }
+  }
+  if constexpr (ADD) {
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int i = it * 256 + lane * 4;
+      if (i < dim) {
+        v[it].x += __uint_as_float(pp[it].x << 16);
+        v[it].y += __uint_as_float(pp[it].x & 0xffff0000u);
+        v[it].z += __uint_as_float(pp[it].y << 16);
+        v[it].w += __uint_as_float(pp[it].y & 0xffff0000u);
+        *reinterpret_cast<float4*>(xr + i) = v[it];
+      }
     }
   }
   float s = 0.f;
@@ -61,28 +79,33 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
 }
 
-template <bool OUT_F32>
-static int launch_layernorm(const float* x, const float* gamma, const float* beta, void* y, int rows, int dim,
-                            float eps, hipStream_t s) {
+template <bool OUT_F32, bool ADD>
+static int launch_layernorm(float* x, const bf16_t* p, const float* gamma, const float* beta, void* y, int rows,
+                            int dim, float eps, hipStream_t s) {
   if (dim % 4 || dim > 3072) return -1;
   dim3 grid((rows + 3) / 4), block(256);
   if (dim <= 512)
-    hipLaunchKernelGGL((layernorm_kernel<2, OUT_F32>), grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
+    hipLaunchKernelGGL((layernorm_kernel<2, OUT_F32, ADD>), grid, block, 0, s, x, p, gamma, beta, y, rows, dim, eps);
   else if (dim <= 1280)
-    hipLaunchKernelGGL((layernorm_kernel<5, OUT_F32>), grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
+    hipLaunchKernelGGL((layernorm_kernel<5, OUT_F32, ADD>), grid, block, 0, s, x, p, gamma, beta, y, rows, dim, eps);
   else
-    hipLaunchKernelGGL((layernorm_kernel<12, OUT_F32>), grid, block, 0, s, x, gamma, beta, y, rows, dim, eps);
+    hipLaunchKernelGGL((layernorm_kernel<12, OUT_F32, ADD>), grid, block, 0, s, x, p, gamma, beta, y, rows, dim, eps);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
                        float eps, hipStream_t s) {
-  return launch_layernorm<false>(x, gamma, beta, y, rows, dim, eps, s);
+  return launch_layernorm<false, false>(const_cast<float*>(x), nullptr, gamma, beta, y, rows, dim, eps, s);
 }
 
 int layernorm_f32_f32(const float* x, const float* gamma, const float* beta, float* y, int rows, int dim, float eps,
                       hipStream_t s) {
-  return launch_layernorm<true>(x, gamma, beta, y, rows, dim, eps, s);
+  return launch_layernorm<true, false>(const_cast<float*>(x), nullptr, gamma, beta, y, rows, dim, eps, s);
+}
+
+int add_layernorm_f32_bf16(float* x, const unsigned short* p, const float* gamma, const float* beta,
+                           unsigned short* y, int rows, int dim, float eps, hipStream_t s) {
+  return launch_layernorm<false, true>(x, reinterpret_cast<const bf16_t*>(p), gamma, beta, y, rows, dim, eps, s);
 }
 
 // ---------------------------------------------------------------- attention

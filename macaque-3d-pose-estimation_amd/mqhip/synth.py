@@ -462,6 +462,169 @@ def write_clip(root, data_name="clip", n_frames=300, n_views=8, n_animals=4, poo
     return cams, raw, res, cfg, truth[:, :n_frames]
 
 
+# ----------------------------------------------------------------------------- marker scenes
+#
+# Seeded random ViTPose weights give noise-like heatmaps: flat tops, peaks nowhere near the joints, and a
+# DARK Newton step that is ill-conditioned.  A parity test of 3D joints needs realistic heatmaps: one
+# smooth peak per joint at the joint.  No trained checkpoint is distributable, so the scene and the
+# weights are built together: every joint is painted into the frames as a two-tone Gaussian marker, and
+# ``marker_weights`` is a ViTPose whose patch embedding is a matched filter for those markers, whose
+# encoder layers are the seeded random layers with their residual branches scaled down (they still run,
+# and still perturb every token), and whose deconvolution head is a pixel shuffle of the filter outputs.
+#
+# Flip test (step1_proc2d.py:101; the second forward sees x.flip(-1), its heatmap is flipped back and
+# re-indexed by FLIP_INDICES): a marker is colour A_j left of its centre line and B_j right of it, and a
+# mirror pair (j, FLIP_INDICES[j]) swaps the two, so the flipped image of joint j's marker is exactly joint
+# FLIP_INDICES[j]'s marker -- the flip-equivariance a trained network learns.  Joint 0 (nose) is one
+# colour.  Heatmap column h matches the marker whose centre line lies between crop columns 4h+1 and 4h+2,
+# which is mirror-symmetric (4h + 1.5 + 4(47 - h) + 1.5 = 191), so both forwards peak at the same pixel.
+
+_MEAN_RGB = np.array([123.675, 116.28, 103.53])
+_STD_RGB = np.array([58.395, 57.12, 57.375])
+MARKER_AMP = 1.5           # marker colour deviation from the background, in normalised units
+MARKER_SIGMA_CROP = 4.0    # marker Gaussian sigma in crop pixels (~1 heatmap pixel)
+# Colours (unit directions in normalised RGB): mirror pair k = (joints 2k+1, 2k+2) is (A_k | B_k) and
+# (B_k | A_k) with A_k orthogonal to B_k; the nose is one colour.  Numerically packed so that no joint's
+# template reads another joint's marker -- whole, or a uniform region of either half -- above 1/2 of its own
+# perfect match (the floor: a template inside the half of its mirror partner's marker that has its own
+# colour reads exactly 1/2).
+_NOSE_DIR = np.array([-0.9318, 0.1957, 0.3057])
+_PAIR_A = np.array([[0.7961, 0.3362, -0.5031], [-0.3831, -0.4358, -0.8145], [0.2773, 0.4808, 0.8318],
+                    [-0.4393, 0.841, -0.3159], [-0.7377, -0.6037, -0.3021], [-0.6996, -0.6919, -0.1783],
+                    [0.5245, -0.1587, -0.8365], [0.4829, -0.831, 0.2763]])
+_PAIR_B = np.array([[0.2756, 0.5387, 0.7961], [0.4328, -0.8636, 0.2585], [0.4666, -0.8242, 0.3209],
+                    [-0.1284, 0.2893, 0.9486], [-0.4753, 0.7823, -0.4026], [-0.2094, -0.04, 0.977],
+                    [-0.4093, 0.8145, -0.4112], [0.8065, 0.299, -0.5101]])
+MARKER_CH_PER_JOINT = 20   # 4 row groups x (3 in-token column templates + the two halves of the 4th)
+
+
+def marker_colours():
+    """(J, 2, 3) unit colour directions (left half A, right half B) in normalised RGB per joint."""
+    unit = lambda v: v / np.linalg.norm(v, axis=-1, keepdims=True)
+    A = unit(_PAIR_A)
+    B = unit(_PAIR_B - np.sum(_PAIR_B * A, axis=-1, keepdims=True) * A)
+    out = np.zeros((17, 2, 3))
+    out[0] = [unit(_NOSE_DIR), unit(_NOSE_DIR)]
+    for j in range(1, 17):
+        k = (j - 1) // 2
+        out[j] = [A[k], B[k]] if FLIP_INDICES[j] > j else [B[k], A[k]]
+    return out
+
+
+def marker_weights(cfg, seed: int = 11, device="cpu", branch_scale: float = 1.0 / 32, gain: float = 0.6):
+    """ViTPose weights (mmpose naming, bf16-representable) that detect the markers of ``render_markers``.
+
+    * patch embedding: for joint j, row group sy (crop rows 4sy..4sy+3 of the token's 16) and heatmap column
+      sx of the token, a template reading colour A_j on four crop columns and B_j on the next four (weights
+      1/32, so a perfect match reads MARKER_AMP; eight columns, so a marker half-way between two heatmap
+      columns still reads 3/4 of a match while a uniform half of the mirror partner's marker reads 1/2); the
+      4th column's template straddles two tokens, so its A half is a channel of this token and its B half a
+      channel of the next one.  340 channels; the rest keep
+      the seeded random weights with biases of +-1 (they set the LayerNorm scale, as real features would);
+    * encoder layers: the seeded random layers with the attention and FFN output projections scaled by
+      ``branch_scale`` (a power of two, so still bf16-exact);
+    * head: deconvolution 1 adds the two halves of the 4th template (tap kx = 0 of the next token) and
+      shuffles each token's 4x4 templates into 2x2 parity channels, deconvolution 2 shuffles those into the
+      64x48 map, the 1x1 layer scales joint j's channel by ``gain``.
+    """
+    import torch
+    from .weights import make_random_weights
+    w = make_random_weights(cfg, seed=seed, device="cpu")
+    D, J, c = cfg.embed_dims, cfg.n_joints, cfg.deconv_ch
+    nsig = MARKER_CH_PER_JOINT * J
+    assert D >= nsig + 64 and c >= 4 * J and cfg.patch == 16 and cfg.patch_pad == 2, "marker weights need ViT-B/H"
+    col = marker_colours()
+    pe = torch.zeros(nsig, 3, 16, 16)
+    for j in range(J):
+        A, B = (torch.tensor(v, dtype=torch.float32) / 32.0 for v in col[j])
+        for sy in range(4):
+            base = MARKER_CH_PER_JOINT * j + 5 * sy
+            rows = slice(4 * sy, 4 * sy + 4)
+            for sx in range(3):
+                pe[base + sx, :, rows, 4 * sx:4 * sx + 4] = A[:, None, None]
+                pe[base + sx, :, rows, 4 * sx + 4:4 * sx + 8] = B[:, None, None]
+            pe[base + 3, :, rows, 12:16] = A[:, None, None]
+            pe[base + 4, :, rows, 0:4] = B[:, None, None]
+    bf = lambda t: t.to(torch.bfloat16).to(torch.float32)
+    w["backbone.patch_embed.projection.weight"][:nsig] = bf(pe)
+    bias = w["backbone.patch_embed.projection.bias"]
+    bias[:nsig] = 0.0
+    bias[nsig:] = torch.tensor([1.0, -1.0]).repeat((D - nsig + 1) // 2)[:D - nsig]
+    # top-down prior: a token centred outside the middle of the crop (where step 1's tight box sits after
+    # the margin and the x1.25 scale) pushes its templates below zero, so the same joint of a neighbouring
+    # individual inside the crop does not out-score the centred one (pos_embed is not flipped, and the prior
+    # is symmetric about the crop centre)
+    gh, gw = cfg.grid
+    xi_t = np.abs((16.0 * np.arange(gw) + 5.5 - 95.5) / 96.0)
+    eta_t = np.abs((16.0 * np.arange(gh) + 5.5 - 127.5) / 128.0)
+    pen = np.minimum(2.0, 10.0 * (np.maximum(0.0, eta_t[:, None] - 0.66) + np.maximum(0.0, xi_t[None, :] - 0.66)))
+    w["backbone.pos_embed"][..., :nsig] = bf(-torch.tensor(pen, dtype=torch.float32).reshape(1, gh * gw, 1))
+    for i in range(cfg.num_layers):
+        p = f"backbone.layers.{i}."
+        for k in ("attn.proj.weight", "attn.proj.bias", "ffn.layers.1.weight", "ffn.layers.1.bias"):
+            w[p + k] = w[p + k] * branch_scale
+    w["backbone.ln1.weight"][:nsig] = 1.0
+    w["backbone.ln1.bias"][:nsig] = 0.0
+    d1 = torch.zeros(D, c, 4, 4)
+    for j in range(J):
+        for sy in range(4):
+            base = MARKER_CH_PER_JOINT * j + 5 * sy
+            py, qy = sy // 2, sy % 2
+            for sx in range(3):
+                d1[base + sx, 4 * j + 2 * qy + sx % 2, 1 + py, 1 + sx // 2] = 1.0
+            d1[base + 3, 4 * j + 2 * qy + 1, 1 + py, 2] = 1.0      # 4th column, A half: this token (b = 1)
+            d1[base + 4, 4 * j + 2 * qy + 1, 1 + py, 0] = 1.0      # B half: the previous token's column (b = 0)
+    w["head.deconv_layers.0.weight"] = d1
+    d2 = torch.zeros(c, c, 4, 4)
+    for j in range(J):
+        for qy in range(2):
+            for qx in range(2):
+                d2[4 * j + 2 * qy + qx, j, 1 + qy, 1 + qx] = 1.0
+    w["head.deconv_layers.3.weight"] = d2
+    for bn in (1, 4):
+        w[f"head.deconv_layers.{bn}.weight"][:] = 1.0
+        w[f"head.deconv_layers.{bn}.bias"][:] = 0.0
+        w[f"head.deconv_layers.{bn}.running_mean"][:] = 0.0
+        w[f"head.deconv_layers.{bn}.running_var"][:] = 1.0
+    fin = torch.zeros(J, c, 1, 1)
+    fin[torch.arange(J), torch.arange(J)] = gain
+    w["head.final_layer.weight"] = bf(fin)
+    w["head.final_layer.bias"] = torch.zeros(J)
+    return {k: v.to(device) for k, v in w.items()}
+
+
+def render_markers(kp2d_frame, boxes, seed: int = 4, height: int = IMG_H, width: int = IMG_W, noise: int = 12):
+    """uint8 BGR frames (C, H, W, 3) for ``marker_weights``: background = the normalisation mean +-``noise``,
+    every visible joint of kp2d_frame (C, A, J, 3) a two-tone Gaussian marker (``marker_colours``, amplitude
+    MARKER_AMP) whose frame-pixel sigma maps to MARKER_SIGMA_CROP crop pixels through its individual's box
+    (boxes (C, A, 4) xyxy; expanded and aspect-fixed like step 1, x1.25 like mmpose's TopdownAffine)."""
+    rng = np.random.default_rng(seed)
+    C, A, J, _ = kp2d_frame.shape
+    col = marker_colours() * MARKER_AMP * _STD_RGB              # (J, 2, 3) RGB deviations
+    frames = np.empty((C, height, width, 3), np.uint8)
+    for c in range(C):
+        img = _MEAN_RGB[None, None, :] + rng.uniform(-noise, noise, (height, width, 3))
+        bb = expand_boxes(np.asarray(boxes[c], np.float64).reshape(-1, 4))
+        for a in range(A):
+            w_, h_ = bb[a, 2] - bb[a, 0], bb[a, 3] - bb[a, 1]
+            h_fix = max(h_, w_ / 0.75) * 1.25
+            sig = MARKER_SIGMA_CROP * h_fix / 256.0
+            R = int(np.ceil(3.0 * sig))
+            for j in range(J):
+                u, v, s = kp2d_frame[c, a, j]
+                if s <= 0 or not (R <= u < width - R - 1 and R <= v < height - R - 1):
+                    continue
+                x0, y0 = int(np.floor(u)) - R, int(np.floor(v)) - R
+                xs = np.arange(x0, x0 + 2 * R + 2) - u                 # pixel centres (integer coordinates) relative to the marker
+                ys = np.arange(y0, y0 + 2 * R + 2) - v
+                al = np.exp(-(ys[:, None] ** 2 + xs[None, :] ** 2) / (2.0 * sig * sig))[..., None]
+                dev = np.where((xs < 0.0)[None, :, None], col[j, 0], col[j, 1])
+                patch = img[y0:y0 + 2 * R + 2, x0:x0 + 2 * R + 2]
+                patch[:] = patch * (1.0 - al) + (_MEAN_RGB + dev) * al
+        frames[c] = np.clip(np.rint(img), 0, 255).astype(np.uint8)[..., ::-1]
+    return frames
+
+
 def confident_head(weights, gain=20.0, shift=0.5):
     """Random ViTPose weights with the 1x1 head scaled and shifted so that heatmap peaks score above
     step 1's KP_THR / step 4's score threshold (seeded random weights otherwise give scores near 0 and

@@ -3,8 +3,13 @@
 Test infrastructure, shared by tests/test_gpu_parity3d.py and bench.py's parity leg.
 The scene is BASELINE config 2 per frame (8 synthetic omnidir views at 2048 x 1536, 4 individuals,
 17 joints, boxes around the projected skeletons) over ``n_frames`` consecutive frames (config 4's
-clip, sliced).  Weights: seeded random ViTPose-H with ``synth.confident_head`` (no real checkpoint is
-distributable), identical in both chains.
+clip, sliced).  No trained checkpoint is distributable and seeded random weights give noise-like heatmaps
+(flat tops, peaks unrelated to the joints, an ill-conditioned DARK step), so the frames and the weights are
+built together (``synth.render_markers`` / ``synth.marker_weights``): every joint is a two-tone Gaussian
+marker, the ViTPose-H patch embedding is a matched filter for the markers, the 32 encoder layers are the
+seeded random layers with their residual branches scaled by 1/32, and the head shuffles the filter outputs
+into the 64x48 map -- one smooth, flip-consistent peak per joint, as a trained model gives.  Identical
+weights in both chains.
 
 HIP chain (the product path, reference call sites in brackets):
   step 1 ``process_frame_multiview`` [step1_proc2d.py:294-343]: UDP crop -> ViTPose-H bf16 flip test ->
@@ -60,14 +65,20 @@ def make_scene(n_frames=1, n_views=8, n_animals=4, seed=7):
 
 
 def scene_frames(scene, f):
+    """Frame f's 8 rendered views (cached in the scene: both chains read the same arrays)."""
     from mqhip import synth
-    return synth.make_frames(scene["n_views"], scene["truth"][:, f].transpose(1, 0, 2, 3), seed=1000 + f)
+    cache = scene.setdefault("_frames", {})
+    if f in cache:
+        return cache[f]
+    boxes = np.array([[t[:4] for t in scene["tracks"][f][c]] for c in range(scene["n_views"])])
+    cache[f] = synth.render_markers(scene["truth"][:, f].transpose(1, 0, 2, 3), boxes, seed=1000 + f)
+    return cache[f]
 
 
 def make_weights(device="cuda", seed=11):
     from mqhip import synth
-    from mqhip.weights import VIT_H, make_random_weights
-    return synth.confident_head(make_random_weights(VIT_H, seed=seed, device=device))
+    from mqhip.weights import VIT_H
+    return synth.marker_weights(VIT_H, seed=seed, device=device)
 
 
 def _kp2d_from_rows(T, n_animals):

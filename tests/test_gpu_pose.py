@@ -225,3 +225,62 @@ def test_vitpose_h_config2_batch_vs_fp32_oracle():
     clear = (top2[..., 1] - top2[..., 0]) / np.abs(flat).max(axis=-1) > 5e-2
     assert clear.sum() > 0
     np.testing.assert_array_equal(am.cpu().numpy()[clear], ram[clear])
+
+
+# Stated tolerances of the config-2 keypoint test below (marker scene, see mqhip/synth.py "marker scenes"):
+KP_CLEAR_MIN = 0.6       # share of (crop, joint) whose top-2 heatmap margin exceeds 5e-2 max|H|
+KP_TOL_PX = 0.5          # image-space keypoint tolerance on clear, Taylor-regime joints
+
+
+def test_vitpose_h_config2_marker_keypoints():
+    """Config 2 (8 views x 4 individuals, ViTPose-H, flip test) on a marker scene, where the heatmaps have one
+    smooth peak per joint as a trained model's do: the HIP path (crop -> bf16 forward ->
+    decode) against the oracle (crop -> fp32 forward on the GPU, TF32 off -> decode).  Stated: the clear
+    fraction is at least KP_CLEAR_MIN; the argmax is bit-exact on every clear joint; keypoints agree within
+    KP_TOL_PX on clear joints whose DARK step stays inside half a heatmap cell (step1_proc2d.py:294-312,
+    model/pose/...macaque.py:4-14)."""
+    import torch
+    from mqhip import synth
+    from mqhip.pose import VitPoseHip
+    from mqhip.weights import VIT_H
+    from oracle.decode import decode_batch
+    from oracle.vitpose import forward_flip_test
+    cams = synth.make_cameras(8)
+    kp2d = synth.make_kp2d(cams, synth.make_skeletons(4, 1, seed=7), noise_px=0.0, drop=0.0)   # (A, 1, C, J, 3)
+    tight = synth.boxes_from_kp2d(kp2d[:, 0].transpose(1, 0, 2, 3))                          # (C, A, 4)
+    frames = synth.render_markers(kp2d[:, 0].transpose(1, 0, 2, 3), tight, seed=8)
+    boxes = synth.expand_boxes(tight.reshape(-1, 4))
+    fidx = np.repeat(np.arange(8, dtype=np.int32), 4)
+    w = synth.marker_weights(VIT_H, device="cuda")
+    model = VitPoseHip(VIT_H, w, graph=True)
+    fr = torch.from_numpy(frames).cuda()
+    crops, center, scale = model.crop(fr, torch.from_numpy(boxes).cuda(), torch.from_numpy(fidx).cuda())
+    hm = model.forward(crops, flip_test=True)
+    kp, score, am, _ = model.decode(hm, center, scale)
+    torch.cuda.synchronize()
+    prev = (torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32)
+    torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
+    try:
+        with torch.no_grad():
+            ref, _, _ = forward_flip_test(crops, w, VIT_H)
+    finally:
+        torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = prev
+    got, ref = hm.float().cpu().numpy(), ref.float().cpu().numpy()
+    for i in range(32):
+        assert np.abs(got[i] - ref[i]).max() <= HM_TOL * np.abs(ref[i]).max()
+    cs, ss = center.cpu().numpy(), scale.cpu().numpy()
+    rkp, rsc, ram = decode_batch(ref, cs, ss)
+    flat = ref.reshape(32, 17, -1)
+    top2 = np.sort(flat, axis=-1)[..., -2:]
+    clear = (top2[..., 1] - top2[..., 0]) / np.abs(flat).max(axis=-1) > 5e-2
+    print(f"clear fraction {clear.mean():.3f}")
+    assert clear.mean() >= KP_CLEAR_MIN
+    np.testing.assert_array_equal(am.cpu().numpy()[clear], ram[clear])
+    # Taylor regime: the oracle's DARK step stays within half a heatmap cell of its argmax cell
+    cell = np.stack([ram % 48 / 47.0, ram // 48 / 63.0], axis=-1) * ss[:, None] + cs[:, None] - 0.5 * ss[:, None]
+    taylor = np.abs(rkp - cell).max(axis=-1) <= 0.5 * ss.max(axis=-1)[:, None] / 63.0
+    ok = clear & taylor
+    d = np.abs(kp.cpu().numpy().astype(np.float64) - rkp)[ok].max(axis=-1)
+    print(f"clear+taylor {ok.mean():.3f}; max |dkp| {d.max():.4f} px; p99 {np.percentile(d, 99):.4f} px")
+    assert ok.sum() >= 0.5 * ok.size and d.max() <= KP_TOL_PX
+    np.testing.assert_allclose(score.cpu().numpy()[clear], rsc[clear], rtol=HM_TOL)
