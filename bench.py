@@ -194,6 +194,8 @@ def parity_3d(device, slice_frames=8):
     / EMA, step 3 kp2d, step 4 Viterbi -> DLT [-> optim_points]) against the oracle chain (oracle crop -> fp32
     ViT-H on the GPU, TF32 off -> oracle decode / smoother / Viterbi / DLT -> scipy optim_points) from the same
     frames and weights: config 2 (one 8-view x 4-individual frame) and a ``slice_frames``-frame clip slice.
+    The scene is a marker scene (mqhip/synth.py: two-tone joint markers and matched-filter ViTPose-H weights,
+    so every joint has one smooth, flip-consistent heatmap peak as with a trained checkpoint).
     Figures per case: clear fraction, argmax agreement on clear joints, max keypoint deviation on clear
     Taylor-regime joints, kp3d deviation (mm) on all-clear points and on every point."""
     import sys

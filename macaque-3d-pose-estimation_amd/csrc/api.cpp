@@ -513,27 +513,28 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
   mq::GemmArgs g{};
   g = mq::GemmArgs{m->A0, m->w_patch, m->X, m->b_patch, m->pos, rows, D, KP, KP, KP, D, T};
   K_TRY(mq::gemm_bf16(g, mq::EPI_POS_F32, s));
-  // Residual updates: proj and fc2 write their branch output (bias included) as bf16 into P, and the next
-  // LayerNorm adds it to the f32 residual stream X in the same pass (x += p; X written back; y = LN(x)).
+  // Residual updates: proj and fc2 write their branch outputs (bias included) as bf16 into P1 / P2, and the
+  // LayerNorm passes add them to the f32 residual stream X: LN2 normalises x + p1 without storing it, the
+  // next block's LN1 adds p1 then p2 (the same order as two separate updates), stores X and normalises.
   // The f32 read-modify-write of X in the GEMM epilogue, which every CU ran at once at the end of proj's /
-  // fc2's single tile round, is gone; the LayerNorm pass reads 31 MB more and writes X.  P lives in the QKV
-  // buffer: qkv is consumed by the attention before proj writes P, and the next qkv GEMM runs after the
-  // LayerNorm that consumed fc2's P.
-  unsigned short* P = m->QKV;
+  // fc2's single tile round, is gone.  P1 / P2 live in the QKV buffer: the attention has read QKV before
+  // proj writes P1, and the next qkv GEMM runs after the LayerNorm that consumed both.
+  unsigned short* P1 = m->QKV;
+  unsigned short* P2 = m->QKV + (size_t)rows * D;
   for (int l = 0; l < m->L; ++l) {
     const Layer& ly = m->layers[l];
     if (l == 0)
       K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
     else
-      K_TRY(mq::add_layernorm_f32_bf16(m->X, P, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
+      K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, P2, true, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
     // qkv written head-major (each head's Q / K / V rows contiguous) for the attention's loads
     g = mq::GemmArgs{m->Hn, ly.wqkv, m->QKV, ly.bqkv, nullptr, rows, 3 * D, D, D, D, 3 * D, 0};
     g.head_dim = g_qkv_head_major ? D / m->H : 0;
     K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
     K_TRY(mq::attention_bf16(m->QKV, m->O, F, T, D, m->H, s, g_qkv_head_major != 0));
-    g = mq::GemmArgs{m->O, ly.wproj, P, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
+    g = mq::GemmArgs{m->O, ly.wproj, P1, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
     K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
-    K_TRY(mq::add_layernorm_f32_bf16(m->X, P, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
+    K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, nullptr, false, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
     g = mq::GemmArgs{m->Hn, ly.wfc1, m->G, ly.bfc1, nullptr, rows, FF, D, D, D, FF, 0};
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (m->timing) {
@@ -549,11 +550,11 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
     }
     K_TRY(mq::gemm_bf16(g, mq::EPI_GELU_BF16, s));
     if (m->timing) HIP_TRY(hipEventRecord(e1, s));
-    g = mq::GemmArgs{m->G, ly.wfc2, P, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0};
+    g = mq::GemmArgs{m->G, ly.wfc2, P2, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0};
     K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
   }
   if (m->L > 0)
-    K_TRY(mq::add_layernorm_f32_bf16(m->X, P, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
+    K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, P2, false, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
   else
     K_TRY(mq::layernorm_f32_bf16(m->X, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
   // head: deconv1 (GEMM + col2im + BN + ReLU)

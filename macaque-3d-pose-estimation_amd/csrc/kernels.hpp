@@ -71,10 +71,11 @@ int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, un
                        float eps, hipStream_t s);
 int layernorm_f32_f32(const float* x, const float* gamma, const float* beta, float* y, int rows, int dim, float eps,
                       hipStream_t s);
-// x += p (bf16 branch output), x written back, y = LayerNorm(x) in bf16 (the pre-norm residual update fused
-// into the next block's norm)
-int add_layernorm_f32_bf16(float* x, const unsigned short* p, const float* gamma, const float* beta,
-                           unsigned short* y, int rows, int dim, float eps, hipStream_t s);
+// x += p1 (+= p2) (bf16 branch outputs, added in that order), x written back when store_x, y = LayerNorm(x)
+// in bf16: the pre-norm residual updates fused into the next block's norm (p2 may be null)
+int add_layernorm_f32_bf16(float* x, const unsigned short* p1, const unsigned short* p2, bool store_x,
+                           const float* gamma, const float* beta, unsigned short* y, int rows, int dim, float eps,
+                           hipStream_t s);
 // head_major: qkv holds the head-major blocks of the qkv GEMM's head_dim output (GemmArgs::head_dim)
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s, bool head_major = false);

@@ -8,42 +8,49 @@ namespace mq {
 
 // ---------------------------------------------------------------- LayerNorm
 // One wave per row: fp32 in, bf16 (GEMM operand) or f32 (residual stream) out.
-// ADD: the residual update of a pre-norm block fused in front of the next LayerNorm -- x += p (p = the
-// branch output, bf16, bias included, as the proj / fc2 GEMMs write it), x written back, then normalised.
-template <int MAXIT, bool OUT_F32, bool ADD>
-__global__ __launch_bounds__(256) void layernorm_kernel(float* __restrict__ x, const bf16_t* __restrict__ p,
-                                                         const float* __restrict__ g, const float* __restrict__ b,
-                                                         void* __restrict__ yv, int rows, int dim, float eps) {
+// NADD > 0: the residual updates of a pre-norm block fused in front of the next LayerNorm -- x += p1 (+= p2),
+// the branch outputs in bf16 (bias included) as the proj / fc2 GEMMs write them, added in that order; the
+// updated row is written back to x when STORE_X, then normalised.
+template <int MAXIT, bool OUT_F32, int NADD, bool STORE_X>
+__global__ __launch_bounds__(256) void layernorm_kernel(float* __restrict__ x, const bf16_t* __restrict__ p1,
+                                                         const bf16_t* __restrict__ p2, const float* __restrict__ g,
+                                                         const float* __restrict__ b, void* __restrict__ yv,
+                                                         int rows, int dim, float eps) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   float* xr = x + (size_t)row * dim;
   float4 v[MAXIT], gg[MAXIT], bb[MAXIT];
-  uint2 pp[MAXIT];
-  // gamma / beta (and the branch output) are loaded together with the row (one memory round trip per wave)
+  uint2 pa[MAXIT], pb[MAXIT];
+  // gamma / beta (and the branch outputs) are loaded together with the row (one memory round trip per wave)
 #pragma unroll
   for (int it = 0; it < MAXIT; ++it) {
     const int i = it * 256 + lane * 4;
+    pa[it] = pb[it] = make_uint2(0u, 0u);
     if (i < dim) {
       v[it] = *reinterpret_cast<const float4*>(xr + i);
-      if constexpr (ADD) pp[it] = *reinterpret_cast<const uint2*>(p + (size_t)row * dim + i);
+      if constexpr (NADD >= 1) pa[it] = *reinterpret_cast<const uint2*>(p1 + (size_t)row * dim + i);
+      if constexpr (NADD >= 2) pb[it] = *reinterpret_cast<const uint2*>(p2 + (size_t)row * dim + i);
       gg[it] = *reinterpret_cast<const float4*>(g + i);
       bb[it] = *reinterpret_cast<const float4*>(b + i);
     } else {
       v[it] = gg[it] = bb[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      pp[it] = make_uint2(0u, 0u);
     }
   }
-  if constexpr (ADD) {
+  auto add_bf16x4 = [](float4& a, uint2 q) {
+    a.x += __uint_as_float(q.x << 16);
+    a.y += __uint_as_float(q.x & 0xffff0000u);
+    a.z += __uint_as_float(q.y << 16);
+    a.w += __uint_as_float(q.y & 0xffff0000u);
+  };
+  if constexpr (NADD >= 1) {
 #pragma unroll
     for (int it = 0; it < MAXIT; ++it) {
       const int i = it * 256 + lane * 4;
       if (i < dim) {
-        v[it].x += __uint_as_float(pp[it].x << 16);
-        v[it].y += __uint_as_float(pp[it].x & 0xffff0000u);
-        v[it].z += __uint_as_float(pp[it].y << 16);
-        v[it].w += __uint_as_float(pp[it].y & 0xffff0000u);
-        *reinterpret_cast<float4*>(xr + i) = v[it];
+        add_bf16x4(v[it], pa[it]);
+        if constexpr (NADD >= 2) add_bf16x4(v[it], pb[it]);
+        if constexpr (STORE_X) *reinterpret_cast<float4*>(xr + i) = v[it];
       }
     }
   }
@@ -79,33 +86,44 @@ __global__ __launch_bounds__(256) void layernorm_kernel(float* __restrict__ x, c
   }
 }
 
-template <bool OUT_F32, bool ADD>
-static int launch_layernorm(float* x, const bf16_t* p, const float* gamma, const float* beta, void* y, int rows,
-                            int dim, float eps, hipStream_t s) {
+template <bool OUT_F32, int NADD, bool STORE_X>
+static int launch_layernorm(float* x, const bf16_t* p1, const bf16_t* p2, const float* gamma, const float* beta,
+                            void* y, int rows, int dim, float eps, hipStream_t s) {
   if (dim % 4 || dim > 3072) return -1;
   dim3 grid((rows + 3) / 4), block(256);
   if (dim <= 512)
-    hipLaunchKernelGGL((layernorm_kernel<2, OUT_F32, ADD>), grid, block, 0, s, x, p, gamma, beta, y, rows, dim, eps);
+    hipLaunchKernelGGL((layernorm_kernel<2, OUT_F32, NADD, STORE_X>), grid, block, 0, s, x, p1, p2, gamma, beta, y,
+                       rows, dim, eps);
   else if (dim <= 1280)
-    hipLaunchKernelGGL((layernorm_kernel<5, OUT_F32, ADD>), grid, block, 0, s, x, p, gamma, beta, y, rows, dim, eps);
+    hipLaunchKernelGGL((layernorm_kernel<5, OUT_F32, NADD, STORE_X>), grid, block, 0, s, x, p1, p2, gamma, beta, y,
+                       rows, dim, eps);
   else
-    hipLaunchKernelGGL((layernorm_kernel<12, OUT_F32, ADD>), grid, block, 0, s, x, p, gamma, beta, y, rows, dim, eps);
+    hipLaunchKernelGGL((layernorm_kernel<12, OUT_F32, NADD, STORE_X>), grid, block, 0, s, x, p1, p2, gamma, beta, y,
+                       rows, dim, eps);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,
                        float eps, hipStream_t s) {
-  return launch_layernorm<false, false>(const_cast<float*>(x), nullptr, gamma, beta, y, rows, dim, eps, s);
+  return launch_layernorm<false, 0, false>(const_cast<float*>(x), nullptr, nullptr, gamma, beta, y, rows, dim, eps, s);
 }
 
 int layernorm_f32_f32(const float* x, const float* gamma, const float* beta, float* y, int rows, int dim, float eps,
                       hipStream_t s) {
-  return launch_layernorm<true, false>(const_cast<float*>(x), nullptr, gamma, beta, y, rows, dim, eps, s);
+  return launch_layernorm<true, 0, false>(const_cast<float*>(x), nullptr, nullptr, gamma, beta, y, rows, dim, eps, s);
 }
 
-int add_layernorm_f32_bf16(float* x, const unsigned short* p, const float* gamma, const float* beta,
-                           unsigned short* y, int rows, int dim, float eps, hipStream_t s) {
-  return launch_layernorm<false, true>(x, reinterpret_cast<const bf16_t*>(p), gamma, beta, y, rows, dim, eps, s);
+int add_layernorm_f32_bf16(float* x, const unsigned short* p1, const unsigned short* p2, bool store_x,
+                           const float* gamma, const float* beta, unsigned short* y, int rows, int dim, float eps,
+                           hipStream_t s) {
+  const bf16_t* a = reinterpret_cast<const bf16_t*>(p1);
+  const bf16_t* b = reinterpret_cast<const bf16_t*>(p2);
+  if (!p1) return -1;
+  if (b)
+    return store_x ? launch_layernorm<false, 2, true>(x, a, b, gamma, beta, y, rows, dim, eps, s)
+                   : launch_layernorm<false, 2, false>(x, a, b, gamma, beta, y, rows, dim, eps, s);
+  return store_x ? launch_layernorm<false, 1, true>(x, a, nullptr, gamma, beta, y, rows, dim, eps, s)
+                 : launch_layernorm<false, 1, false>(x, a, nullptr, gamma, beta, y, rows, dim, eps, s);
 }
 
 // ---------------------------------------------------------------- attention
