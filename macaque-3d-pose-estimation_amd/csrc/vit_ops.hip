@@ -227,6 +227,21 @@ __device__ __forceinline__ void att_wait_lgkm_n(int n) {
   }
 }
 
+// max of finite floats without the IEEE-mode operand quieting fmaxf carries (v_max3_f32 / v_max_f32 in asm)
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float bfly16_max_raw(float x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return max3_raw(__uint_as_float(p[0]), __uint_as_float(p[1]), __uint_as_float(p[1]));
+}
+__device__ __forceinline__ float bfly32_max_raw(float x) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return max3_raw(__uint_as_float(p[0]), __uint_as_float(p[1]), __uint_as_float(p[1]));
+}
+
 template <int DH, int TT = 0>
 __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t* __restrict__ qkv,
                                                                      bf16_t* __restrict__ out, int T_rt, int D,
@@ -342,22 +357,23 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
   bf16x8 P[2][MAXT / 32];
   float linv[2];
   auto softmax = [&](int u) {
-    // row max: four independent chains
+    // row max: four independent chains of v_max3_f32 in inline asm (fmaxf on MFMA results made the compiler
+    // quieten every operand first -- one extra v_max_f32 per score in IEEE mode; the scores are finite)
     float m4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
     for (int tb = 0; tb + 1 < MAXT / 16; tb += 2)
       if (tb + 1 < ntb) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m4[e] = fmaxf(m4[e], fmaxf(S[u][tb][e], S[u][tb + 1][e]));
+        for (int e = 0; e < 4; ++e) m4[e] = max3_raw(m4[e], S[u][tb][e], S[u][tb + 1][e]);
       } else if (tb < ntb) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m4[e] = fmaxf(m4[e], S[u][tb][e]);
+        for (int e = 0; e < 4; ++e) m4[e] = max3_raw(m4[e], S[u][tb][e], S[u][tb][e]);
       }
-    float m = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+    float m = max3_raw(max3_raw(m4[0], m4[1], m4[2]), m4[3], m4[3]);
     // the query's other tokens live in lane groups g ^ 1, g ^ 2: butterflies by permlane swaps (VALU,
     // no LDS round trip as with ds_bpermute)
-    m = bfly16_max(m);
-    m = bfly32_max(m);
+    m = bfly16_max_raw(m);
+    m = bfly32_max_raw(m);
     const float mbu = m * scale_log2;
     // exponent arguments (one packed fma per pair) and the running sums on float pairs
     const f32x2 sc2 = {scale_log2, scale_log2}, mb2 = {-mbu, -mbu};
