@@ -27,7 +27,7 @@ Definitions (per crop c and joint j, on the ORACLE's flip-averaged fp32 heatmap 
   taylor  -- the oracle's DARK Newton step stays within half a heatmap cell of its argmax cell (the
              step is ill-conditioned on near-singular Hessians of noise-like random-weight heatmaps);
   a 3D point (individual, frame, joint) is ALL-CLEAR when every view that passes step 4's score
-  threshold in the oracle chain is clear and taylor there, and both chains keep the same views.
+  threshold in the oracle chain is clear there, and both chains keep the same views.
 """
 from __future__ import annotations
 
@@ -202,7 +202,7 @@ def oracle_chain(scene, w, config):
 def compare(scene, hip, ora, score_threshold=0.5):
     """The parity figures (see the module docstring for the definitions)."""
     C, A, J = scene["n_views"], scene["n_animals"], 17
-    am_eq, n_clear, n_all, dkp, n_kp = [], 0, 0, [], 0
+    am_eq, n_clear, n_all, dkp, n_kp, dkp_clear = [], 0, 0, [], 0, []
     clear_cj = np.zeros((A, scene["n_frames"], C, J), bool)
     for f, (h, o) in enumerate(zip(hip["per_frame"], ora["per_frame"])):
         kp, sc, am = h[0], h[1], h[2]
@@ -214,12 +214,16 @@ def compare(scene, hip, ora, score_threshold=0.5):
         n_kp += int(ok.sum())
         if ok.any():
             dkp.append(np.abs(kp[ok] - rkp[ok]).max(axis=-1))
+        okc = clear & (sc >= 0.3) & (rsc >= 0.3)
+        if okc.any():
+            dkp_clear.append(np.abs(kp[okc] - rkp[okc]).max(axis=-1))
         # crop k of view owner[k] is individual (k - first crop of the view): boxes are per individual in order
         first = {c: int(np.argmax(owner == c)) for c in range(C)}
         for k in range(len(owner)):
-            clear_cj[k - first[owner[k]], f, owner[k]] = clear[k] & taylor[k]
+            clear_cj[k - first[owner[k]], f, owner[k]] = clear[k]
     am_eq = np.concatenate([x.ravel() for x in am_eq]) if am_eq else np.zeros(0, bool)
     dkp = np.concatenate(dkp) if dkp else np.zeros(0)
+    dkp_clear = np.concatenate(dkp_clear) if dkp_clear else np.zeros(0)
     # 3D: views that pass the score threshold after the Viterbi filter, per (a, f, j)
     def views(kp2d_f):
         kp = kp2d_f.transpose((2, 4, 0, 1, 3))                               # (A, C, F, J, 3)
@@ -240,6 +244,8 @@ def compare(scene, hip, ora, score_threshold=0.5):
         "n_clear_taylor_scored": n_kp,
         "kp_max_abs_px": float(dkp.max()) if dkp.size else float("nan"),
         "kp_p99_abs_px": q(dkp, 99),
+        "kp_max_abs_px_clear": float(dkp_clear.max()) if dkp_clear.size else float("nan"),
+        "kp_p99_abs_px_clear": q(dkp_clear, 99),
         "points": int(every.sum()),
         "all_clear_points": int(sel.sum()),
         "all_clear_fraction": float(sel.sum()) / max(1, int(every.sum())),
