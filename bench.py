@@ -203,7 +203,11 @@ def parity_3d(device, slice_frames=8):
     import parity3d
     out = {"tolerances": {"argmax": "bit-exact on clear joints (top-2 margin > 5e-2 max|H|)",
                           "keypoint_px": parity3d.KP_TOL_PX,
-                          "kp3d_mm_all_clear": {"median": parity3d.KP3D_MM_MEDIAN, "p99": parity3d.KP3D_MM_P99}}}
+                          "kp3d_dlt_mm_all_clear": {"median": parity3d.KP3D_DLT_MM_MEDIAN,
+                                                    "p99": parity3d.KP3D_DLT_MM_P99},
+                          "kp3d_optim_mm_all_clear": f"within max(scipy ftol 1e-3 vs 1e-10 band, "
+                                                     f"{parity3d.KP3D_OPTIM_MM_MEDIAN} mm median / "
+                                                     f"{parity3d.KP3D_OPTIM_MM_P99} mm p99)"}}
     w = parity3d.make_weights(device=torch_device(device))
     for name, nf in (("config2_frame", 1), ("clip_slice", slice_frames)):
         t0 = time.perf_counter()

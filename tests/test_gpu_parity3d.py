@@ -8,8 +8,12 @@ default step 4 (Viterbi -> DLT -> optim_points, ``ransac = false``).  Stated tol
   * the clear fraction is at least CLEAR_MIN (random-weight heatmaps have flat tops; the figure is the
     share of joints the bit-exact statement covers);
   * keypoints within 0.5 px (SURVEY 8(d)) on clear, Taylor-regime joints;
-  * kp3d within KP3D_MM_MEDIAN (median) / KP3D_MM_P99 (p99) mm on all-clear points, with at least
-    ALL_CLEAR_MIN of them.
+  * on all-clear points (every kept view clear, both chains keep the same views; at least ALL_CLEAR_MIN):
+    the DLT of the score-thresholded views within KP3D_DLT_MM_MEDIAN / KP3D_DLT_MM_P99 mm (median / p99) --
+    the bf16 path's 2D differences carried into 3D; and, where optim_points ran (the reference default,
+    >= 20 points per individual), the optimised joints within max(scipy's own ftol 1e-3 vs 1e-10 band,
+    KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99) -- GPU LM and scipy TRF stop at different points of the
+    same early-stopped problem.
 """
 import json
 
@@ -36,5 +40,8 @@ def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames):
     assert fig["clear_fraction"] >= parity3d.CLEAR_MIN
     assert fig["n_clear_taylor_scored"] > 0 and fig["kp_max_abs_px"] <= parity3d.KP_TOL_PX
     assert fig["all_clear_points"] >= parity3d.ALL_CLEAR_MIN
-    assert fig["kp3d_mm_all_clear_median"] <= parity3d.KP3D_MM_MEDIAN
-    assert fig["kp3d_mm_all_clear_p99"] <= parity3d.KP3D_MM_P99
+    assert fig["kp3d_dlt_mm_all_clear_median"] <= parity3d.KP3D_DLT_MM_MEDIAN
+    assert fig["kp3d_dlt_mm_all_clear_p99"] <= parity3d.KP3D_DLT_MM_P99
+    if fig["optim_points"]:
+        assert fig["kp3d_optim_mm_all_clear_median"] <= max(fig["scipy_band_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
+        assert fig["kp3d_optim_mm_all_clear_p99"] <= max(fig["scipy_band_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)

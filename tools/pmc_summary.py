@@ -5,7 +5,11 @@ FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes 
 coalesced streaming reads (16 B/lane, incl. global_load_lds) -> x2; WRITE_SIZE is exact for
 16 B/lane stores.  hbm_bytes_per_launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
 
-python tools/pmc_summary.py <pmc_dir> <kernel-substring> <algorithmic_bytes> <flops> > out.json
+python tools/pmc_summary.py <pmc_dir> <kernel-substring> <algorithmic_bytes> <flops> [period:stride:phase] > out.json
+
+The optional selector keeps, among the matching dispatches of each pass in dispatch order, ordinal o with
+o % period < period - period % stride and (o % period) % stride == phase: e.g. 97:3:1 picks the attention
+projections out of the ViT-H forward's 97 launches of gemm_pp_kernel<0,...> (32 x (qkv, proj, fc2) + deconv 1).
 """
 import csv
 import glob
@@ -17,18 +21,25 @@ from collections import defaultdict
 
 def main():
     d, key, alg_bytes, flops = sys.argv[1], sys.argv[2], float(sys.argv[3]), float(sys.argv[4])
+    sel = [int(v) for v in sys.argv[5].split(":")] if len(sys.argv) > 5 else None
     csv.field_size_limit(1 << 30)
     vals = defaultdict(list)
     dur = []
     for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         with open(f) as fh:
-            for row in csv.DictReader(fh):
-                if key not in row["Kernel_Name"]:
+            rows = [row for row in csv.DictReader(fh) if key in row["Kernel_Name"]]
+        did = "Dispatch_Id" if rows and "Dispatch_Id" in rows[0] else "Correlation_Id"
+        order = {k: i for i, k in enumerate(sorted({int(r[did]) for r in rows}))}
+        for row in rows:
+            if sel:
+                period, stride, phase = sel
+                r = order[int(row[did])] % period
+                if r >= period - period % stride or r % stride != phase:
                     continue
-                vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
-                dur.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+            vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+            dur.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
-    out = {"kernel": key, "samples": {k: len(v) for k, v in vals.items()}, "counters_avg_per_launch": avg,
+    out = {"kernel": key + (f" [dispatch selector {sys.argv[5]}]" if sel else ""), "samples": {k: len(v) for k, v in vals.items()}, "counters_avg_per_launch": avg,
            "algorithmic_bytes_per_launch": alg_bytes, "flops_per_launch": flops,
            "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (MI355X_MICROARCH.md HBM section gfx950 corrections)"}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
