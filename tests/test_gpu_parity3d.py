@@ -11,9 +11,10 @@ default step 4 (Viterbi -> DLT -> optim_points, ``ransac = false``).  Stated tol
   * on all-clear points (every kept view clear, both chains keep the same views; at least ALL_CLEAR_MIN):
     the DLT of the score-thresholded views within KP3D_DLT_MM_MEDIAN / KP3D_DLT_MM_P99 mm (median / p99) --
     the bf16 path's 2D differences carried into 3D; and, where optim_points ran (the reference default,
-    >= 20 points per individual), the optimised joints within max(scipy's own ftol 1e-3 vs 1e-10 band,
-    KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99) -- GPU LM and scipy TRF stop at different points of the
-    same early-stopped problem.
+    >= 20 points per individual), GPU LM and scipy TRF stop early at different points of the same problem,
+    so: the HIP solution, scored by the oracle's objective on the oracle's inputs, costs at most
+    OPTIM_COST_RATIO x scipy's, and it lies within max(scipy's own ftol 1e-3 vs 1e-10 band,
+    KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99) of the converged (ftol 1e-10) solution.
 """
 import json
 
@@ -43,5 +44,6 @@ def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames):
     assert fig["kp3d_dlt_mm_all_clear_median"] <= parity3d.KP3D_DLT_MM_MEDIAN
     assert fig["kp3d_dlt_mm_all_clear_p99"] <= parity3d.KP3D_DLT_MM_P99
     if fig["optim_points"]:
-        assert fig["kp3d_optim_mm_all_clear_median"] <= max(fig["scipy_band_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
-        assert fig["kp3d_optim_mm_all_clear_p99"] <= max(fig["scipy_band_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
+        assert fig["optim_cost_ratio_max"] <= parity3d.OPTIM_COST_RATIO
+        assert fig["kp3d_optim_to_converged_mm_median"] <= max(fig["scipy_band_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
+        assert fig["kp3d_optim_to_converged_mm_p99"] <= max(fig["scipy_band_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
