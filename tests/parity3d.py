@@ -55,8 +55,10 @@ KP3D_DLT_MM_P99 = 2.0
 # (scipy at ftol 1e-10) is within KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99 (median / p99) mm or within
 # scipy's own distance to it (ftol 1e-3 vs 1e-10), whichever is larger
 OPTIM_COST_RATIO = 1.01
+SOLVER_COST_RATIO = 1.001      # the GPU solver on the oracle chain's inputs vs scipy (tests/test_gpu_pipeline.py)
 KP3D_OPTIM_MM_MEDIAN = 1.0
 KP3D_OPTIM_MM_P99 = 5.0
+KP3D_OPTIM_E2E_MM_MEDIAN = 1.0
 CLEAR_MIN = 0.3        # share of joints with a clear top-2 margin (random-weight heatmaps)
 ALL_CLEAR_MIN = 4      # all-clear 3D points a case must contain
 
@@ -279,16 +281,25 @@ def compare(scene, hip, ora, score_threshold=0.5):
     band = np.linalg.norm(ora["kp3d"] - ora["kp3d_tight"], axis=-1)                  # scipy 1e-3 vs 1e-10
     d_conv = np.linalg.norm(hip["kp3d"] - ora["kp3d_tight"], axis=-1)                # HIP vs scipy 1e-10
     sel_opt = sel & optim_ran[:, None, None] & np.isfinite(band)
-    # the HIP chain's optim_points solution scored by the oracle's objective on the oracle's own 2D inputs
-    cost_ratio = []
-    jl_by_a = hip["joint_len"] if len(hip["joint_len"]) == A else []     # step 4 lists only the optimised ones
-    for a, (p2, targs, cost) in sorted(ora.get("problems", {}).items()):
-        if a >= len(jl_by_a):
-            cost_ratio.append(float("inf"))
-            continue
-        x = np.hstack([hip["kp3d"][a].ravel(), np.asarray(jl_by_a[a], dtype=np.float64)])
-        r = ora["cgroup"]._error_fun_triangulation(x, p2, *targs)
-        cost_ratio.append(0.5 * float(np.sum(r * r)) / cost)
+    def cost_ratios(kp3d, jls):
+        """per individual: the solution's cost under the oracle's objective on the oracle's 2D / scipy's cost"""
+        out = []
+        jl_by_a = jls if len(jls) == A else []                       # step 4 lists only the optimised ones
+        for a, (p2, targs, cost) in sorted(ora.get("problems", {}).items()):
+            if a >= len(jl_by_a):
+                out.append(float("inf"))
+                continue
+            x = np.hstack([kp3d[a].ravel(), np.asarray(jl_by_a[a], dtype=np.float64)])
+            r = ora["cgroup"]._error_fun_triangulation(x, p2, *targs)
+            out.append(0.5 * float(np.sum(r * r)) / cost)
+        return out
+    # the whole HIP chain's solution (its own 2D inputs) and the GPU solver on the oracle chain's inputs
+    cost_ratio = cost_ratios(hip["kp3d"], hip["joint_len"])
+    sol = hip.get("solver_on_oracle_inputs")
+    solver_ratio = cost_ratios(sol["kp3d"], sol["joint_len"]) if sol else []
+    d_sol = np.linalg.norm(sol["kp3d"] - ora["kp3d"], axis=-1) if sol else np.full(band.shape, np.nan)
+    d_sol_conv = np.linalg.norm(sol["kp3d"] - ora["kp3d_tight"], axis=-1) if sol else np.full(band.shape, np.nan)
+    sel_sol = optim_ran[:, None, None] & np.isfinite(band) & np.isfinite(d_sol)
     return {
         "crops_joints": int(n_all),
         "clear_fraction": n_clear / max(1, n_all),
@@ -318,6 +329,14 @@ def compare(scene, hip, ora, score_threshold=0.5):
         "kp3d_optim_to_converged_mm_median": q(d_conv[sel_opt], 50),
         "kp3d_optim_to_converged_mm_p99": q(d_conv[sel_opt], 99),
         "optim_cost_ratio_max": max(cost_ratio) if cost_ratio else float("nan"),
+        "solver_points": int(sel_sol.sum()),
+        "solver_cost_ratio_max": max(solver_ratio) if solver_ratio else float("nan"),
+        "solver_vs_scipy_mm_median": q(d_sol[sel_sol], 50),
+        "solver_vs_scipy_mm_p99": q(d_sol[sel_sol], 99),
+        "solver_to_converged_mm_median": q(d_sol_conv[sel_sol], 50),
+        "solver_to_converged_mm_p99": q(d_sol_conv[sel_sol], 99),
+        "scipy_band_all_mm_median": q(band[sel_sol], 50),
+        "scipy_band_all_mm_p99": q(band[sel_sol], 99),
         "same_views_fraction": float(same_views.mean()),
     }
 
@@ -337,4 +356,10 @@ def run(n_frames=1, optim=True, seed=7, weights=None):
     config = load_config(optim=optim)
     hip = hip_chain(scene, w, config)
     ora = oracle_chain(scene, w, config)
+    if ora["problems"]:
+        # the GPU step 4 on the ORACLE chain's filtered 2D: optim_points against scipy on identical inputs
+        from mqhip.geometry import CameraGroup
+        from src.pipeline import step4_aniposefiltering as step4
+        k3, _, _, jl = step4.reconstruct_3d(ora["kp2d_f"].copy(), CameraGroup.from_dicts(scene["cams"]), config)
+        hip["solver_on_oracle_inputs"] = {"kp3d": k3, "joint_len": jl}
     return compare(scene, hip, ora, config["triangulation"]["score_threshold"]), hip, ora

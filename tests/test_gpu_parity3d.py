@@ -44,6 +44,9 @@ def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames):
     assert fig["kp3d_dlt_mm_all_clear_median"] <= parity3d.KP3D_DLT_MM_MEDIAN
     assert fig["kp3d_dlt_mm_all_clear_p99"] <= parity3d.KP3D_DLT_MM_P99
     if fig["optim_points"]:
-        assert fig["optim_cost_ratio_max"] <= parity3d.OPTIM_COST_RATIO
-        assert fig["kp3d_optim_to_converged_mm_median"] <= max(fig["scipy_band_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
-        assert fig["kp3d_optim_to_converged_mm_p99"] <= max(fig["scipy_band_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
+        # the GPU optim_points against scipy on the oracle chain's own (ViT-derived) 2D inputs
+        assert fig["solver_cost_ratio_max"] <= parity3d.SOLVER_COST_RATIO
+        assert fig["solver_vs_scipy_mm_median"] <= max(fig["scipy_band_all_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
+        assert fig["solver_vs_scipy_mm_p99"] <= max(fig["scipy_band_all_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
+        # end to end (each chain its own 2D, each solver its own stopping point): the median is stated
+        assert fig["kp3d_optim_mm_all_clear_median"] <= parity3d.KP3D_OPTIM_E2E_MM_MEDIAN

@@ -1,4 +1,4 @@
-# Round 4 (session 2): the end-to-end parity tests on the marker scene (DLT propagation + optim band),
+# Round 4 (session 2): the end-to-end parity probe on the marker scene (DLT propagation, optim vs scipy),
 # PMC passes over the ViT-H forward after the residual move (proj = gemm_pp_kernel<0> launches 97:3:1, the
 # fused add + LayerNorm kernels, attention), then the config-3 clip.  First failure ends the call.
 set -o pipefail
@@ -6,8 +6,8 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=${1:-r04g}
 mkdir -p gpurun_out/$OUT
-timeout -k 10 900 python3 -u -m pytest tests/test_gpu_parity3d.py tests/test_gpu_pose.py -m gpu -x -v -s --timeout 800 --timeout-method thread > gpurun_out/$OUT/pytest_parity.log 2>&1 || { echo PYTEST PARITY FAILED; grep -E "parity3d|clear|FAILED|Error" gpurun_out/$OUT/pytest_parity.log | cut -c1-600 | head -20; exit 1; }
-grep -E "parity3d|clear" gpurun_out/$OUT/pytest_parity.log | cut -c1-1500
+timeout -k 10 700 python3 -u tools/parity3d_probe.py --frames 24 --seeds 7 > gpurun_out/$OUT/parity3d.log 2>&1 || { echo PARITY PROBE FAILED; tail -30 gpurun_out/$OUT/parity3d.log; exit 1; }
+grep "^{" gpurun_out/$OUT/parity3d.log
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" \
            "GRBM_GUI_ACTIVE SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_WAVES" \
