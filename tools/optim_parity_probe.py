@@ -1,0 +1,65 @@
+"""GPU optim_points vs scipy on the 2D keypoints of the marker-scene oracle chain (tests/parity3d.py): per
+individual the cost of the GPU solution under the oracle's objective / scipy's cost at ftol 1e-3, the distance
+to scipy's converged (ftol 1e-10) solution, and the solver's iterations / stop status, for several conjugate-
+gradient caps (MQ_TUNE_OPTIM_PCG_ITERS) and GPU ftol values.  python tools/optim_parity_probe.py [--frames 24]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "tests"), ROOT, os.path.join(ROOT, "macaque-3d-pose-estimation_amd")):
+    sys.path.insert(0, p)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=24)
+    ap.add_argument("--pcg", default="20,40,80,128")
+    ap.add_argument("--ftol", default="1e-3,1e-4")
+    a = ap.parse_args()
+    import parity3d
+    from mqhip import _lib
+    from mqhip.geometry import CameraGroup
+    from mqhip.optim import optim_points_batch
+    from src.pipeline.step4_aniposefiltering import BODYPARTS, load_constraints
+    scene = parity3d.make_scene(n_frames=a.frames)
+    config = parity3d.load_config()
+    ora = parity3d.oracle_chain(scene, parity3d.make_weights(), config)
+    tri = config["triangulation"]
+    cons, weak = load_constraints(config, BODYPARTS), load_constraints(config, BODYPARTS, "constraints_weak")
+    cg = CameraGroup.from_dicts(scene["cams"])
+    kp = ora["kp2d_f"].transpose((2, 4, 0, 1, 3))
+    A, C, F, J, _ = kp.shape
+    run = sorted(ora["problems"])
+    pts = np.stack([ora["problems"][i][0] for i in run])                  # (B, C, F, J, 2) oracle inputs
+    init = np.stack([np.asarray(cg.triangulate(pts[b].reshape(C, -1, 2))).reshape(F, J, 3) for b in range(len(run))])
+    lib = _lib.Context.get(0).lib
+    for pcg in [int(v) for v in a.pcg.split(",")]:
+        _lib.check(lib.mq_set_tuning(4, pcg), "pcg")
+        for ftol in [float(v) for v in a.ftol.split(",")]:
+            p3, jl, stats, _ = optim_points_batch(
+                cg, pts, init, cons, weak, scale_smooth=tri["scale_smooth"], scale_length=tri["scale_length"],
+                scale_length_weak=tri["scale_length_weak"], reproj_error_threshold=tri["reproj_error_threshold"],
+                n_deriv_smooth=tri["n_deriv_smooth"], ftol=ftol, return_stats=True)
+            rows = []
+            for b, i in enumerate(run):
+                p2, targs, cost = ora["problems"][i]
+                r = ora["cgroup"]._error_fun_triangulation(np.hstack([p3[b].ravel(), jl[b]]), p2, *targs)
+                d = np.linalg.norm(p3[b] - ora["kp3d_tight"][i], axis=-1)
+                d = d[np.isfinite(d)]
+                st = np.asarray(stats).reshape(len(run), -1)[b]
+                rows.append({"ind": i, "cost_ratio": round(0.5 * float(r @ r) / cost, 5),
+                             "to_converged_mm_p50_p99": [round(float(np.median(d)), 3), round(float(np.percentile(d, 99)), 2)],
+                             "iters": int(st[2]), "status": int(st[3])})
+            print(json.dumps({"pcg": pcg, "ftol": ftol, "rows": rows}), flush=True)
+    _lib.check(lib.mq_set_tuning(4, 20), "pcg")
+    band = np.linalg.norm(ora["kp3d"] - ora["kp3d_tight"], axis=-1)
+    print(json.dumps({"scipy_1e-3_to_converged_mm_p50_p99": [round(float(np.nanmedian(band)), 3),
+                                                            round(float(np.nanpercentile(band, 99)), 2)]}))
+
+
+if __name__ == "__main__":
+    main()
