@@ -69,6 +69,9 @@ const char* mq_last_error(void);
                                        64x64-tile kernel (same accumulation order, tested equal); 0: 128x128 */
 #define MQ_TUNE_QKV_HEAD_MAJOR 20   /* 1 (default): the ViT qkv GEMM writes Q / K / V head-major (each head's rows
                                        contiguous) for the attention's loads; 0: row-major (same results) */
+#define MQ_TUNE_OPTIM_STOP 21       /* optim_points' stop rule on an accepted LM step, bits: 0 = scipy's ftol test
+                                       alone (dF < ftol F); 1 = and the step's actual / predicted reduction > 0.25
+                                       (scipy trf's condition); 2 = the test passed on two accepted steps in a row */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

@@ -164,6 +164,10 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_QKV_HEAD_MAJOR:
       g_qkv_head_major = value != 0;
       break;
+    case MQ_TUNE_OPTIM_STOP:
+      if (value < 0 || value > 3) return fail("mq_set_tuning: optim stop rule must be in [0, 3]", -2);
+      mq::g_optim_stop = value;
+      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -179,6 +183,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_OPTIM_PRECOND_LDS: return mq::g_optim_precond_lds;
     case MQ_TUNE_GEMM_TILE64: return mq::g_gemm_tile64;
     case MQ_TUNE_QKV_HEAD_MAJOR: return g_qkv_head_major;
+    case MQ_TUNE_OPTIM_STOP: return mq::g_optim_stop;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }

@@ -99,6 +99,7 @@ int udp_decode(const float* avg, int n, int joints, int h, int w, const float* c
 
 // optim_points (optim.hip)
 extern int g_optim_pcg_iters;
+extern int g_optim_stop;  // optim_points stop-rule bits (MQ_TUNE_OPTIM_STOP)
 extern int g_optim_precond_lds;  // 1 (default): LDS-staged preconditioner when the series fits; 0: global memory
 size_t optim_workspace_bytes(int B, int F, int J, int NL);
 int optim_points(const double* cams, int C, const double* p2d, double* x, int B, int F, int J, const int* cons_host,

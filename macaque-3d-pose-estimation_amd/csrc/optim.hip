@@ -1449,6 +1449,33 @@ __global__ void optim_axpy_kernel(const double* x, const double* d, double* xt, 
   xt[i] = (fix && k >= NX) ? x[i] : x[i] + d[i];
 }
 
+// Predicted cost reduction of the Gauss-Newton model for the step d (one workgroup per batch element):
+// pred = -g.d - d.H.d / 2.  The PCG iterate solves (H + lam Dm) d = -g over a Krylov space that holds d, so
+// d.(H + lam Dm).d = -g.d and pred = (-g.d + lam d.Dm.d) / 2 from two dot products (fixed lengths excluded).
+__global__ __launch_bounds__(256) void optim_pred_kernel(OptDims D, OptBufs Bf, double* pred) {
+  const int b = blockIdx.x;
+  const int nv = D.fix ? D.NX : D.NV;
+  const size_t o = (size_t)b * D.NV;
+  double gd = 0.0, dd = 0.0;
+  for (int k = threadIdx.x; k < nv; k += 256) {
+    const double dk = Bf.d[o + k];
+    gd += Bf.g[o + k] * dk;
+    dd += damp_of(Bf.diag[o + k]) * dk * dk;
+  }
+  __shared__ double sg[256], sd[256];
+  sg[threadIdx.x] = gd;
+  sd[threadIdx.x] = dd;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+      sg[threadIdx.x] += sg[threadIdx.x + w];
+      sd[threadIdx.x] += sd[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) pred[b] = 0.5 * (-sg[0] + Bf.ctl[2 * b] * sd[0]);
+}
+
 __global__ void optim_accept_kernel(double* x, const double* xt, const double* ctl, int NV, int B) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)B * NV) return;
@@ -1459,6 +1486,7 @@ __global__ void optim_accept_kernel(double* x, const double* xt, const double* c
 
 int g_optim_precond_lds = 1;
 int g_optim_pcg_iters = 20;  // LM inner-solve cap: tools/optim_probe.py (cost within 3e-4 of scipy at 20; 40 costs 1.6x the time)
+int g_optim_stop = 0;        // stop rule bits (MQ_TUNE_OPTIM_STOP): 1 model-agreement ratio > 0.25, 2 two steps in a row
 
 size_t optim_workspace_bytes(int B, int F, int J, int NL) {
   const size_t NV = (size_t)F * J * 3 + NL;
@@ -1471,7 +1499,7 @@ size_t optim_workspace_bytes(int B, int F, int J, int NL) {
   n += (size_t)B * J * F * OPT_FS + (size_t)B * OPT_MAXL;  // fac pinvL
   n += (size_t)B * J * F * 18 * OPT_MAXN + 2;               // mn (+ 16-B alignment)
   n += (size_t)B * (OPT_MAXIT + 1) * (J + 2);    // rzJ, pq
-  n += (size_t)B * 4;                            // cost, cost_t, ctl(2)
+  n += (size_t)B * 5;                            // cost, cost_t + pred (2), ctl(2)
   n += (size_t)NL + 2 + B;                       // constraint pairs (int32), ssf
   return n * sizeof(double);
 }
@@ -1538,7 +1566,8 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
   Bf.rzJ = take((size_t)B * (OPT_MAXIT + 1) * (J + 1));
   Bf.pq = take((size_t)B * (OPT_MAXIT + 1));
   Bf.cost = take(B);
-  double* cost_t = take(B);
+  double* cost_t = take(2 * (size_t)B);   // trial costs, then the predicted reductions (one copy back)
+  double* pred_d = cost_t + B;
   double* ctl = take(2 * (size_t)B);
   Bf.ctl = ctl;
   Bf.cams = cams;
@@ -1554,8 +1583,9 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
   const int npcg = std::max(1, std::min(g_optim_pcg_iters, OPT_MAXIT));
   const dim3 gridFB(F, B);
   const int ew_blocks = (int)((NVB + 255) / 256);
-  std::vector<double> lam(B, 1e-3), cost(B), costt(B), hctl(2 * B, 0.0);
-  std::vector<int> active(B, 1), iters(B, 0), status(B, 2);
+  std::vector<double> lam(B, 1e-3), cost(B), costt(2 * B), hctl(2 * B, 0.0);
+  std::vector<int> active(B, 1), iters(B, 0), status(B, 2), small(B, 0);
+  const bool stop_ratio = (g_optim_stop & 1) != 0, stop_twice = (g_optim_stop & 2) != 0;
 
   // preconditioner step: series staged in LDS when they fit (every clip up to ~450 frames at n = 2)
   const size_t lds_b = optim_precond_lds_bytes(F, D.n);
@@ -1631,8 +1661,11 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
       precond(it);
     }
     hipLaunchKernelGGL(optim_axpy_kernel, dim3(ew_blocks), dim3(256), 0, s, x, Bf.d, xt, D.NX, D.NV, B, D.fix);
+    if (stop_ratio) hipLaunchKernelGGL(optim_pred_kernel, dim3(B), dim3(256), 0, s, D, Bf, pred_d);
     eval(xt, 1, cost_t);
-    if (hipMemcpyAsync(costt.data(), cost_t, sizeof(double) * B, hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
+    if (hipMemcpyAsync(costt.data(), cost_t, sizeof(double) * (stop_ratio ? 2 * B : B), hipMemcpyDeviceToHost, s) !=
+        hipSuccess)
+      return -3;
     if (hipStreamSynchronize(s) != hipSuccess) return -3;
     bool accepted_any = false;
     for (int b = 0; b < B; ++b) {
@@ -1642,7 +1675,12 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
         const double dF = cost[b] - costt[b];
         hctl[2 * b + 1] = 1;
         accepted_any = true;
-        if (dF < ftol * cost[b]) {  // scipy's ftol test on an accepted step
+        // scipy's ftol test on an accepted step; with stop bit 1 also its model-agreement condition
+        // (trf: dF < ftol F and ratio > 0.25), with bit 2 on two accepted steps in a row
+        bool ft = dF < ftol * cost[b];
+        if (ft && stop_ratio) ft = dF > 0.25 * costt[B + b];
+        small[b] = ft ? small[b] + 1 : 0;
+        if (small[b] >= (stop_twice ? 2 : 1)) {
           active[b] = 0;
           status[b] = 1;
         }
