@@ -44,8 +44,11 @@ extern "C" {
  *   3 -- camera rows carry a model (slot 22: 0 omnidir, 1 pinhole, 2 fisheye) and a fifth distortion
  *        coefficient (slot 23); rows written for ABI 1-2 (zeros there) keep the omnidir meaning.
  *        mq_camera_undistort / mq_camera_project added (mq_omnidir_* are the same functions).
- *   4 -- mq_alldata_json (host: step 1's alldata.json text from row arrays) added. */
-#define MQ_ABI_VERSION 4
+ *   4 -- mq_alldata_json (host: step 1's alldata.json text from row arrays) added.
+ *   5 -- tuning key MQ_TUNE_OPTIM_STOP (21) added; optim_points defaults to 40 PCG iterations per LM step and
+ *        the ftol test on two accepted steps in a row (it lands closer to the converged solution than
+ *        scipy's own ftol stop on ViT-derived 2D). */
+#define MQ_ABI_VERSION 5
 
 typedef struct mq_ctx mq_ctx;
 typedef struct mq_vitpose mq_vitpose;
@@ -59,7 +62,7 @@ const char* mq_last_error(void);
  * something else.  Changing one makes the next mq_vitpose_forward re-capture its graph. */
 #define MQ_TUNE_GEMM_FORCE_SMALL 2  /* 1: route every GEMM to the 128x128 / 64x64 kernel (default 0; the reference
                                        route of the bitwise implicit-convolution tests) */
-#define MQ_TUNE_OPTIM_PCG_ITERS 4   /* cap on the conjugate-gradient iterations per Levenberg-Marquardt step (default 20;
+#define MQ_TUNE_OPTIM_PCG_ITERS 4   /* cap on the conjugate-gradient iterations per Levenberg-Marquardt step (default 40;
                                        results stay within the optim_points tolerance) */
 #define MQ_TUNE_GEMM_PINGPONG 12    /* 1 (default): 256x256 GEMMs with K % 64 == 0 on the ping-pong kernel (wave groups
                                        alternate LDS traffic and MFMA, gemm_pp.hip); 0: the interleaved-K-step kernel */
@@ -71,7 +74,8 @@ const char* mq_last_error(void);
                                        contiguous) for the attention's loads; 0: row-major (same results) */
 #define MQ_TUNE_OPTIM_STOP 21       /* optim_points' stop rule on an accepted LM step, bits: 0 = scipy's ftol test
                                        alone (dF < ftol F); 1 = and the step's actual / predicted reduction > 0.25
-                                       (scipy trf's condition); 2 = the test passed on two accepted steps in a row */
+                                       (scipy trf's condition); 2 (default) = the test passed on two accepted steps
+                                       in a row */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

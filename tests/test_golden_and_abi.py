@@ -114,7 +114,7 @@ def test_library_exports_every_header_symbol(lib):
     for s in syms:
         assert hasattr(lib, s), f"libmq_hip.so does not export {s}"
     assert sorted(_lib.EXPORTED) == syms
-    assert lib.mq_abi_version() == 4
+    assert lib.mq_abi_version() == 5
 
 
 def test_library_is_gfx950_code_object(lib):
@@ -128,7 +128,7 @@ def test_last_error_is_safe_without_gpu(lib):
     assert isinstance(lib.mq_last_error(), bytes)
 
 
-OPTIM_STOP_DEFAULT = 0   # include/mq_hip.h MQ_TUNE_OPTIM_STOP
+OPTIM_STOP_DEFAULT = 2   # include/mq_hip.h MQ_TUNE_OPTIM_STOP
 
 
 def test_tuning_knobs_only_select_equivalent_variants(lib):
@@ -138,7 +138,7 @@ def test_tuning_knobs_only_select_equivalent_variants(lib):
     for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 17, 22, 99):
         assert lib.mq_set_tuning(key, 1) == -2, key
         assert lib.mq_get_tuning(key) == -2, key
-    for key, default, other in ((2, 0, 1), (12, 1, 0), (18, 1, 0), (19, 1, 0), (20, 1, 0), (4, 20, 10),
+    for key, default, other in ((2, 0, 1), (12, 1, 0), (18, 1, 0), (19, 1, 0), (20, 1, 0), (4, 40, 10),
                                 (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1)):
         assert lib.mq_get_tuning(key) == default
         assert lib.mq_set_tuning(key, other) == 0
