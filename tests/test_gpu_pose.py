@@ -8,6 +8,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="n
 
 # bf16 heatmaps vs the fp32 oracle: max|dH| <= 2e-2 * max|H| per sample
 HM_TOL = 2e-2
+# share of clear joints on the seeded random ViT-H of the config-2 batch test (noise-like maps)
+RANDOM_CLEAR_MIN = 0.01
 
 
 def _frames_and_boxes(n_views=3, seed=0):
@@ -223,7 +225,11 @@ def test_vitpose_h_config2_batch_vs_fp32_oracle():
     flat = ref.reshape(32, 17, -1)
     top2 = np.sort(flat, axis=-1)[..., -2:]
     clear = (top2[..., 1] - top2[..., 0]) / np.abs(flat).max(axis=-1) > 5e-2
-    assert clear.sum() > 0
+    # seeded random weights give noise-like maps: few joints have a clear top-2 margin, and every one of
+    # them must decode to the oracle's argmax; the keypoint tolerance on realistic peaks is the marker-scene
+    # test below (test_vitpose_h_config2_marker_keypoints)
+    print(f"random-weight heatmaps: clear fraction {clear.mean():.3f}")
+    assert clear.mean() >= RANDOM_CLEAR_MIN
     np.testing.assert_array_equal(am.cpu().numpy()[clear], ram[clear])
 
 
