@@ -51,10 +51,12 @@ KP3D_DLT_MM_P99 = 2.0
 # kp3d after optim_points (the reference default, scipy TRF stopped at ftol 1e-3; the GPU LM stops by its own
 # rule): the two early-stopped solvers land at different points of the same problem, so the statement is
 # about the problem, not the stopping point -- (i) the HIP solution scored by the oracle's objective on the
-# oracle's own 2D inputs costs at most OPTIM_COST_RATIO x scipy's; (ii) its distance to the converged solution
-# (scipy at ftol 1e-10) is within KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99 (median / p99) mm or within
-# scipy's own distance to it (ftol 1e-3 vs 1e-10), whichever is larger
-OPTIM_COST_RATIO = 1.01
+# oracle's own 2D inputs costs at most OPTIM_COST_RATIO x scipy's (SOLVER_COST_RATIO for the GPU solver on
+# identical inputs); (ii) its distance to the converged solution (scipy at ftol 1e-10) is within
+# KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99 (median / p99) mm or within scipy's own distance to it (ftol 1e-3
+# vs 1e-10), whichever is larger; (iii) the two chains' optimised joints differ by at most
+# KP3D_OPTIM_E2E_MM_MEDIAN mm at the median
+OPTIM_COST_RATIO = 1.002
 SOLVER_COST_RATIO = 1.001      # the GPU solver on the oracle chain's inputs vs scipy (tests/test_gpu_pipeline.py)
 KP3D_OPTIM_MM_MEDIAN = 1.0
 KP3D_OPTIM_MM_P99 = 5.0

@@ -12,9 +12,11 @@ default step 4 (Viterbi -> DLT -> optim_points, ``ransac = false``).  Stated tol
     the DLT of the score-thresholded views within KP3D_DLT_MM_MEDIAN / KP3D_DLT_MM_P99 mm (median / p99) --
     the bf16 path's 2D differences carried into 3D; and, where optim_points ran (the reference default,
     >= 20 points per individual), GPU LM and scipy TRF stop early at different points of the same problem,
-    so: the HIP solution, scored by the oracle's objective on the oracle's inputs, costs at most
-    OPTIM_COST_RATIO x scipy's, and it lies within max(scipy's own ftol 1e-3 vs 1e-10 band,
-    KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99) of the converged (ftol 1e-10) solution.
+    so: the GPU solver on the oracle chain's own 2D costs at most SOLVER_COST_RATIO x scipy's; the HIP
+    chain's solution, scored by the oracle's objective on the oracle's inputs, at most OPTIM_COST_RATIO x;
+    both lie within max(scipy's own ftol 1e-3 vs 1e-10 band, KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99) of
+    the converged (ftol 1e-10) solution; the chains' optimised joints differ by at most
+    KP3D_OPTIM_E2E_MM_MEDIAN mm (median).
 """
 import json
 
@@ -44,9 +46,14 @@ def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames):
     assert fig["kp3d_dlt_mm_all_clear_median"] <= parity3d.KP3D_DLT_MM_MEDIAN
     assert fig["kp3d_dlt_mm_all_clear_p99"] <= parity3d.KP3D_DLT_MM_P99
     if fig["optim_points"]:
-        # the GPU optim_points against scipy on the oracle chain's own (ViT-derived) 2D inputs
+        # the GPU optim_points against scipy on the oracle chain's own (ViT-derived) 2D inputs: cost within
+        # 0.1 % of scipy's, and no farther from the converged solution than scipy's own ftol-1e-3 stop is
         assert fig["solver_cost_ratio_max"] <= parity3d.SOLVER_COST_RATIO
-        assert fig["solver_vs_scipy_mm_median"] <= max(fig["scipy_band_all_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
-        assert fig["solver_vs_scipy_mm_p99"] <= max(fig["scipy_band_all_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
-        # end to end (each chain its own 2D, each solver its own stopping point): the median is stated
+        assert fig["solver_to_converged_mm_median"] <= max(fig["scipy_band_all_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
+        assert fig["solver_to_converged_mm_p99"] <= max(fig["scipy_band_all_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
+        # end to end (each chain its own 2D): the same two statements on all-clear points, and the median
+        # distance between the chains' optimised joints
+        assert fig["optim_cost_ratio_max"] <= parity3d.OPTIM_COST_RATIO
+        assert fig["kp3d_optim_to_converged_mm_median"] <= max(fig["scipy_band_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
+        assert fig["kp3d_optim_to_converged_mm_p99"] <= max(fig["scipy_band_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
         assert fig["kp3d_optim_mm_all_clear_median"] <= parity3d.KP3D_OPTIM_E2E_MM_MEDIAN
