@@ -9,7 +9,7 @@ pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="n
 # bf16 heatmaps vs the fp32 oracle: max|dH| <= 2e-2 * max|H| per sample
 HM_TOL = 2e-2
 # share of clear joints on the seeded random ViT-H of the config-2 batch test (noise-like maps)
-RANDOM_CLEAR_MIN = 0.01
+RANDOM_CLEAR_MIN = 0.15
 
 
 def _frames_and_boxes(n_views=3, seed=0):
