@@ -45,7 +45,7 @@ extern "C" {
  *        coefficient (slot 23); rows written for ABI 1-2 (zeros there) keep the omnidir meaning.
  *        mq_camera_undistort / mq_camera_project added (mq_omnidir_* are the same functions).
  *   4 -- mq_alldata_json (host: step 1's alldata.json text from row arrays) added.
- *   5 -- tuning key MQ_TUNE_OPTIM_STOP (21) added; optim_points defaults to 40 PCG iterations per LM step and
+ *   5 -- mq_add_layernorm added; tuning key MQ_TUNE_OPTIM_STOP (21) added; optim_points defaults to 40 PCG iterations per LM step and
  *        the ftol test on two accepted steps in a row (it lands closer to the converged solution than
  *        scipy's own ftol stop on ViT-derived 2D). */
 #define MQ_ABI_VERSION 5
@@ -178,6 +178,13 @@ int mq_det_resize_patch(mq_ctx* ctx, const uint8_t* frames, int64_t frame_stride
 /* LayerNorm over rows of f32 x (rows, dim), dim % 4 == 0 and <= 3072: y bf16 (out_f32 = 0) or f32. */
 int mq_layernorm(mq_ctx* ctx, const float* x, const float* gamma, const float* beta, void* y, int rows, int dim,
                  float eps, int out_f32, void* stream);
+
+/* The pre-norm residual update fused in front of a LayerNorm (ABI 5): x (rows, dim) f32 += p1 (+= p2, in that
+ * order; the bf16 branch outputs of the previous GEMMs, bias included; p2 may be null), x written back when
+ * store_x, y = LayerNorm(x) in bf16.  dim as mq_layernorm.  Used by the ViT (inside mq_vitpose_forward) and
+ * the Swin detector's blocks (x = x + attn(norm1 x); x = x + mlp(norm2 x): SWIN-Mask_R-CNN_bbox_only.py:29-61). */
+int mq_add_layernorm(mq_ctx* ctx, float* x, const uint16_t* p1, const uint16_t* p2, int store_x, const float* gamma,
+                     const float* beta, uint16_t* y, int rows, int dim, float eps, void* stream);
 
 /* Swin (shifted) window attention, window 7, head_dim 32 (dim = 32 * heads): qkv bf16 (n_img * height *
  * width, 3 * dim) of the LayerNorm-ed tokens, qkv_bias f32 (3 * dim) (the q/k/v of the zero-padded

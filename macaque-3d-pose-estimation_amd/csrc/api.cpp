@@ -844,6 +844,17 @@ int mq_layernorm(mq_ctx* ctx, const float* x, const float* gamma, const float* b
   return 0;
 }
 
+int mq_add_layernorm(mq_ctx* ctx, float* x, const uint16_t* p1, const uint16_t* p2, int store_x, const float* gamma,
+                     const float* beta, uint16_t* y, int rows, int dim, float eps, void* stream) {
+  if (int rc = check_det(ctx)) return rc;
+  if (!x || !p1 || !gamma || !beta || !y) return fail("mq_add_layernorm: null argument");
+  if (rows < 0 || dim <= 0 || dim % 4 || dim > 3072)
+    return fail("mq_add_layernorm: dim must be a multiple of 4, <= 3072", -2);
+  if (rows == 0) return 0;
+  K_TRY(mq::add_layernorm_f32_bf16(x, p1, p2, store_x != 0, gamma, beta, y, rows, dim, eps, (hipStream_t)stream));
+  return 0;
+}
+
 int mq_window_attention(mq_ctx* ctx, const uint16_t* qkv, const float* qkv_bias, const float* rel_table, uint16_t* out,
                         int n_img, int height, int width, int dim, int heads, int shift, void* stream) {
   if (int rc = check_det(ctx)) return rc;

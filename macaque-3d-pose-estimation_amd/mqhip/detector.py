@@ -213,6 +213,12 @@ class SwinDetectorHip:
                    "mq_im2col3x3")
         self._gemm(cols, wt, out, bias, rows, out.shape[1], 9 * 256, epi)
 
+    def _add_ln(self, x, p1, p2, store, g, b, y, rows, dim):
+        _lib.check(self.ctx.lib.mq_add_layernorm(self.ctx.handle, _lib.ptr(x), _lib.ptr(p1),
+                                                 None if p2 is None else _lib.ptr(p2), 1 if store else 0, _lib.ptr(g),
+                                                 _lib.ptr(b), _lib.ptr(y), rows, dim, LN_EPS, self._s()),
+                   "mq_add_layernorm")
+
     def _ln(self, x, g, b, y, rows, dim, out_f32=False):
         _lib.check(self.ctx.lib.mq_layernorm(self.ctx.handle, _lib.ptr(x), _lib.ptr(g), _lib.ptr(b), _lib.ptr(y), rows,
                                              dim, LN_EPS, 1 if out_f32 else 0, self._s()), "mq_layernorm")
@@ -267,9 +273,16 @@ class SwinDetectorHip:
             qkv = torch.empty((T, 3 * Cs), dtype=torch.bfloat16, device=dev)
             att = torch.empty((T, Cs), dtype=torch.bfloat16, device=dev)
             mlp = torch.empty((T, 4 * Cs), dtype=torch.bfloat16, device=dev)
+            # residual updates as in the ViT: proj and fc2 write their branch outputs in
+            # bf16 (bias included) and the next LayerNorm adds them to the f32 stream x (x += p1; x += p2)
+            p1 = torch.empty((T, Cs), dtype=torch.bfloat16, device=dev)
+            p2 = torch.empty((T, Cs), dtype=torch.bfloat16, device=dev)
             for bi in range(depth):
                 p = f"backbone.stages.{si}.blocks.{bi}."
-                self._ln(x, self.w[p + "norm1.weight"], self.w[p + "norm1.bias"], h, T, Cs)
+                if bi == 0:
+                    self._ln(x, self.w[p + "norm1.weight"], self.w[p + "norm1.bias"], h, T, Cs)
+                else:
+                    self._add_ln(x, p1, p2, True, self.w[p + "norm1.weight"], self.w[p + "norm1.bias"], h, T, Cs)
                 self._gemm(h, self.w[p + "attn.w_msa.qkv.weight"], qkv, self.w[p + "attn.w_msa.qkv.bias"], T, 3 * Cs,
                            Cs, EPI_BF16)
                 shift = self.cfg["window"] // 2 if bi % 2 else 0
@@ -277,15 +290,18 @@ class SwinDetectorHip:
                     self.ctx.handle, _lib.ptr(qkv), _lib.ptr(self.w[p + "attn.w_msa.qkv.bias"]),
                     _lib.ptr(self.w[p + "attn.w_msa.relative_position_bias_table"]), _lib.ptr(att), n, Hs, Ws, Cs,
                     heads, shift, self._s()), "mq_window_attention")
-                self._gemm(att, self.w[p + "attn.w_msa.proj.weight"], x, self.w[p + "attn.w_msa.proj.bias"], T, Cs,
-                           Cs, EPI_RESID)
-                self._ln(x, self.w[p + "norm2.weight"], self.w[p + "norm2.bias"], h, T, Cs)
+                self._gemm(att, self.w[p + "attn.w_msa.proj.weight"], p1, self.w[p + "attn.w_msa.proj.bias"], T, Cs,
+                           Cs, EPI_BF16)
+                self._add_ln(x, p1, None, False, self.w[p + "norm2.weight"], self.w[p + "norm2.bias"], h, T, Cs)
                 self._gemm(h, self.w[p + "ffn.layers.0.0.weight"], mlp, self.w[p + "ffn.layers.0.0.bias"], T, 4 * Cs,
                            Cs, EPI_GELU)
-                self._gemm(mlp, self.w[p + "ffn.layers.1.weight"], x, self.w[p + "ffn.layers.1.bias"], T, Cs,
-                           4 * Cs, EPI_RESID)
+                self._gemm(mlp, self.w[p + "ffn.layers.1.weight"], p2, self.w[p + "ffn.layers.1.bias"], T, Cs,
+                           4 * Cs, EPI_BF16)
             o = torch.empty((T, Cs), dtype=torch.bfloat16, device=dev)
-            self._ln(x, self.w[f"backbone.norm{si}.weight"], self.w[f"backbone.norm{si}.bias"], o, T, Cs)
+            # the last block's updates, stored (patch merging reads x), and the stage's output norm
+            self._add_ln(x, p1, p2, True, self.w[f"backbone.norm{si}.weight"], self.w[f"backbone.norm{si}.bias"], o, T,
+                         Cs)
+            del p1, p2
             outs.append(o)
             if si < 3:
                 H2, W2 = g["sizes"][si + 1]
