@@ -201,7 +201,10 @@ def parity_3d(device, slice_frames=8):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import parity3d
-    out = {"tolerances": {"argmax": "bit-exact on clear joints (top-2 margin > 5e-2 max|H|)",
+    out = {"scene": "marker scene (mqhip/synth.py): two-tone joint markers in the synthetic frames and matched-"
+                    "filter ViTPose-H weights (one flip-consistent heatmap peak per joint); identical frames and "
+                    "weights in both chains",
+           "tolerances": {"argmax": "bit-exact on clear joints (top-2 margin > 5e-2 max|H|)",
                           "keypoint_px": parity3d.KP_TOL_PX,
                           "kp3d_dlt_mm_all_clear": {"median": parity3d.KP3D_DLT_MM_MEDIAN,
                                                     "p99": parity3d.KP3D_DLT_MM_P99},
