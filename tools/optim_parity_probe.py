@@ -17,9 +17,9 @@ for p in (os.path.join(ROOT, "tests"), ROOT, os.path.join(ROOT, "macaque-3d-pose
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=24)
-    ap.add_argument("--pcg", default="20,40,80,128")
-    ap.add_argument("--ftol", default="1e-3,1e-4")
-    ap.add_argument("--stop", default="0", help="MQ_TUNE_OPTIM_STOP values (key 21)")
+    ap.add_argument("--pcg", default="20,40")
+    ap.add_argument("--ftol", default="1e-3")
+    ap.add_argument("--stop", default="0,2", help="MQ_TUNE_OPTIM_STOP values (key 21)")
     a = ap.parse_args()
     import parity3d
     from mqhip import _lib
@@ -43,26 +43,25 @@ def main():
                             for f in a.ftol.split(",")]:
         _lib.check(lib.mq_set_tuning(4, pcg), "pcg")
         _lib.check(lib.mq_set_tuning(21, stop), "stop")
-        if True:
-            t0 = time.perf_counter()
-            p3, jl, stats, _ = optim_points_batch(
-                cg, pts, init, cons, weak, scale_smooth=tri["scale_smooth"], scale_length=tri["scale_length"],
-                scale_length_weak=tri["scale_length_weak"], reproj_error_threshold=tri["reproj_error_threshold"],
-                n_deriv_smooth=tri["n_deriv_smooth"], ftol=ftol, return_stats=True)
-            ms = (time.perf_counter() - t0) * 1e3
-            rows = []
-            for b, i in enumerate(run):
-                p2, targs, cost = ora["problems"][i]
-                r = ora["cgroup"]._error_fun_triangulation(np.hstack([p3[b].ravel(), jl[b]]), p2, *targs)
-                d = np.linalg.norm(p3[b] - ora["kp3d_tight"][i], axis=-1)
-                d = d[np.isfinite(d)]
-                st = np.asarray(stats).reshape(len(run), -1)[b]
-                rows.append({"ind": i, "cost_ratio": round(0.5 * float(r @ r) / cost, 5),
-                             "to_converged_mm_p50_p99": [round(float(np.median(d)), 3), round(float(np.percentile(d, 99)), 2)],
-                             "iters": int(st[2]), "status": int(st[3])})
-            print(json.dumps({"pcg": pcg, "stop": stop, "ftol": ftol, "ms": round(ms, 1), "rows": rows}), flush=True)
-    _lib.check(lib.mq_set_tuning(4, 20), "pcg")
-    _lib.check(lib.mq_set_tuning(21, 0), "stop")
+        t0 = time.perf_counter()
+        p3, jl, stats, _ = optim_points_batch(
+            cg, pts, init, cons, weak, scale_smooth=tri["scale_smooth"], scale_length=tri["scale_length"],
+            scale_length_weak=tri["scale_length_weak"], reproj_error_threshold=tri["reproj_error_threshold"],
+            n_deriv_smooth=tri["n_deriv_smooth"], ftol=ftol, return_stats=True)
+        ms = (time.perf_counter() - t0) * 1e3
+        rows = []
+        for b, i in enumerate(run):
+            p2, targs, cost = ora["problems"][i]
+            r = ora["cgroup"]._error_fun_triangulation(np.hstack([p3[b].ravel(), jl[b]]), p2, *targs)
+            d = np.linalg.norm(p3[b] - ora["kp3d_tight"][i], axis=-1)
+            d = d[np.isfinite(d)]
+            st = np.asarray(stats).reshape(len(run), -1)[b]
+            rows.append({"ind": i, "cost_ratio": round(0.5 * float(r @ r) / cost, 5),
+                         "to_converged_mm_p50_p99": [round(float(np.median(d)), 3), round(float(np.percentile(d, 99)), 2)],
+                         "iters": int(st[2]), "status": int(st[3])})
+        print(json.dumps({"pcg": pcg, "stop": stop, "ftol": ftol, "ms": round(ms, 1), "rows": rows}), flush=True)
+    _lib.check(lib.mq_set_tuning(4, 40), "pcg")      # the ABI-5 defaults
+    _lib.check(lib.mq_set_tuning(21, 2), "stop")
     band = np.linalg.norm(ora["kp3d"] - ora["kp3d_tight"], axis=-1)
     print(json.dumps({"scipy_1e-3_to_converged_mm_p50_p99": [round(float(np.nanmedian(band)), 3),
                                                             round(float(np.nanpercentile(band, 99)), 2)]}))
