@@ -370,7 +370,10 @@ def lift_gpu(device, reps=3):
             f"optim {1e3 * (t5 - t4):.1f} ms, reproj {1e3 * (t6 - t5):.1f} ms")
     med = {k: float(np.median(v[1:])) * 1e3 for k, v in times.items()}
     tot = sum(med.values())
+    import hashlib
+    digest = hashlib.sha256(np.ascontiguousarray(res).tobytes() + np.ascontiguousarray(jl).tobytes()).hexdigest()[:16]
     return {"gpu_ms": {k: round(v, 3) for k, v in med.items()}, "total_ms": round(tot, 3),
+            "optim_result_sha256_16": digest,
             "individuals_frames_per_s": round(A * F / (tot * 1e-3), 2),
             "optim_lm_iterations": stats[:, 2].tolist(), "statistic": f"median of {reps} after 1 warm-up",
             "workload": f"BASELINE config 4: {F} frames x {C} views x {A} individuals x {J} joints, ransac + optim",

@@ -20,6 +20,10 @@ from . import _lib
 
 LOSSES = {"linear": 0, "soft_l1": 1, "huber": 2}
 
+# Set to a list to record every optim_points_batch call (problem size, LM steps per individual, wall ms):
+# the config-3 clip driver (tools/run_clip_sharded.py) reports step 4's solver work from it.
+CALL_LOG = None
+
 
 def prepare_batch(p3ds, constraints, constraints_weak, scale_smooth):
     """x0 (B, F*J*3 + n_strong + n_weak) and scale_smooth_full (B) for every animal, exactly as the
@@ -76,6 +80,8 @@ def optim_points_batch(cgroup, points, p3ds, constraints=(), constraints_weak=()
     ssf_h = np.ascontiguousarray(np.array(ssf, dtype=np.float64))
     stats = np.zeros((B, 4), dtype=np.float64)
     import ctypes
+    import time
+    t0 = time.perf_counter()
     rc = ctx.lib.mq_optim_points(
         ctx.handle, _lib.ptr(cams), C, _lib.ptr(p2_d), _lib.ptr(x_d), B, F, J,
         allc.ctypes.data_as(ctypes.c_void_p), nS, nW, ssf_h.ctypes.data_as(ctypes.c_void_p),
@@ -84,6 +90,9 @@ def optim_points_batch(cgroup, points, p3ds, constraints=(), constraints_weak=()
         stats.ctypes.data_as(ctypes.c_void_p), _lib.stream_ptr(dev))
     _lib.check(rc, "mq_optim_points")
     x = x_d.cpu().numpy()
+    if CALL_LOG is not None:
+        CALL_LOG.append({"B": B, "F": F, "J": J, "lm_steps": stats[:, 2].astype(int).tolist(),
+                         "status": stats[:, 3].astype(int).tolist(), "ms": round((time.perf_counter() - t0) * 1e3, 2)})
     if verbose:
         for b in range(B):
             print(f"optim_points[{b}]: cost {stats[b, 0]:.6g} -> {stats[b, 1]:.6g} in {int(stats[b, 2])} LM steps")

@@ -23,6 +23,7 @@ def open_lib(path):
     lib.mq_gemm_bf16.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]
     lib.mq_attention_bf16.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp]
     lib.mq_layernorm.argtypes = [vp, vp, vp, vp, vp, i32, i32, C.c_float, i32, vp]
+    lib.mq_add_layernorm.argtypes = [vp, vp, vp, vp, i32, vp, vp, vp, i32, i32, C.c_float, vp]
     ctx = vp()
     assert lib.mq_create(0, C.byref(ctx)) == 0
     return lib, ctx
@@ -37,6 +38,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--attention", action="store_true")
     ap.add_argument("--layernorm", action="store_true", help="also time mq_layernorm (ViT-H rows, bf16 and f32 out)")
+    ap.add_argument("--add-layernorm", action="store_true",
+                    help="also time mq_add_layernorm at the bench's rows, 64 images x 192 tokens (x += p1 [+ p2], stored or not)")
     args = ap.parse_args()
     import torch
     libs = {"A": open_lib(args.a), "B": open_lib(args.b)}
@@ -114,6 +117,40 @@ def main():
                           flush=True)
             print(f"layernorm out_f32={out_f32}: A and B bit-identical = {bool(torch.equal(outs['A'], outs['B']))}",
                   flush=True)
+
+    if args.add_layernorm:
+        rows, dim = 64 * 192, 1280
+        x0 = torch.randn((rows, dim), generator=g, device=dev) * 3 + 0.5
+        p1 = torch.randn((rows, dim), generator=g, device=dev).to(torch.bfloat16)
+        p2 = torch.randn((rows, dim), generator=g, device=dev).to(torch.bfloat16)
+        gam = torch.randn((dim,), generator=g, device=dev)
+        bet = torch.randn((dim,), generator=g, device=dev)
+        for nadd, store in ((2, 1), (1, 0), (2, 0)):
+            outs = {}
+            for rnd in range(args.rounds):
+                for key, (lib, ctx) in libs.items():
+                    x = x0.clone()
+                    y = torch.empty((rows, dim), device=dev, dtype=torch.bfloat16)
+                    q2 = P(p2) if nadd == 2 else None
+                    run = lambda: lib.mq_add_layernorm(ctx, P(x), P(p1), q2, store, P(gam), P(bet), P(y), rows, dim,  # noqa
+                                                       1e-6, s)
+                    assert run() == 0
+                    torch.cuda.synchronize()
+                    outs.setdefault(key, (x.clone(), y.clone()))
+                    for _ in range(2):
+                        run()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(args.iters):
+                        run()
+                    e1.record()
+                    torch.cuda.synchronize()
+                    us = e0.elapsed_time(e1) / args.iters * 1e3
+                    nbytes = rows * dim * (4 + 2 * nadd + 4 * store + 2)
+                    print(f"add_layernorm nadd={nadd} store={store} {key} r={rnd}: {us:.2f} us  "
+                          f"{nbytes / (us * 1e-6) / 1e12:.2f} TB/s", flush=True)
+            same = torch.equal(outs["A"][0], outs["B"][0]) and torch.equal(outs["A"][1], outs["B"][1])
+            print(f"add_layernorm nadd={nadd} store={store}: A and B bit-identical = {same}", flush=True)
 
 
 if __name__ == "__main__":

@@ -71,6 +71,8 @@ def main():
     del w
     id_model = None if a.no_id else "random"
     times = {}
+    from mqhip import optim as _optim
+    _optim.CALL_LOG = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run_demo.proc(a.data, 24, res, f"cuda:{local}", cfg_path, os.path.join(a.root, "videos"), 17,
@@ -88,7 +90,7 @@ def main():
                           "world": world,
                           "backend": os.environ.get("MQ_DIST_BACKEND", "nccl") if dist.is_initialized() else None,
                           "id_classifier": not a.no_id, "seconds": {k: round(v, 4) for k, v in times.items()},
-                          "total_s": round(total, 4),
+                          "total_s": round(total, 4), "optim_points_calls": _optim.CALL_LOG,
                           "individuals_frames_per_s": round(a.animals * a.frames / total, 2)}), flush=True)
     if dist.is_initialized():
         dist.barrier()
