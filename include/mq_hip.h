@@ -47,8 +47,10 @@ extern "C" {
  *   4 -- mq_alldata_json (host: step 1's alldata.json text from row arrays) added.
  *   5 -- mq_add_layernorm added; tuning key MQ_TUNE_OPTIM_STOP (21) added; optim_points defaults to 40 PCG iterations per LM step and
  *        the ftol test on two accepted steps in a row (it lands closer to the converged solution than
- *        scipy's own ftol stop on ViT-derived 2D). */
-#define MQ_ABI_VERSION 5
+ *        scipy's own ftol stop on ViT-derived 2D).
+ *   6 -- MQ_TUNE_OPTIM_STOP bit 4: the ftol test at ftol / 2; default 6 (two steps in a row at ftol / 2: at or
+ *        below scipy's cost on every marker scene probed, where ftol alone stopped 1.5 % above it on one). */
+#define MQ_ABI_VERSION 6
 
 typedef struct mq_ctx mq_ctx;
 typedef struct mq_vitpose mq_vitpose;
@@ -74,8 +76,8 @@ const char* mq_last_error(void);
                                        contiguous) for the attention's loads; 0: row-major (same results) */
 #define MQ_TUNE_OPTIM_STOP 21       /* optim_points' stop rule on an accepted LM step, bits: 0 = scipy's ftol test
                                        alone (dF < ftol F); 1 = and the step's actual / predicted reduction > 0.25
-                                       (scipy trf's condition); 2 (default) = the test passed on two accepted steps
-                                       in a row */
+                                       (scipy trf's condition); 2 = the test passed on two accepted steps in a row;
+                                       4 = the test at ftol / 2.  Default 6 (2 | 4) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

@@ -165,7 +165,7 @@ int mq_set_tuning(int key, int value) {
       g_qkv_head_major = value != 0;
       break;
     case MQ_TUNE_OPTIM_STOP:
-      if (value < 0 || value > 3) return fail("mq_set_tuning: optim stop rule must be in [0, 3]", -2);
+      if (value < 0 || value > 7) return fail("mq_set_tuning: optim stop rule must be in [0, 7]", -2);
       mq::g_optim_stop = value;
       break;
     default:

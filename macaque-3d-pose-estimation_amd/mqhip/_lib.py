@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmq_hip.so"))
-ABI_VERSION = 5  # include/mq_hip.h MQ_ABI_VERSION
+ABI_VERSION = 6  # include/mq_hip.h MQ_ABI_VERSION
 
 EXPORTED = [
     "mq_abi_version", "mq_last_error", "mq_set_tuning", "mq_get_tuning", "mq_create", "mq_destroy",

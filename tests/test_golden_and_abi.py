@@ -114,7 +114,7 @@ def test_library_exports_every_header_symbol(lib):
     for s in syms:
         assert hasattr(lib, s), f"libmq_hip.so does not export {s}"
     assert sorted(_lib.EXPORTED) == syms
-    assert lib.mq_abi_version() == 5
+    assert lib.mq_abi_version() == 6
 
 
 def test_library_is_gfx950_code_object(lib):
@@ -128,7 +128,7 @@ def test_last_error_is_safe_without_gpu(lib):
     assert isinstance(lib.mq_last_error(), bytes)
 
 
-OPTIM_STOP_DEFAULT = 2   # include/mq_hip.h MQ_TUNE_OPTIM_STOP
+OPTIM_STOP_DEFAULT = 6   # include/mq_hip.h MQ_TUNE_OPTIM_STOP
 
 
 def test_tuning_knobs_only_select_equivalent_variants(lib):
@@ -145,7 +145,7 @@ def test_tuning_knobs_only_select_equivalent_variants(lib):
         assert lib.mq_get_tuning(key) == other
         assert lib.mq_set_tuning(key, default) == 0
     assert lib.mq_set_tuning(4, 0) == -2
-    assert lib.mq_set_tuning(21, 4) == -2
+    assert lib.mq_set_tuning(21, 8) == -2
 
 
 def test_context_ignores_tuning_environment():

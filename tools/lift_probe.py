@@ -21,7 +21,13 @@ def main():
     import torch
     from mqhip import _lib
     if args.lib:  # after torch: torch's HIP runtime must be the one the library binds to
-        _lib.load(args.lib)
+        import ctypes
+        probe = ctypes.CDLL(os.path.abspath(args.lib))
+        for name in list(_lib._SIGS):  # an older build may lack newer entry points
+            if not hasattr(probe, name):
+                del _lib._SIGS[name]
+        _lib.ABI_VERSION = probe.mq_abi_version()  # an A/B build may predate the current ABI
+        _lib.load(os.path.abspath(args.lib))
     _lib.apply_tuning_env(_lib.load())
     import bench
     print(json.dumps(bench.lift_gpu(0, reps=args.reps)), flush=True)
