@@ -34,10 +34,13 @@ def weights():
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("n_frames", [1, 24])
-def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames):
+@pytest.mark.parametrize("n_frames,seed", [(1, 7), (24, 7), (24, 8), (24, 9)])
+def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames, seed):
+    """Seeds 8 and 9 are further marker scenes (other skeletons and marker noise) for the same statements:
+    the ABI-5 solver stop missed SOLVER_COST_RATIO on seed 8 (1.015x), the ABI-6 one passes all three
+    (profiles/r04p_parity3d_seeds_8_9.log, r04t_parity3d_seeds_8_9_abi6.log)."""
     import parity3d
-    fig, hip, ora = parity3d.run(n_frames=n_frames, weights=weights)
+    fig, hip, ora = parity3d.run(n_frames=n_frames, seed=seed, weights=weights)
     print("parity3d", json.dumps(fig))
     assert fig["argmax_equal_on_clear"] == 1.0
     assert fig["clear_fraction"] >= parity3d.CLEAR_MIN

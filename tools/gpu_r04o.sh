@@ -1,6 +1,8 @@
-# optim_points matvec with its loads issued up front: config-4 lift A/B against lib_base (timing + result
-# digest, bit-identity expected), the config-3 clip (step-4 solver calls logged), the optim GPU tests, then
-# the lift's kernel profile.  First failure ends the call.
+# optim_points PCG latency work: config-4 lift A/B (timing + result digest, bit-identity expected) of lib
+# (everything: matvec loads up front, p.q reduced by the matvec's last block, precond staging before the
+# done check, G / H / I blocks in registers, interleaved rz butterflies, the factor's smoothness couplings precomputed) against lib_base and the partial
+# builds lib_pq / lib_pq2 / lib_pq3, the config-3 clip (step-4 solver calls logged), the optim GPU tests,
+# then the lift's kernel profile.  First failure ends the call.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
