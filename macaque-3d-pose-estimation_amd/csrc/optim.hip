@@ -363,10 +363,36 @@ __device__ __forceinline__ void len_partials(const OptDims& D, const double* __r
                                              const double* __restrict__ lenJ, double (*pa)[OPT_MAXL],
                                              double (*pb)[OPT_MAXL], int t) {
   const int ch = t / 32;
+  constexpr int UF = 512 / OPT_RCH;  // frames per chunk held in registers: every load of a clip up to 512 frames in flight at once
   for (int l = t % 32; l < D.NL; l += 32) {
     double a = 0, bsum = 0;
-#pragma unroll 8
-    for (int f = ch; f < D.F; f += OPT_RCH) {
+    double va[UF], vb[UF];
+#pragma unroll
+    for (int k = 0; k < UF; ++k) {
+      const int f = ch + k * OPT_RCH;
+      va[k] = vb[k] = 0.0;
+      if (f < D.F) {
+        if (qLf) {
+          va[k] = qLf[(size_t)f * D.NL + l];
+        } else {
+          const double* q = lenJ + ((size_t)f * D.NL + l) * 5;
+          va[k] = q[4];
+          vb[k] = q[3];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < UF; ++k) {  // the sums in ascending frame order, as before
+      if (ch + k * OPT_RCH < D.F) {
+        if (qLf) {
+          a += va[k];
+        } else {
+          a += va[k] * vb[k];
+          bsum += vb[k] * vb[k];
+        }
+      }
+    }
+    for (int f = ch + UF * OPT_RCH; f < D.F; f += OPT_RCH) {  // longer clips (global-memory route)
       if (qLf) {
         a += qLf[(size_t)f * D.NL + l];
       } else {
@@ -1438,6 +1464,27 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_matvec_kernel(OptDims D, Op
   }
   const double lam = Bf.ctl[2 * b];
   const double ssf = Bf.ssf[b];
+  // z and the previous direction of the 2n + 1 frames this block couples, loaded before the done check too
+  const double* Pp = (it & 1) ? Bf.P0 : Bf.P1;
+  constexpr int NW = 2 * OPT_MAXN + 1;
+  double zv[NW], pv[NW], zl = 0.0, pl = 0.0;
+  if (t < J3) {
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int ff = f + w - n;
+      zv[w] = pv[w] = 0.0;
+      if (w <= 2 * n && ff >= 0 && ff < F) {
+        const size_t o = base + (size_t)ff * J3 + t;
+        zv[w] = Bf.z[o];
+        if (it > 0) pv[w] = Pp[o];
+      }
+    }
+  }
+  if (t < NL && !D.fix) {
+    const size_t o = base + D.NX + t;
+    zl = Bf.z[o];
+    if (it > 0) pl = Pp[o];
+  }
   // pcg_done and beta from the same three rz reads
   double rz3[3];
   rz_at_n<3>(D, Bf, b, {0, it, it > 0 ? it - 1 : 0}, rz3);
@@ -1447,23 +1494,21 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_matvec_kernel(OptDims D, Op
   if (!(r0 > 0) || (it > 0 && !(ri > D.tol2 * r0))) return;  // pcg_done: the whole block
   const double beta = it == 0 ? 0.0 : ri / rim;
   double* Pc = (it & 1) ? Bf.P1 : Bf.P0;
-  const double* Pp = (it & 1) ? Bf.P0 : Bf.P1;
   if (t < J3) {
-    for (int df = -n; df <= n; ++df) {
-      const int ff = f + df;
-      if (ff < 0 || ff >= F) continue;
-      const size_t o = base + (size_t)ff * J3 + t;
-      const double p = it == 0 ? Bf.z[o] : Bf.z[o] + beta * Pp[o];
-      sp[df + n][t] = p;
-      if (df == 0) Pc[o] = p;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int ff = f + w - n;
+      if (w > 2 * n || ff < 0 || ff >= F) continue;
+      const double p = it == 0 ? zv[w] : zv[w] + beta * pv[w];
+      sp[w][t] = p;
+      if (w == n) Pc[base + (size_t)ff * J3 + t] = p;
     }
   }
-  if (t < D.NL) {
+  if (t < NL) {
     double p = 0;
     if (!D.fix) {
-      const size_t o = base + D.NX + t;
-      p = it == 0 ? Bf.z[o] : Bf.z[o] + beta * Pp[o];
-      if (f == 0) Pc[o] = p;
+      p = it == 0 ? zl : zl + beta * pl;
+      if (f == 0) Pc[base + D.NX + t] = p;
     }
     spL[t] = p;
   }
@@ -1510,14 +1555,15 @@ __global__ void __launch_bounds__(OPT_THREADS) optim_matvec_kernel(OptDims D, Op
 // matvec 4x slower, profiles/r04p_*.)
 __global__ void __launch_bounds__(OPT_RTHREADS) optim_reduce_pq_kernel(OptDims D, OptBufs Bf, int it) {
   const int b = blockIdx.x, t = threadIdx.x;
-  if (pcg_done(D, Bf, b, it)) return;
   __shared__ double red[OPT_RTHREADS];
   const double* P = (it & 1) ? Bf.P1 : Bf.P0;
   const size_t base = (size_t)b * D.NV;
   __shared__ double part[OPT_RCH][OPT_MAXL];
   double s = 0;
+  // the partial loads go out before the "PCG finished" check (stale values are then only discarded)
   for (int f = t; f < D.F; f += OPT_RTHREADS) s += Bf.pqF[(size_t)b * D.F + f];
   if (!D.fix) len_partials(D, Bf.qLf + (size_t)b * D.F * D.NL, nullptr, part, nullptr, t);
+  if (pcg_done(D, Bf, b, it)) return;  // the whole block
   __syncthreads();
   if (!D.fix && t < D.NL) {
     double qL = len_combine(part, t);
