@@ -49,8 +49,11 @@ extern "C" {
  *        the ftol test on two accepted steps in a row (it lands closer to the converged solution than
  *        scipy's own ftol stop on ViT-derived 2D).
  *   6 -- MQ_TUNE_OPTIM_STOP bit 4: the ftol test at ftol / 2; default 6 (two steps in a row at ftol / 2: at or
- *        below scipy's cost on every marker scene probed, where ftol alone stopped 1.5 % above it on one). */
-#define MQ_ABI_VERSION 6
+ *        below scipy's cost on every marker scene probed, where ftol alone stopped 1.5 % above it on one).
+ *   7 -- mq_optim_points takes a solver (0: scipy's trust-region-reflective + lsmr, restated -- the default and
+ *        the parity mode; 1: the Levenberg-Marquardt + PCG solver of ABI 1-6) and writes 8 stats per animal;
+ *        tuning key MQ_TUNE_OPTIM_TRF_CHUNK (22) added. */
+#define MQ_ABI_VERSION 7
 
 typedef struct mq_ctx mq_ctx;
 typedef struct mq_vitpose mq_vitpose;
@@ -77,7 +80,9 @@ const char* mq_last_error(void);
 #define MQ_TUNE_OPTIM_STOP 21       /* optim_points' stop rule on an accepted LM step, bits: 0 = scipy's ftol test
                                        alone (dF < ftol F); 1 = and the step's actual / predicted reduction > 0.25
                                        (scipy trf's condition); 2 = the test passed on two accepted steps in a row;
-                                       4 = the test at ftol / 2.  Default 6 (2 | 4) */
+                                       4 = the test at ftol / 2.  Default 6 (2 | 4).  Levenberg-Marquardt solver only */
+#define MQ_TUNE_OPTIM_TRF_CHUNK 22  /* lsmr iterations the trust-region solver launches between two reads of its done
+                                       flags (default 8, 1..64; same results) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);
@@ -404,21 +409,29 @@ int mq_alldata_json(int n_frames, const int32_t* nrows, const int64_t* tid, cons
                     int J, const int64_t* assigned, const double* score, char* out, int64_t cap, int64_t* len);
 
 /* CameraGroup.optim_points (cameras.py:1116-1190) and optim_points_jointlenfix (:1192-1415) for
- * B animals at once.  Replaces scipy least_squares(trf, 2-point sparse Jacobian) with
- * Levenberg-Marquardt on the analytic Jacobian, PCG inner solves.
+ * B animals at once.  Replaces scipy least_squares (cameras.py:1166-1180: trf, 2-point sparse Jacobian,
+ * loss 'linear', ftol 1e-3; jointlenfix :1246-1260 adds max_nfev 15) on the analytic Jacobian, with
+ *   solver 0: the same algorithm, restated (scipy 1.15.3 trf_no_bounds + lsmr: damped lsmr Gauss-Newton step,
+ *             2-D subspace trust region, update_tr_radius, check_termination with ftol / xtol 1e-8 / gtol
+ *             1e-8); the parity default (csrc/optim_trf.hip);
+ *   solver 1: Levenberg-Marquardt + PCG inner solves with its own stop rule (MQ_TUNE_OPTIM_STOP): a
+ *             "converged" mode that stops later than scipy (csrc/optim.hip).
  *   p2d  device (B, C, F, J, 2) float64, NaN = missing coordinate
  *   x    device (B, F*J*3 + n_strong + n_weak) in/out: [p3d, strong lengths, weak lengths]
  *        (the reference's _initialize_params_triangulation layout, :1670-1697)
  *   constraints host int32 (n_strong + n_weak, 2) joint pairs; scale_smooth_full host (B)
  *   reproj_loss 0 linear, 1 soft_l1 (reference default), 2 huber
  *   fix_lengths 1: lengths are constants (jointlenfix variant), only p3d is optimised
- *   max_iter LM iterations (reference: unbounded / max_nfev 15), ftol scipy-style on accepted steps
- *   stats host (B, 4): initial cost, final cost, LM iterations, status (1 ftol, 2 max_iter, 3 damping). */
+ *   max_iter solver 0: max_nfev (0 = scipy's default, 100 x parameters; the jointlenfix call passes 15);
+ *            solver 1: Levenberg-Marquardt iterations
+ *   stats host (B, 8): initial cost, final cost, iterations, status, then for solver 0 nfev, njev, lsmr
+ *         iterations in total, the longest lsmr run.  status, solver 0: scipy's (0 max_nfev, 1 gtol, 2 ftol,
+ *         3 xtol, 4 ftol + xtol); solver 1: 1 ftol, 2 max_iter, 3 damping overflow. */
 int mq_optim_points(mq_ctx* ctx, const double* cams, int n_cams, const double* p2d, double* x, int n_animals,
                     int n_frames, int n_joints, const int32_t* constraints, int n_strong, int n_weak,
                     const double* scale_smooth_full, double scale_length, double scale_length_weak,
                     double reproj_error_threshold, int reproj_loss, int n_deriv_smooth, int fix_lengths,
-                    int max_iter, double ftol, double* stats, void* stream);
+                    int max_iter, double ftol, int solver, double* stats, void* stream);
 
 #ifdef __cplusplus
 }

@@ -168,6 +168,10 @@ int mq_set_tuning(int key, int value) {
       if (value < 0 || value > 7) return fail("mq_set_tuning: optim stop rule must be in [0, 7]", -2);
       mq::g_optim_stop = value;
       break;
+    case MQ_TUNE_OPTIM_TRF_CHUNK:
+      if (value < 1 || value > 64) return fail("mq_set_tuning: lsmr chunk must be in [1, 64]", -2);
+      mq::g_optim_trf_chunk = value;
+      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -184,6 +188,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_GEMM_TILE64: return mq::g_gemm_tile64;
     case MQ_TUNE_QKV_HEAD_MAJOR: return g_qkv_head_major;
     case MQ_TUNE_OPTIM_STOP: return mq::g_optim_stop;
+    case MQ_TUNE_OPTIM_TRF_CHUNK: return mq::g_optim_trf_chunk;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }
@@ -1178,7 +1183,8 @@ int mq_viterbi_filter(mq_ctx* ctx, const double* kp, int A, int F, int C, int J,
 int mq_optim_points(mq_ctx* ctx, const double* cams, int C, const double* p2d, double* x, int B, int F, int J,
                     const int32_t* constraints, int n_strong, int n_weak, const double* scale_smooth_full,
                     double scale_length, double scale_length_weak, double reproj_error_threshold, int reproj_loss,
-                    int n_deriv_smooth, int fix_lengths, int max_iter, double ftol, double* stats, void* stream) {
+                    int n_deriv_smooth, int fix_lengths, int max_iter, double ftol, int solver, double* stats,
+                    void* stream) {
   if (!ctx || !cams || !p2d || !x || !scale_smooth_full || !stats) return fail("mq_optim_points: null argument");
   if (B < 0 || F < 0 || J < 0 || n_strong < 0 || n_weak < 0) return fail("mq_optim_points: negative size", -2);
   if ((int64_t)B * F * J == 0) return 0;
@@ -1187,16 +1193,31 @@ int mq_optim_points(mq_ctx* ctx, const double* cams, int C, const double* p2d, d
   if (n_deriv_smooth < 1 || n_deriv_smooth > 3) return fail("mq_optim_points: n_deriv_smooth must be 1..3", -2);
   if (reproj_loss < 0 || reproj_loss > 2) return fail("mq_optim_points: loss must be 0 linear, 1 soft_l1, 2 huber", -2);
   if (!(reproj_error_threshold > 0)) return fail("mq_optim_points: reproj_error_threshold must be > 0", -2);
+  if (solver != 0 && solver != 1) return fail("mq_optim_points: solver must be 0 (trf) or 1 (lm)", -2);
+  if (max_iter < 0) return fail("mq_optim_points: max_iter must be >= 0", -2);
   if (n_strong + n_weak > 0 && !constraints) return fail("mq_optim_points: null constraints");
   for (int k = 0; k < 2 * (n_strong + n_weak); ++k)
     if (constraints[k] < 0 || constraints[k] >= J) return fail("mq_optim_points: constraint joint out of range", -2);
   HIP_TRY(hipSetDevice(ctx->device));
-  if (ctx->optim_ws.ensure(mq::optim_workspace_bytes(B, F, J, n_strong + n_weak)))
-    return fail("optim workspace alloc failed", -5);
-  const int rc = mq::optim_points(cams, C, p2d, x, B, F, J, constraints, n_strong, n_weak, scale_smooth_full,
-                                  scale_length, scale_length_weak, reproj_error_threshold, reproj_loss,
-                                  n_deriv_smooth, fix_lengths, max_iter, ftol, ctx->optim_ws.p, stats,
-                                  (hipStream_t)stream);
+  const int NL = n_strong + n_weak;
+  int rc;
+  if (solver == 0) {
+    if (ctx->optim_ws.ensure(mq::optim_trf_workspace_bytes(B, F, J, C, NL)))
+      return fail("optim workspace alloc failed", -5);
+    rc = mq::optim_points_trf(cams, C, p2d, x, B, F, J, constraints, n_strong, n_weak, scale_smooth_full, scale_length,
+                              scale_length_weak, reproj_error_threshold, reproj_loss, n_deriv_smooth, fix_lengths,
+                              max_iter, ftol, ctx->optim_ws.p, stats, (hipStream_t)stream);
+  } else {
+    if (ctx->optim_ws.ensure(mq::optim_workspace_bytes(B, F, J, NL))) return fail("optim workspace alloc failed", -5);
+    std::vector<double> st4(4 * (size_t)B, 0.0);
+    rc = mq::optim_points(cams, C, p2d, x, B, F, J, constraints, n_strong, n_weak, scale_smooth_full, scale_length,
+                          scale_length_weak, reproj_error_threshold, reproj_loss, n_deriv_smooth, fix_lengths,
+                          max_iter > 0 ? max_iter : 200, ftol, ctx->optim_ws.p, st4.data(), (hipStream_t)stream);
+    for (int b = 0; b < B; ++b) {
+      for (int i = 0; i < 4; ++i) stats[8 * b + i] = st4[4 * b + i];
+      for (int i = 4; i < 8; ++i) stats[8 * b + i] = 0.0;
+    }
+  }
   if (rc != 0) return fail("mq_optim_points: solver failed (" + std::to_string(rc) + ")", -6);
   return 0;
 }

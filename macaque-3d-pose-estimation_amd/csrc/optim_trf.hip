@@ -1,0 +1,1213 @@
+// optim_points, scipy-faithful solver (row a16; the parity default since ABI 7).
+//
+// The reference refines 3D points with scipy.optimize.least_squares(method='trf', jac_sparsity=...,
+// loss='linear', ftol=1e-3) (cameras.py:1166-1180).  Without bounds and with a sparse Jacobian that is
+// scipy 1.15.3's trf_no_bounds with tr_solver='lsmr' (optimize/_lsq/trf.py:401-540), restated step for step:
+//   * J and g = J^T f at every accepted x; gtol / max_nfev tests at the top of the loop;
+//   * the damping of the lsmr step from the 1-D quadratic along -g inside the trust region (regularize);
+//   * gn = lsmr(J, f, damp) with atol = btol = 1e-6, conlim 1e8, maxiter min(m, n)  (sparse/linalg lsmr.py);
+//   * S = orth([g, gn]), B_S = (J S)^T (J S), g_S = S^T g; solve_trust_region_2d; update_tr_radius;
+//     check_termination (ftol with the ratio > 0.25 condition, xtol 1e-8).
+// oracle/trf.py restates the same algorithm in this file's phase order and is pinned bit for bit against scipy
+// (tests/test_oracle_trf.py).  What differs here: the Jacobian is analytic (scipy: 2-point differences, which
+// move scipy's own answer by < 0.2 mm on the marker scenes, profiles/r05*), and the reductions run in a fixed
+// order of their own (so floating-point results are not scipy's bits).
+//
+// Work decomposition (one animal = one independent problem; B animals per call, batched in every launch):
+//   * a workgroup owns a block of TRF_FB consecutive frames of one animal: its reprojection rows (camera x
+//     joint x {u, v}), smoothness rows (np.diff order n, row i at frame i) and limb-length rows (m space), and
+//     its 3 J parameters per frame (n space); the length variables belong to block 0;
+//   * lsmr is two launches per iteration: phase 1 (u = J v - alpha u; the previous iteration's recurrences and
+//     the x / h / hbar updates), phase 2 (the previous iteration's stop test, then v = J^T u - beta v).  Every
+//     workgroup reduces the norms it needs from the previous launch's per-block partials itself, in the same
+//     fixed order, so every workgroup holds the same scalars bit for bit and no launch waits on another
+//     workgroup.  The host checks the per-animal done flags every few iterations;
+//   * the trust-region logic (2x2 subproblem, radius, termination) runs on the host from the partials.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "camera.hpp"
+#include "common.hpp"
+#include "optim_dev.hpp"
+
+namespace mq {
+namespace {
+
+constexpr int TRF_THREADS = 256;
+constexpr int TRF_FB = 4;  // frames per workgroup
+constexpr int TRF_MAXJ = 32, TRF_MAXL = 64, TRF_MAXN = 3;
+constexpr int TRF_NS = 24;  // lsmr state doubles per slot
+
+struct TrfDims {
+  int B, C, F, J, NL, nS, fix, n, loss;
+  int NX, NV, MR, MRrep, NB;
+  double rp, s_len, s_len_weak;
+  double c[TRF_MAXN + 1];
+  double atol, btol, ctol;
+};
+
+struct TrfBufs {
+  const double* cams;
+  const double* p2d;
+  const int* cons;
+  const double* ssf;
+  const int* act;  // [B] the animal takes part in this launch
+  int* done;       // [B] lsmr finished
+  double *fres, *ftr, *Jrep, *lenJ;
+  double *g, *u, *vraw, *vn, *h, *hbar, *xl, *s1, *s2;
+  double* fpart;  // [B][NB][4]: sum r^2 at x, sum r^2 at the trial point, rows
+  double* fL;     // [B][NB][NL]: sum over the block's frames of dL * r_len at x
+  double* upart;  // [2][B][NB]
+  double* vpart;  // [2][B][NB][2]: sum v^2, max |v|
+  double* xpart;  // [2][B][NB]
+  double* Lpart;  // [B][NB][NL]
+  double* npart;  // [B][NB][4]
+  double* jpart;  // [B][NB][4]
+  double* st;     // [2][B][TRF_NS]
+  double* lctl;   // [B][4]: damp, normb, maxiter, final lsmr itn
+  double* coef;   // [B][4]
+};
+
+// Sum over the workgroup; every thread returns the same bits (xor butterflies add the same two values,
+// commuted, and the wave sums combine in one fixed order).
+__device__ __forceinline__ double block_sum_all(double v, double* red) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const double s = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return s;
+}
+
+__device__ __forceinline__ double block_max_all(double v, double* red) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) v = fmax(v, __shfl_xor(v, m));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const double s = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  __syncthreads();
+  return s;
+}
+
+// sum_i p[i * stride] over i < count, the same value in every thread of every workgroup that asks
+__device__ __forceinline__ double reduce_parts(const double* __restrict__ p, int count, int stride, double* red) {
+  double v = 0.0;
+  for (int i = threadIdx.x; i < count; i += TRF_THREADS) v += p[(size_t)i * stride];
+  return block_sum_all(v, red);
+}
+
+// scipy.sparse.linalg._isolve.lsqr._sym_ortho (np.sign(0) = 0)
+__device__ __forceinline__ double sgn0(double a) { return a > 0 ? 1.0 : (a < 0 ? -1.0 : 0.0); }
+__device__ __forceinline__ void sym_ortho(double a, double b, double& c, double& s, double& r) {
+  if (b == 0) {
+    c = sgn0(a);
+    s = 0;
+    r = fabs(a);
+  } else if (a == 0) {
+    c = 0;
+    s = sgn0(b);
+    r = fabs(b);
+  } else if (fabs(b) > fabs(a)) {
+    const double tau = a / b;
+    s = sgn0(b) / sqrt(1 + tau * tau);
+    c = s * tau;
+    r = b / s;
+  } else {
+    const double tau = b / a;
+    c = sgn0(a) / sqrt(1 + tau * tau);
+    s = c * tau;
+    r = a / c;
+  }
+}
+
+// lsmr state slot
+enum {
+  S_ALPHABAR, S_RHO, S_RHOBAR, S_CBAR, S_SBAR, S_ZETABAR, S_ZETA, S_BETADD, S_BETAD, S_RHODOLD, S_TAUTILDEOLD,
+  S_THETATILDE, S_D, S_NORMA2, S_MAXRBAR, S_MINRBAR, S_ITN, S_NORMR, S_NORMAR, S_NORMA, S_CONDA
+};
+
+// ---------------------------------------------------------------------------------------------------------
+// Residuals (and, mode 1, the Jacobian) at x for the block's frames.  fout: m vector [B][F][MR]:
+//   [(j C + c) 2 + comp] reprojection (0 where the coordinate is NaN), [MRrep + 3 j + k] smoothness (frames
+//   f < F - n), [MRrep + 3 J + l] limb lengths.  Partials: sum r^2 (slot 0 at x / 1 at a trial point), rows.
+__global__ void __launch_bounds__(TRF_THREADS) trf_eval_kernel(TrfDims D, TrfBufs Bf, const double* __restrict__ x,
+                                                              double* __restrict__ fout, int mode) {
+  const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  if (!Bf.act[b]) return;
+  const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL;
+  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
+  __shared__ double sx[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3];
+  __shared__ double sL[TRF_MAXL];
+  __shared__ int scons[2 * TRF_MAXL];
+  __shared__ double sLr[TRF_FB][TRF_MAXL];
+  __shared__ double red[4];
+  const double* xb = x + (size_t)b * D.NV;
+  const int nfx = min(nf + n, F - f0);
+  for (int i = t; i < nfx * J3; i += TRF_THREADS) sx[i] = xb[(size_t)f0 * J3 + i];
+  if (t < NL) sL[t] = xb[D.NX + t];
+  if (t < 2 * NL) scons[t] = Bf.cons[t];
+  __syncthreads();
+  const double ssf = Bf.ssf[b];
+  double cost = 0.0, rows = 0.0;
+  const int nrep = J * C, ntask = nrep + J3 + NL;
+  for (int task = t; task < nf * ntask; task += TRF_THREADS) {
+    const int fl = task / ntask, r = task - fl * ntask, f = f0 + fl;
+    double* fo = fout + ((size_t)b * F + f) * D.MR;
+    if (r < nrep) {  // reprojection (cameras.py:1579-1590): rho(|p2d - project(X)|) per non-NaN coordinate
+      const int j = r / C, c = r - j * C;
+      const double* pp = Bf.p2d + ((((size_t)b * C + c) * F + f) * J + j) * 2;
+      const double px = pp[0], py = pp[1];
+      double res[2] = {0.0, 0.0}, jr[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+      if (!(isnan(px) && isnan(py))) {
+        const double X[3] = {sx[fl * J3 + 3 * j], sx[fl * J3 + 3 * j + 1], sx[fl * J3 + 3 * j + 2]};
+        double pu, pv, Ju[3], Jv[3];
+        project_jac(cam_at(Bf.cams, c), X, pu, pv, Ju, Jv);
+#pragma unroll
+        for (int comp = 0; comp < 2; ++comp) {
+          const double obs = comp ? py : px;
+          if (isnan(obs)) continue;
+          double rr, dr;
+          reproj_loss(obs - (comp ? pv : pu), D.rp, D.loss, rr, dr);
+          res[comp] = rr;
+          cost += rr * rr;
+          rows += 1.0;
+          const double* Jp = comp ? Jv : Ju;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) jr[3 * comp + k] = -dr * Jp[k];
+        }
+      }
+      fo[2 * r] = res[0];
+      fo[2 * r + 1] = res[1];
+      if (mode == 1) {
+        double* jo = Bf.Jrep + (((size_t)b * F + f) * nrep + r) * 6;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) jo[k] = jr[k];
+      }
+    } else if (r < nrep + J3) {  // smoothness: np.diff(p3ds, n, axis=0) * scale_smooth (:1595)
+      const int q = r - nrep;
+      double val = 0.0;
+      if (f < F - n) {
+        double d[TRF_MAXN + 1];
+        for (int m = 0; m <= n; ++m) d[m] = sx[(fl + m) * J3 + q];
+        for (int o = 0; o < n; ++o)
+          for (int m = 0; m < n - o; ++m) d[m] = d[m + 1] - d[m];
+        val = d[0] * ssf;
+        cost += val * val;
+        rows += 1.0;
+      }
+      fo[D.MRrep + q] = val;
+    } else {  // limb lengths (:1597-1616): 100 (|Xa - Xb| - L) / L * scale
+      const int l = r - nrep - J3;
+      const int a = scons[2 * l], c2 = scons[2 * l + 1];
+      const double L = sL[l], s = l < D.nS ? D.s_len : D.s_len_weak;
+      const double dx = sx[fl * J3 + 3 * a] - sx[fl * J3 + 3 * c2];
+      const double dy = sx[fl * J3 + 3 * a + 1] - sx[fl * J3 + 3 * c2 + 1];
+      const double dz = sx[fl * J3 + 3 * a + 2] - sx[fl * J3 + 3 * c2 + 2];
+      const double nr = sqrt(dx * dx + dy * dy + dz * dz);
+      const double val = 100 * (nr - L) / L * s;
+      cost += val * val;
+      rows += 1.0;
+      fo[D.MRrep + J3 + l] = val;
+      if (mode == 1) {
+        const double k = nr > 0 ? s * 100 / L / nr : 0.0;
+        double* lo = Bf.lenJ + (((size_t)b * F + f) * NL + l) * 4;
+        lo[0] = k * dx;
+        lo[1] = k * dy;
+        lo[2] = k * dz;
+        lo[3] = -s * 100 * nr / (L * L);
+        sLr[fl][l] = lo[3] * val;
+      }
+    }
+  }
+  cost = block_sum_all(cost, red);
+  rows = block_sum_all(rows, red);
+  double* fp = Bf.fpart + ((size_t)b * D.NB + blk) * 4;
+  if (t == 0) {
+    fp[mode == 1 ? 0 : 1] = cost;
+    fp[2] = rows;
+  }
+  if (mode == 1 && t < NL) {
+    double s = 0.0;
+    for (int fl = 0; fl < nf; ++fl) s += sLr[fl][t];
+    Bf.fL[((size_t)b * D.NB + blk) * NL + t] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// v = J^T (u / beta) - beta vn for the block's parameters (and block 0's length variables).
+//   MODE 0: g = J^T f (u = fres, beta = 1, no vn); partials (sum g^2, max |g|) in vpart slot 0
+//   MODE 1: lsmr's start, v = J^T (f / normb)
+//   MODE 2: lsmr phase 2 of iteration k: first the stop test of iteration k - 1 (phase 1 of iteration k
+//           ran its recurrences and wrote x_{k-1}), then v = J^T (u / beta_k) - beta_k v_{k-1}.
+template <int MODE>
+__global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs Bf, int k) {
+  const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  if (!Bf.act[b]) return;
+  if (MODE > 0 && Bf.done[b]) return;
+  const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
+  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
+  const int par = k & 1;
+  __shared__ double red[4];
+  __shared__ double slen[TRF_FB][TRF_MAXL][3];
+  __shared__ int scons[2 * TRF_MAXL];
+  extern __shared__ double su[];  // m rows of frames [f0 - n, f0 + nf), normalised
+  const double* uin = MODE == 2 ? Bf.u : Bf.fres;
+  // loads that do not depend on the norms go out first
+  const int fa = max(0, f0 - n), nrow = (f0 + nf - fa) * D.MR;
+  const double* ub = uin + ((size_t)b * F + fa) * D.MR;
+  for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
+  for (int i = t; i < nf * NL * 3; i += TRF_THREADS) {
+    const int fl = i / (NL * 3), rem = i - fl * NL * 3, l = rem / 3, kk = rem - 3 * l;
+    slen[fl][l][kk] = Bf.lenJ[(((size_t)b * F + f0 + fl) * NL + l) * 4 + kk];
+  }
+  double beta = 1.0;
+  if (MODE == 1) beta = Bf.lctl[4 * b + 1];
+  if (MODE == 2) {
+    beta = sqrt(reduce_parts(Bf.upart + ((size_t)par * D.B + b) * NB, NB, 1, red));
+    if (k >= 2) {  // the stop test of iteration k - 1 (lsmr.py:413-441)
+      const double* S = Bf.st + ((size_t)par * D.B + b) * TRF_NS;
+      const double normx = sqrt(reduce_parts(Bf.xpart + ((size_t)par * D.B + b) * NB, NB, 1, red));
+      const double normb = Bf.lctl[4 * b + 1], maxiter = Bf.lctl[4 * b + 2];
+      const double normr = S[S_NORMR], normar = S[S_NORMAR], normA = S[S_NORMA], condA = S[S_CONDA];
+      const double itn = S[S_ITN];
+      const double test1 = normr / normb;
+      const double test2 = (normA * normr) != 0 ? normar / (normA * normr) : INFINITY;
+      const double test3 = 1 / condA;
+      const double t1 = test1 / (1 + normA * normx / normb);
+      const double rtol = D.btol + D.atol * normA * normx / normb;
+      int istop = 0;
+      if (itn >= maxiter) istop = 7;
+      if (1 + test3 <= 1) istop = 6;
+      if (1 + test2 <= 1) istop = 5;
+      if (1 + t1 <= 1) istop = 4;
+      if (test3 <= D.ctol) istop = 3;
+      if (test2 <= D.atol) istop = 2;
+      if (test1 <= rtol) istop = 1;
+      if (istop) {
+        if (blk == 0 && t == 0) {
+          Bf.done[b] = istop;
+          Bf.lctl[4 * b + 3] = itn;
+        }
+        return;
+      }
+    }
+  }
+  const double ib = 1.0 / beta;
+  for (int i = t; i < nrow; i += TRF_THREADS) su[i] = ub[i] * ib;
+  __syncthreads();
+  const double ssf = Bf.ssf[b];
+  const size_t nb = (size_t)b * D.NV;
+  double vsq = 0.0, vmax = 0.0;
+  const int nrep = J * C;
+  for (int task = t; task < nf * J3; task += TRF_THREADS) {
+    const int fl = task / J3, q = task - fl * J3, j = q / 3, kk = q - 3 * j, f = f0 + fl;
+    const double* uf = su + (size_t)(f - fa) * D.MR;
+    const double* jr = Bf.Jrep + (((size_t)b * F + f) * nrep + (size_t)j * C) * 6;
+    double acc = 0.0;
+    for (int c = 0; c < C; ++c) {
+      acc += jr[6 * c + kk] * uf[2 * (j * C + c)];
+      acc += jr[6 * c + 3 + kk] * uf[2 * (j * C + c) + 1];
+    }
+    for (int m = 0; m <= n; ++m) {  // smoothness rows i = f - m hold frame f with coefficient c[m]
+      const int i = f - m;
+      if (i >= 0 && i < F - n) acc += ssf * D.c[m] * su[(size_t)(i - fa) * D.MR + D.MRrep + q];
+    }
+    for (int l = 0; l < NL; ++l) {
+      const int a = scons[2 * l], c2 = scons[2 * l + 1];
+      if (a == j) acc += slen[fl][l][kk] * uf[D.MRrep + J3 + l];
+      else if (c2 == j) acc -= slen[fl][l][kk] * uf[D.MRrep + J3 + l];
+    }
+    const size_t o = nb + (size_t)f * J3 + q;
+    const double v = MODE == 2 ? Bf.vn[o] * -beta + acc : acc;
+    (MODE == 0 ? Bf.g : Bf.vraw)[o] = v;
+    vsq += v * v;
+    vmax = fmax(vmax, fabs(v));
+  }
+  if (blk == 0 && t < NL) {  // the length variables: sum over frames of dL * u_len
+    const size_t o = nb + D.NX + t;
+    double v = 0.0;
+    if (!D.fix) {
+      const double* lp = (MODE == 2 ? Bf.Lpart : Bf.fL) + (size_t)b * NB * NL + t;
+      double s = 0.0;
+      for (int bb = 0; bb < NB; ++bb) s += lp[(size_t)bb * NL];
+      const double acc = s * ib;
+      v = MODE == 2 ? Bf.vn[o] * -beta + acc : acc;
+      vsq += v * v;
+      vmax = fmax(vmax, fabs(v));
+    }
+    (MODE == 0 ? Bf.g : Bf.vraw)[o] = v;
+  }
+  vsq = block_sum_all(vsq, red);
+  vmax = block_max_all(vmax, red);
+  if (t == 0) {
+    double* vp = Bf.vpart + (((size_t)par * D.B + b) * NB + blk) * 2;
+    vp[0] = vsq;
+    vp[1] = vmax;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// lsmr phase 1 of iteration k (k >= 1): alpha_{k-1}, beta_{k-1} from the partials; FIRST (k = 1) starts the
+// recurrences (lsmr.py:205-239), otherwise runs iteration k - 1's (:301-410) and updates hbar, x, h; then
+// u_k = J v_{k-1} - alpha_{k-1} u_{k-1} for the block's rows.
+__device__ __forceinline__ void lsmr_recurrence(double* S, double alpha, double beta, double damp, double& chb,
+                                                double& cx, double& ch) {
+  double chat, shat, alphahat;
+  sym_ortho(S[S_ALPHABAR], damp, chat, shat, alphahat);
+  const double rhoold = S[S_RHO];
+  double c, s, rho;
+  sym_ortho(alphahat, beta, c, s, rho);
+  const double thetanew = s * alpha;
+  S[S_ALPHABAR] = c * alpha;
+  const double rhobarold = S[S_RHOBAR];
+  const double zetaold = S[S_ZETA];
+  const double thetabar = S[S_SBAR] * rho;
+  const double rhotemp = S[S_CBAR] * rho;
+  double cbar, sbar, rhobar;
+  sym_ortho(S[S_CBAR] * rho, thetanew, cbar, sbar, rhobar);
+  const double zeta = cbar * S[S_ZETABAR];
+  const double zetabar = -sbar * S[S_ZETABAR];
+  chb = -(thetabar * rho / (rhoold * rhobarold));
+  cx = zeta / (rho * rhobar);
+  ch = -(thetanew / rho);
+  const double betaacute = chat * S[S_BETADD];
+  const double betacheck = -shat * S[S_BETADD];
+  const double betahat = c * betaacute;
+  const double betadd = -s * betaacute;
+  const double thetatildeold = S[S_THETATILDE];
+  double ctildeold, stildeold, rhotildeold;
+  sym_ortho(S[S_RHODOLD], thetabar, ctildeold, stildeold, rhotildeold);
+  const double thetatilde = stildeold * rhobar;
+  const double rhodold = ctildeold * rhobar;
+  const double betad = -stildeold * S[S_BETAD] + ctildeold * betahat;
+  const double tautildeold = (zetaold - thetatildeold * S[S_TAUTILDEOLD]) / rhotildeold;
+  const double taud = (zeta - thetatilde * tautildeold) / rhodold;
+  const double d = S[S_D] + betacheck * betacheck;
+  const double bt = betad - taud;
+  const double normr = sqrt(d + bt * bt + betadd * betadd);
+  double normA2 = S[S_NORMA2] + beta * beta;
+  const double normA = sqrt(normA2);
+  normA2 = normA2 + alpha * alpha;
+  const double itn = S[S_ITN] + 1;
+  const double maxrbar = fmax(S[S_MAXRBAR], rhobarold);
+  const double minrbar = itn > 1 ? fmin(S[S_MINRBAR], rhobarold) : S[S_MINRBAR];
+  const double condA = fmax(maxrbar, rhotemp) / fmin(minrbar, rhotemp);
+  S[S_RHO] = rho;
+  S[S_RHOBAR] = rhobar;
+  S[S_CBAR] = cbar;
+  S[S_SBAR] = sbar;
+  S[S_ZETABAR] = zetabar;
+  S[S_ZETA] = zeta;
+  S[S_BETADD] = betadd;
+  S[S_BETAD] = betad;
+  S[S_RHODOLD] = rhodold;
+  S[S_TAUTILDEOLD] = tautildeold;
+  S[S_THETATILDE] = thetatilde;
+  S[S_D] = d;
+  S[S_NORMA2] = normA2;
+  S[S_MAXRBAR] = maxrbar;
+  S[S_MINRBAR] = minrbar;
+  S[S_ITN] = itn;
+  S[S_NORMR] = normr;
+  S[S_NORMAR] = fabs(zetabar);
+  S[S_NORMA] = normA;
+  S[S_CONDA] = condA;
+}
+
+template <bool FIRST>
+__global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBufs Bf, int k) {
+  const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  if (!Bf.act[b] || Bf.done[b]) return;
+  const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
+  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
+  const int par = k & 1, pp = par ^ 1;
+  __shared__ double red[4];
+  __shared__ double sv[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3];
+  __shared__ double sL[TRF_MAXL];
+  __shared__ double sLu[TRF_FB][TRF_MAXL];
+  __shared__ int scons[2 * TRF_MAXL];
+  __shared__ double sS[TRF_NS];
+  __shared__ double scoef[4];
+  for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
+  const double alpha = sqrt(reduce_parts(Bf.vpart + ((size_t)pp * D.B + b) * NB * 2, NB, 2, red));
+  const double beta = FIRST ? Bf.lctl[4 * b + 1] : sqrt(reduce_parts(Bf.upart + ((size_t)pp * D.B + b) * NB, NB, 1, red));
+  const size_t nb = (size_t)b * D.NV;
+  if (t == 0) {
+    double* S = sS;
+    double chb = 0.0, cx = 0.0, ch = 0.0;
+    if (FIRST) {
+      for (int i = 0; i < TRF_NS; ++i) S[i] = 0.0;
+      S[S_ZETABAR] = alpha * beta;
+      S[S_ALPHABAR] = alpha;
+      S[S_RHO] = 1;
+      S[S_RHOBAR] = 1;
+      S[S_CBAR] = 1;
+      S[S_SBAR] = 0;
+      S[S_BETADD] = beta;
+      S[S_RHODOLD] = 1;
+      S[S_NORMA2] = alpha * alpha;
+      S[S_MINRBAR] = 1e+100;
+      S[S_ITN] = 0;
+    } else {
+      const double* Sp = Bf.st + ((size_t)pp * D.B + b) * TRF_NS;
+      for (int i = 0; i < TRF_NS; ++i) S[i] = Sp[i];
+      lsmr_recurrence(S, alpha, beta, Bf.lctl[4 * b], chb, cx, ch);
+    }
+    scoef[0] = chb;
+    scoef[1] = cx;
+    scoef[2] = ch;
+    if (blk == 0) {
+      double* So = Bf.st + ((size_t)par * D.B + b) * TRF_NS;
+      for (int i = 0; i < TRF_NS; ++i) So[i] = S[i];
+    }
+  }
+  __syncthreads();
+  if (FIRST && !(alpha * beta != 0)) {  // normar == 0 (or normb == 0): x = 0 (lsmr.py:247-256)
+    for (int i = t; i < nf * J3; i += TRF_THREADS) Bf.xl[nb + (size_t)f0 * J3 + i] = 0.0;
+    if (blk == 0 && t < NL) Bf.xl[nb + D.NX + t] = 0.0;
+    if (blk == 0 && t == 0) {
+      Bf.done[b] = 8;
+      Bf.lctl[4 * b + 3] = 0;
+    }
+    return;
+  }
+  const double chb = scoef[0], cx = scoef[1], ch = scoef[2];
+  const double ia = 1.0 / alpha;
+  // n space: v_{k-1} = v_raw / alpha (scipy's in-place v *= 1 / alpha), staged with the halo frames
+  const int nfx = min(nf + n, F - f0);
+  double xsq = 0.0;
+  for (int i = t; i < nfx * J3; i += TRF_THREADS) {
+    const size_t o = nb + (size_t)f0 * J3 + i;
+    const double v = Bf.vraw[o] * ia;
+    sv[i] = v;
+    if (i < nf * J3) {
+      Bf.vn[o] = v;
+      if (FIRST) {
+        Bf.h[o] = v;
+        Bf.hbar[o] = 0.0;
+        Bf.xl[o] = 0.0;
+      } else {
+        const double hb = Bf.hbar[o] * chb + Bf.h[o];
+        const double xv = Bf.xl[o] + cx * hb;
+        Bf.hbar[o] = hb;
+        Bf.xl[o] = xv;
+        Bf.h[o] = Bf.h[o] * ch + v;
+        xsq += xv * xv;
+      }
+    }
+  }
+  if (t < NL) {
+    double v = 0.0;
+    if (!D.fix) {
+      const size_t o = nb + D.NX + t;
+      v = Bf.vraw[o] * ia;
+      if (blk == 0) {
+        Bf.vn[o] = v;
+        if (FIRST) {
+          Bf.h[o] = v;
+          Bf.hbar[o] = 0.0;
+          Bf.xl[o] = 0.0;
+        } else {
+          const double hb = Bf.hbar[o] * chb + Bf.h[o];
+          const double xv = Bf.xl[o] + cx * hb;
+          Bf.hbar[o] = hb;
+          Bf.xl[o] = xv;
+          Bf.h[o] = Bf.h[o] * ch + v;
+          xsq += xv * xv;
+        }
+      }
+    }
+    sL[t] = v;
+  }
+  __syncthreads();
+  // m space: u_k = (u_{k-1} / beta) * -alpha + J v   (lsmr.py:284-286)
+  const double ib = 1.0 / beta;
+  const double* uin = FIRST ? Bf.fres : Bf.u;
+  const double ssf = Bf.ssf[b];
+  const int nrep = J * C, ntask = nrep + J3 + NL;
+  double usq = 0.0;
+  for (int task = t; task < nf * ntask; task += TRF_THREADS) {
+    const int fl = task / ntask, r = task - fl * ntask, f = f0 + fl;
+    const size_t mo = ((size_t)b * F + f) * D.MR;
+    if (r < nrep) {
+      const int j = r / C;
+      const double* jr = Bf.Jrep + (((size_t)b * F + f) * nrep + r) * 6;
+      const double* v = sv + fl * J3 + 3 * j;
+#pragma unroll
+      for (int comp = 0; comp < 2; ++comp) {
+        const double jv = jr[3 * comp] * v[0] + jr[3 * comp + 1] * v[1] + jr[3 * comp + 2] * v[2];
+        const double un = (uin[mo + 2 * r + comp] * ib) * -alpha + jv;
+        Bf.u[mo + 2 * r + comp] = un;
+        usq += un * un;
+      }
+    } else if (r < nrep + J3) {
+      const int q = r - nrep;
+      double un = 0.0;
+      if (f < F - n) {
+        double jv = 0.0;
+        for (int m = 0; m <= n; ++m) jv += ssf * D.c[m] * sv[(fl + m) * J3 + q];
+        un = (uin[mo + D.MRrep + q] * ib) * -alpha + jv;
+      }
+      Bf.u[mo + D.MRrep + q] = un;
+      usq += un * un;
+    } else {
+      const int l = r - nrep - J3;
+      const int a = scons[2 * l], c2 = scons[2 * l + 1];
+      const double* lj = Bf.lenJ + (((size_t)b * F + f) * NL + l) * 4;
+      double jv = lj[0] * (sv[fl * J3 + 3 * a] - sv[fl * J3 + 3 * c2]) +
+                  lj[1] * (sv[fl * J3 + 3 * a + 1] - sv[fl * J3 + 3 * c2 + 1]) +
+                  lj[2] * (sv[fl * J3 + 3 * a + 2] - sv[fl * J3 + 3 * c2 + 2]);
+      if (!D.fix) jv += lj[3] * sL[l];
+      const double un = (uin[mo + D.MRrep + J3 + l] * ib) * -alpha + jv;
+      Bf.u[mo + D.MRrep + J3 + l] = un;
+      usq += un * un;
+      sLu[fl][l] = lj[3] * un;
+    }
+  }
+  usq = block_sum_all(usq, red);
+  if (!FIRST) xsq = block_sum_all(xsq, red);
+  if (t == 0) {
+    Bf.upart[((size_t)par * D.B + b) * NB + blk] = usq;
+    if (!FIRST) Bf.xpart[((size_t)par * D.B + b) * NB + blk] = xsq;
+  }
+  if (t < NL) {
+    double s = 0.0;
+    for (int fl = 0; fl < nf; ++fl) s += sLu[fl][t];
+    Bf.Lpart[((size_t)b * NB + blk) * NL + t] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// m-space products J a (and J c) without storage: partials sum (Ja)^2, sum (Jc)^2, sum (Ja)(Jc).
+__global__ void __launch_bounds__(TRF_THREADS) trf_jv_kernel(TrfDims D, TrfBufs Bf, const double* __restrict__ va,
+                                                            const double* __restrict__ vc) {
+  const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  if (!Bf.act[b]) return;
+  const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL;
+  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
+  __shared__ double red[4];
+  __shared__ double sa[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3], sc[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3];
+  __shared__ double saL[TRF_MAXL], scL[TRF_MAXL];
+  __shared__ int scons[2 * TRF_MAXL];
+  const size_t nb = (size_t)b * D.NV;
+  const int nfx = min(nf + n, F - f0);
+  for (int i = t; i < nfx * J3; i += TRF_THREADS) {
+    sa[i] = va[nb + (size_t)f0 * J3 + i];
+    sc[i] = vc ? vc[nb + (size_t)f0 * J3 + i] : 0.0;
+  }
+  if (t < NL) {
+    saL[t] = D.fix ? 0.0 : va[nb + D.NX + t];
+    scL[t] = (D.fix || !vc) ? 0.0 : vc[nb + D.NX + t];
+  }
+  if (t < 2 * NL) scons[t] = Bf.cons[t];
+  __syncthreads();
+  const double ssf = Bf.ssf[b];
+  const int nrep = J * C, ntask = nrep + J3 + NL;
+  double saa = 0.0, scc = 0.0, sac = 0.0;
+  for (int task = t; task < nf * ntask; task += TRF_THREADS) {
+    const int fl = task / ntask, r = task - fl * ntask, f = f0 + fl;
+    if (r < nrep) {
+      const int j = r / C;
+      const double* jr = Bf.Jrep + (((size_t)b * F + f) * nrep + r) * 6;
+      const double* a = sa + fl * J3 + 3 * j;
+      const double* c = sc + fl * J3 + 3 * j;
+#pragma unroll
+      for (int comp = 0; comp < 2; ++comp) {
+        const double ja = jr[3 * comp] * a[0] + jr[3 * comp + 1] * a[1] + jr[3 * comp + 2] * a[2];
+        const double jc = jr[3 * comp] * c[0] + jr[3 * comp + 1] * c[1] + jr[3 * comp + 2] * c[2];
+        saa += ja * ja;
+        scc += jc * jc;
+        sac += ja * jc;
+      }
+    } else if (r < nrep + J3) {
+      const int q = r - nrep;
+      if (f < F - n) {
+        double ja = 0.0, jc = 0.0;
+        for (int m = 0; m <= n; ++m) {
+          ja += ssf * D.c[m] * sa[(fl + m) * J3 + q];
+          jc += ssf * D.c[m] * sc[(fl + m) * J3 + q];
+        }
+        saa += ja * ja;
+        scc += jc * jc;
+        sac += ja * jc;
+      }
+    } else {
+      const int l = r - nrep - J3;
+      const int a = scons[2 * l], c2 = scons[2 * l + 1];
+      const double* lj = Bf.lenJ + (((size_t)b * F + f) * NL + l) * 4;
+      double ja = 0.0, jc = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk) {
+        ja += lj[kk] * (sa[fl * J3 + 3 * a + kk] - sa[fl * J3 + 3 * c2 + kk]);
+        jc += lj[kk] * (sc[fl * J3 + 3 * a + kk] - sc[fl * J3 + 3 * c2 + kk]);
+      }
+      ja += lj[3] * saL[l];
+      jc += lj[3] * scL[l];
+      saa += ja * ja;
+      scc += jc * jc;
+      sac += ja * jc;
+    }
+  }
+  saa = block_sum_all(saa, red);
+  scc = block_sum_all(scc, red);
+  sac = block_sum_all(sac, red);
+  if (t == 0) {
+    double* jp = Bf.jpart + ((size_t)b * D.NB + blk) * 4;
+    jp[0] = saa;
+    jp[1] = scc;
+    jp[2] = sac;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// n-space operations of the trust-region step, with per-block partials in npart[b][blk][0..2]:
+//   0 XNORM  x.x
+//   1 DOTS   g.gn, gn.gn                            (gn = lsmr's x)
+//   2 S1T    s1 = g * c0;  s2 = gn - c1 * s1;  s2.s2  (Gram-Schmidt of [g, gn])
+//   3 S2     s2 = s2 * c2;  g.s1, g.s2
+//   4 STEP   xt = x + (s1 p0 + s2 p1);  step.step
+//   5 ACCEPT x = xt
+enum { OP_XNORM, OP_DOTS, OP_S1T, OP_S2, OP_STEP, OP_ACCEPT };
+__global__ void __launch_bounds__(TRF_THREADS) trf_nops_kernel(TrfDims D, TrfBufs Bf, double* __restrict__ x,
+                                                              double* __restrict__ xt, int op) {
+  const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
+  if (!Bf.act[b]) return;
+  const int J3 = 3 * D.J, F = D.F;
+  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
+  __shared__ double red[4];
+  const double* cf = Bf.coef + 4 * (size_t)b;
+  const size_t nb = (size_t)b * D.NV;
+  double p0 = 0.0, p1 = 0.0;
+  auto one = [&](size_t o) {
+    switch (op) {
+      case OP_XNORM: p0 += x[o] * x[o]; break;
+      case OP_DOTS: p0 += Bf.g[o] * Bf.xl[o]; p1 += Bf.xl[o] * Bf.xl[o]; break;
+      case OP_S1T: {
+        const double s1 = Bf.g[o] * cf[0];
+        const double tt = Bf.xl[o] - cf[1] * s1;
+        Bf.s1[o] = s1;
+        Bf.s2[o] = tt;
+        p0 += tt * tt;
+        break;
+      }
+      case OP_S2: {
+        const double s2 = Bf.s2[o] * cf[2];
+        Bf.s2[o] = s2;
+        p0 += Bf.g[o] * Bf.s1[o];
+        p1 += Bf.g[o] * s2;
+        break;
+      }
+      case OP_STEP: {
+        const double st = Bf.s1[o] * cf[0] + Bf.s2[o] * cf[1];
+        xt[o] = x[o] + st;
+        p0 += st * st;
+        break;
+      }
+      default: x[o] = xt[o]; break;
+    }
+  };
+  for (int i = t; i < nf * J3; i += TRF_THREADS) one(nb + (size_t)f0 * J3 + i);
+  if (blk == 0 && t < D.NL) {
+    const size_t o = nb + D.NX + t;
+    if (!D.fix) one(o);
+    else if (op == OP_STEP) xt[o] = x[o];  // the fixed lengths ride along
+    else if (op == OP_XNORM) p0 += 0.0;
+  }
+  p0 = block_sum_all(p0, red);
+  p1 = block_sum_all(p1, red);
+  if (t == 0) {
+    double* np = Bf.npart + ((size_t)b * D.NB + blk) * 4;
+    np[0] = p0;
+    np[1] = p1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Host: the 2-D trust-region subproblem (common.py solve_trust_region_2d).  np.roots of the quartic is
+// replaced by its real roots found by bracketing between the critical points (the roots of the derivative,
+// recursively) and bisecting; a root the polynomial only touches is not bracketed (numpy's companion
+// eigenvalues of such a root are a near-real complex pair, excluded there too unless exactly real).
+double poly_eval(const double* c, int d, double t) {
+  double v = c[0];
+  for (int i = 1; i <= d; ++i) v = v * t + c[i];
+  return v;
+}
+
+void poly_real_roots(const double* cin, int din, std::vector<double>& out) {
+  out.clear();
+  int s = 0;
+  while (s <= din && cin[s] == 0.0) ++s;  // leading zeros (np.roots strips them)
+  const int d = din - s;
+  if (d <= 0) return;
+  const double* c = cin + s;
+  if (d == 1) {
+    out.push_back(-c[1] / c[0]);
+    return;
+  }
+  if (d == 2) {
+    const double disc = c[1] * c[1] - 4 * c[0] * c[2];
+    if (disc < 0) return;
+    const double q = -0.5 * (c[1] + (c[1] >= 0 ? sqrt(disc) : -sqrt(disc)));
+    if (q != 0) {
+      out.push_back(q / c[0]);
+      out.push_back(c[2] / q);
+    } else {
+      out.push_back(0.0);
+      out.push_back(0.0);
+    }
+    std::sort(out.begin(), out.end());
+    return;
+  }
+  double dc[8];
+  for (int i = 0; i < d; ++i) dc[i] = c[i] * (d - i);
+  std::vector<double> crit;
+  poly_real_roots(dc, d - 1, crit);
+  double R = 0.0;
+  for (int i = 1; i <= d; ++i) R = std::max(R, std::fabs(c[i] / c[0]));
+  R += 1.0;
+  std::vector<double> pts;
+  pts.push_back(-R);
+  for (double x : crit)
+    if (x > -R && x < R) pts.push_back(x);
+  pts.push_back(R);
+  std::sort(pts.begin(), pts.end());
+  for (size_t i = 0; i + 1 < pts.size(); ++i) {
+    double a = pts[i], b = pts[i + 1];
+    double fa = poly_eval(c, d, a), fb = poly_eval(c, d, b);
+    if (fa == 0.0) {
+      if (out.empty() || out.back() != a) out.push_back(a);
+      continue;
+    }
+    if (fb == 0.0 || (fa < 0) == (fb < 0)) continue;
+    for (int it = 0; it < 200; ++it) {
+      const double m = 0.5 * (a + b);
+      if (m <= a || m >= b) break;
+      const double fm = poly_eval(c, d, m);
+      if (fm == 0.0) {
+        a = b = m;
+        break;
+      }
+      if ((fm < 0) == (fa < 0)) {
+        a = m;
+        fa = fm;
+      } else {
+        b = m;
+      }
+    }
+    out.push_back(0.5 * (a + b));
+  }
+  if (poly_eval(c, d, pts.back()) == 0.0) out.push_back(pts.back());
+}
+
+void solve_trust_region_2d(const double B[3], const double g[2], double Delta, double p[2]) {
+  // cho_factor (upper) + cho_solve, p = -B^-1 g, if B is positive definite and p lies inside
+  const double b00 = B[0], b01 = B[1], b11 = B[2];
+  if (b00 > 0) {
+    const double r00 = std::sqrt(b00), r01 = b01 / r00, s = b11 - r01 * r01;
+    if (s > 0) {
+      const double r11 = std::sqrt(s);
+      const double y0 = g[0] / r00, y1 = (g[1] - r01 * y0) / r11;  // R^T y = g
+      const double q1 = y1 / r11, q0 = (y0 - r01 * q1) / r00;      // R q = y
+      const double pn0 = -q0, pn1 = -q1;
+      if (pn0 * pn0 + pn1 * pn1 <= Delta * Delta) {
+        p[0] = pn0;
+        p[1] = pn1;
+        return;
+      }
+    }
+  }
+  const double a = b00 * Delta * Delta, b = b01 * Delta * Delta, c = b11 * Delta * Delta;
+  const double d = g[0] * Delta, f = g[1] * Delta;
+  const double co[5] = {-b + d, 2 * (a - c + f), 6 * b, 2 * (-a + c + f), -b - d};
+  std::vector<double> ts;
+  poly_real_roots(co, 4, ts);
+  double best = std::numeric_limits<double>::infinity();
+  p[0] = 0.0;
+  p[1] = -Delta;
+  bool any = false;
+  for (double tt : ts) {
+    const double q0 = Delta * (2 * tt / (1 + tt * tt)), q1 = Delta * ((1 - tt * tt) / (1 + tt * tt));
+    const double val = 0.5 * (q0 * (b00 * q0 + b01 * q1) + q1 * (b01 * q0 + b11 * q1)) + (g[0] * q0 + g[1] * q1);
+    if (!any || val < best) {
+      best = val;
+      p[0] = q0;
+      p[1] = q1;
+      any = true;
+    }
+  }
+}
+
+}  // namespace
+
+int g_optim_trf_chunk = 8;  // lsmr iterations launched between two reads of the done flags
+
+size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL) {
+  const size_t NV = (size_t)F * J * 3 + NL, MR = (size_t)J * C * 2 + (size_t)J * 3 + NL;
+  const size_t NB = ((size_t)F + TRF_FB - 1) / TRF_FB;
+  size_t n = 0;
+  n += (size_t)B * F * MR * 3;           // fres ftr u
+  n += (size_t)B * F * J * C * 6;        // Jrep
+  n += (size_t)B * F * NL * 4;           // lenJ
+  n += (size_t)B * NV * 10;              // g vraw vn h hbar xl s1 s2 xt (+1)
+  n += (size_t)B * NB * (4 + NL + 2 + 4 + 2 + NL + 4 + 4);  // fpart fL upart vpart xpart Lpart npart jpart
+  n += 2 * (size_t)B * TRF_NS + (size_t)B * 8;
+  n += (size_t)NL + 2 + 2 * (size_t)B + 16;  // cons, act, done, ssf
+  return n * sizeof(double) + 256;
+}
+
+// Host driver (the trf_no_bounds loop).  x: device (B, NV) in/out.  stats[8 b + ...]: 0 initial cost, 1 final
+// cost, 2 iterations (njev - 1), 3 status (scipy's: 0 max_nfev, 1 gtol, 2 ftol, 3 xtol, 4 ftol and xtol),
+// 4 nfev, 5 njev, 6 lsmr iterations in total, 7 largest lsmr run.
+int optim_points_trf(const double* cams, int C, const double* p2d, double* x, int B, int F, int J, const int* cons_host,
+                     int n_strong, int n_weak, const double* ssf_host, double scale_length, double scale_length_weak,
+                     double rp, int loss, int n_deriv, int fix_lengths, int max_nfev_arg, double ftol, void* ws,
+                     double* stats, hipStream_t s) {
+  const int NL = n_strong + n_weak;
+  if (B <= 0 || F <= 0 || J <= 0) return 0;
+  if (J > TRF_MAXJ || NL > TRF_MAXL || C > 16 || C < 1 || n_deriv < 1 || n_deriv > TRF_MAXN) return -2;
+  TrfDims D{};
+  D.B = B;
+  D.C = C;
+  D.F = F;
+  D.J = J;
+  D.NL = NL;
+  D.nS = n_strong;
+  D.fix = fix_lengths;
+  D.n = n_deriv;
+  D.loss = loss;
+  D.NX = F * J * 3;
+  D.NV = D.NX + NL;
+  D.MRrep = J * C * 2;
+  D.MR = D.MRrep + J * 3 + NL;
+  D.NB = (F + TRF_FB - 1) / TRF_FB;
+  D.rp = rp;
+  D.s_len = scale_length;
+  D.s_len_weak = scale_length_weak;
+  D.atol = 1e-6;
+  D.btol = 1e-6;
+  D.ctol = 1.0 / 1e8;
+  {
+    int binom = 1;
+    for (int m = 0; m <= n_deriv; ++m) {
+      D.c[m] = (((n_deriv - m) & 1) ? -1.0 : 1.0) * binom;
+      binom = binom * (n_deriv - m) / (m + 1);
+    }
+  }
+  const int NB = D.NB;
+  const size_t NVB = (size_t)B * D.NV, MB = (size_t)B * F * D.MR;
+  double* w = static_cast<double*>(ws);
+  auto take = [&](size_t cnt) {
+    double* p = w;
+    w += cnt;
+    return p;
+  };
+  TrfBufs Bf{};
+  Bf.fres = take(MB);
+  Bf.ftr = take(MB);
+  Bf.u = take(MB);
+  Bf.Jrep = take((size_t)B * F * J * C * 6);
+  Bf.lenJ = take((size_t)B * F * NL * 4);
+  Bf.g = take(NVB);
+  Bf.vraw = take(NVB);
+  Bf.vn = take(NVB);
+  Bf.h = take(NVB);
+  Bf.hbar = take(NVB);
+  Bf.xl = take(NVB);
+  Bf.s1 = take(NVB);
+  Bf.s2 = take(NVB);
+  double* xt = take(NVB);
+  Bf.fpart = take((size_t)B * NB * 4);
+  Bf.fL = take((size_t)B * NB * NL);
+  Bf.upart = take(2 * (size_t)B * NB);
+  Bf.vpart = take(2 * (size_t)B * NB * 2);
+  Bf.xpart = take(2 * (size_t)B * NB);
+  Bf.Lpart = take((size_t)B * NB * NL);
+  Bf.npart = take((size_t)B * NB * 4);
+  Bf.jpart = take((size_t)B * NB * 4);
+  Bf.st = take(2 * (size_t)B * TRF_NS);
+  Bf.lctl = take(4 * (size_t)B);
+  Bf.coef = take(4 * (size_t)B);
+  int* cons_d = reinterpret_cast<int*>(take(((size_t)NL * 2 + 1) / 2 + 1));
+  int* act_d = reinterpret_cast<int*>(take(((size_t)B + 1) / 2 + 1));
+  int* done_d = reinterpret_cast<int*>(take(((size_t)B + 1) / 2 + 1));
+  double* ssf_d = take(B);
+  Bf.cams = cams;
+  Bf.p2d = p2d;
+  Bf.cons = cons_d;
+  Bf.ssf = ssf_d;
+  Bf.act = act_d;
+  Bf.done = done_d;
+  auto H2D = [&](void* d, const void* h, size_t bytes) {
+    return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
+  };
+  auto D2H = [&](void* h, const void* d, size_t bytes) {
+    return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s) == hipSuccess;
+  };
+  if (NL && !H2D(cons_d, cons_host, sizeof(int) * 2 * NL)) return -3;
+  if (!H2D(ssf_d, ssf_host, sizeof(double) * B)) return -3;
+  std::vector<int> act(B, 1), doneh(B, 1);
+  if (!H2D(act_d, act.data(), sizeof(int) * B)) return -3;
+
+  const dim3 grid(NB, B), blk(TRF_THREADS);
+  const size_t jt_lds = (size_t)(TRF_FB + D.n) * D.MR * sizeof(double);
+  {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+      attr = true;
+    }
+  }
+  if (jt_lds > 120 * 1024) return -2;
+  std::vector<double> part((size_t)B * NB * 4), vp((size_t)B * NB * 2), ctl(4 * (size_t)B), coef(4 * (size_t)B, 0.0);
+  auto sync = [&]() { return hipStreamSynchronize(s) == hipSuccess; };
+  auto upload_act = [&]() { return H2D(act_d, act.data(), sizeof(int) * B); };
+  // per-animal sums of a partial field over the blocks (fixed order)
+  auto sum_field = [&](const std::vector<double>& p, int stride, int field, int b) {
+    double v = 0.0;
+    for (int k = 0; k < NB; ++k) v += p[((size_t)b * NB + k) * stride + field];
+    return v;
+  };
+  // J, f, cost at x (mode 1) and g = J^T f with its norms, for the animals in act
+  std::vector<double> cost(B), gnorm2(B), ginf(B), rows(B);
+  auto jac_and_grad = [&]() -> bool {
+    hipLaunchKernelGGL(trf_eval_kernel, grid, blk, 0, s, D, Bf, x, Bf.fres, 1);
+    hipLaunchKernelGGL(trf_jt_kernel<0>, grid, blk, jt_lds, s, D, Bf, 0);
+    if (!D2H(part.data(), Bf.fpart, sizeof(double) * part.size())) return false;
+    if (!D2H(vp.data(), Bf.vpart, sizeof(double) * vp.size())) return false;
+    if (!sync()) return false;
+    for (int b = 0; b < B; ++b) {
+      if (!act[b]) continue;
+      cost[b] = 0.5 * sum_field(part, 4, 0, b);
+      rows[b] = sum_field(part, 4, 2, b);
+      gnorm2[b] = sum_field(vp, 2, 0, b);
+      double m = 0.0;
+      for (int k = 0; k < NB; ++k) m = std::max(m, vp[((size_t)b * NB + k) * 2 + 1]);
+      ginf[b] = m;
+    }
+    return true;
+  };
+  auto nops = [&](double* xx, double* xtt, int op, bool read) -> bool {
+    hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, xx, xtt, op);
+    if (!read) return true;
+    if (!D2H(part.data(), Bf.npart, sizeof(double) * part.size())) return false;
+    return sync();
+  };
+  auto jv = [&](const double* a, const double* c) -> bool {
+    hipLaunchKernelGGL(trf_jv_kernel, grid, blk, 0, s, D, Bf, a, c);
+    if (!D2H(part.data(), Bf.jpart, sizeof(double) * part.size())) return false;
+    return sync();
+  };
+
+  const int nparam = fix_lengths ? D.NX : D.NV;
+  const long long max_nfev = max_nfev_arg > 0 ? max_nfev_arg : 100LL * (fix_lengths ? D.NX : D.NV);
+  const double xtol = 1e-8, gtol = 1e-8;
+  enum { RUN, STOP };
+  std::vector<int> state(B, RUN), status(B, 0), lsmr_total(B, 0), lsmr_max(B, 0);
+  std::vector<long long> nfev(B, 1), njev(B, 1);
+  std::vector<double> Delta(B), xnorm(B), damp(B), BS(3 * (size_t)B), gS(2 * (size_t)B), cost_new(B), actual(B);
+  if (!jac_and_grad()) return -3;
+  if (!nops(x, xt, OP_XNORM, true)) return -3;
+  for (int b = 0; b < B; ++b) {
+    stats[8 * b + 0] = cost[b];
+    xnorm[b] = std::sqrt(sum_field(part, 4, 0, b));
+    Delta[b] = xnorm[b] == 0 ? 1.0 : xnorm[b];
+  }
+  for (;;) {
+    bool any = false;
+    for (int b = 0; b < B; ++b) {
+      act[b] = 0;
+      if (state[b] != RUN) continue;
+      if (ginf[b] < gtol) status[b] = 1;  // trf.py:463-465 (ftol stops end the loop below)
+      if (status[b] != 0 || nfev[b] == max_nfev) {
+        state[b] = STOP;
+        continue;
+      }
+      act[b] = 1;
+      any = true;
+    }
+    if (!any) break;
+    if (!upload_act()) return -3;
+    // regularize: the 1-D quadratic along -g inside the trust region (trf.py:480-484)
+    if (!jv(Bf.g, nullptr)) return -3;
+    for (int b = 0; b < B; ++b) {
+      ctl[4 * b] = ctl[4 * b + 1] = ctl[4 * b + 2] = ctl[4 * b + 3] = 0.0;
+      doneh[b] = act[b] ? 0 : 1;
+      if (!act[b]) continue;
+      const double a = 0.5 * sum_field(part, 4, 0, b);
+      const double bq = -gnorm2[b];
+      const double to_tr = Delta[b] / std::sqrt(gnorm2[b]);
+      double ag = 0.0 * (a * 0.0 + bq);
+      const double y1 = to_tr * (a * to_tr + bq);
+      if (y1 < ag) ag = y1;
+      if (a != 0) {
+        const double ext = -0.5 * bq / a;
+        if (0 < ext && ext < to_tr) {
+          const double y2 = ext * (a * ext + bq);
+          if (y2 < ag) ag = y2;
+        }
+      }
+      const double reg = -ag / (Delta[b] * Delta[b]);
+      damp[b] = std::sqrt(0.0 + reg);
+      ctl[4 * b] = damp[b];
+      ctl[4 * b + 1] = std::sqrt(2.0 * cost[b]);  // norm(f)
+      ctl[4 * b + 2] = std::min(rows[b], (double)nparam);
+    }
+    if (!H2D(Bf.lctl, ctl.data(), sizeof(double) * ctl.size())) return -3;
+    if (!H2D(done_d, doneh.data(), sizeof(int) * B)) return -3;
+    // lsmr(J, f, damp)
+    hipLaunchKernelGGL(trf_jt_kernel<1>, grid, blk, jt_lds, s, D, Bf, 0);
+    int k = 1;
+    hipLaunchKernelGGL(trf_lsmr1_kernel<true>, grid, blk, 0, s, D, Bf, k);
+    hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, s, D, Bf, k);
+    ++k;
+    double maxit = 0.0;
+    for (int b = 0; b < B; ++b)
+      if (act[b]) maxit = std::max(maxit, ctl[4 * b + 2]);
+    for (;;) {
+      const int ch = std::max(1, g_optim_trf_chunk);
+      for (int i = 0; i < ch; ++i, ++k) {
+        hipLaunchKernelGGL(trf_lsmr1_kernel<false>, grid, blk, 0, s, D, Bf, k);
+        hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, s, D, Bf, k);
+      }
+      if (!D2H(doneh.data(), done_d, sizeof(int) * B)) return -3;
+      if (!sync()) return -3;
+      bool all = true;
+      for (int b = 0; b < B; ++b) all &= doneh[b] != 0;
+      if (all) break;
+      if (k > maxit + 4) return -7;  // the device test stops every run by maxiter
+    }
+    if (!D2H(ctl.data(), Bf.lctl, sizeof(double) * ctl.size())) return -3;
+    // S = orth([g, gn]) by Gram-Schmidt, B_S and g_S (trf.py:489-493)
+    if (!nops(x, xt, OP_DOTS, true)) return -3;
+    for (int b = 0; b < B; ++b) {
+      if (!act[b]) continue;
+      const int it = (int)ctl[4 * b + 3];
+      lsmr_total[b] += it;
+      lsmr_max[b] = std::max(lsmr_max[b], it);
+      const double ng = std::sqrt(gnorm2[b]);
+      coef[4 * b] = 1.0 / ng;
+      coef[4 * b + 1] = sum_field(part, 4, 0, b) / ng;  // s1 . gn
+    }
+    if (!H2D(Bf.coef, coef.data(), sizeof(double) * coef.size())) return -3;
+    if (!nops(x, xt, OP_S1T, true)) return -3;
+    for (int b = 0; b < B; ++b) {
+      if (!act[b]) continue;
+      const double nt = std::sqrt(sum_field(part, 4, 0, b));
+      coef[4 * b + 2] = nt > 0 ? 1.0 / nt : 0.0;
+    }
+    if (!H2D(Bf.coef, coef.data(), sizeof(double) * coef.size())) return -3;
+    if (!nops(x, xt, OP_S2, true)) return -3;
+    for (int b = 0; b < B; ++b) {
+      if (!act[b]) continue;
+      gS[2 * b] = sum_field(part, 4, 0, b);
+      gS[2 * b + 1] = sum_field(part, 4, 1, b);
+    }
+    if (!jv(Bf.s1, Bf.s2)) return -3;
+    for (int b = 0; b < B; ++b) {
+      if (!act[b]) continue;
+      BS[3 * b] = sum_field(part, 4, 0, b);
+      BS[3 * b + 1] = sum_field(part, 4, 2, b);
+      BS[3 * b + 2] = sum_field(part, 4, 1, b);
+    }
+    // the trial steps (trf.py:496-540), every animal until it accepts, terminates or runs out of evaluations
+    std::vector<int> trial(B, 0);
+    for (int b = 0; b < B; ++b) {
+      trial[b] = act[b];
+      actual[b] = -1;
+    }
+    std::vector<double> pred(B), step_norm(B);
+    for (;;) {
+      bool anyt = false;
+      for (int b = 0; b < B; ++b) {
+        act[b] = trial[b] && actual[b] <= 0 && nfev[b] < max_nfev;
+        trial[b] = act[b];
+        if (!act[b]) continue;
+        anyt = true;
+        double p[2];
+        solve_trust_region_2d(&BS[3 * b], &gS[2 * b], Delta[b], p);
+        coef[4 * b] = p[0];
+        coef[4 * b + 1] = p[1];
+        const double q = p[0] * (BS[3 * b] * p[0] + BS[3 * b + 1] * p[1]) + p[1] * (BS[3 * b + 1] * p[0] + BS[3 * b + 2] * p[1]);
+        pred[b] = -(0.5 * q + (p[0] * gS[2 * b] + p[1] * gS[2 * b + 1]));
+      }
+      if (!anyt) break;
+      if (!upload_act()) return -3;
+      if (!H2D(Bf.coef, coef.data(), sizeof(double) * coef.size())) return -3;
+      hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_STEP);
+      std::vector<double> stp((size_t)B * NB * 4);
+      if (!D2H(stp.data(), Bf.npart, sizeof(double) * stp.size())) return -3;
+      hipLaunchKernelGGL(trf_eval_kernel, grid, blk, 0, s, D, Bf, xt, Bf.ftr, 0);
+      if (!D2H(part.data(), Bf.fpart, sizeof(double) * part.size())) return -3;
+      if (!sync()) return -3;
+      for (int b = 0; b < B; ++b) {
+        if (!act[b]) continue;
+        nfev[b]++;
+        const double sh = std::sqrt(sum_field(stp, 4, 0, b));
+        step_norm[b] = sh;
+        const double cn = 0.5 * sum_field(part, 4, 1, b);
+        if (!std::isfinite(cn)) {
+          Delta[b] = 0.25 * sh;
+          actual[b] = -1;
+          continue;
+        }
+        cost_new[b] = cn;
+        actual[b] = cost[b] - cn;
+        double ratio;
+        if (pred[b] > 0) ratio = actual[b] / pred[b];
+        else if (pred[b] == actual[b] && actual[b] == 0) ratio = 1;
+        else ratio = 0;
+        double Dn = Delta[b];
+        if (ratio < 0.25) Dn = 0.25 * sh;
+        else if (ratio > 0.75 && sh > 0.95 * Delta[b]) Dn *= 2.0;
+        const bool ft = actual[b] < ftol * cost[b] && ratio > 0.25;
+        const bool xt_ok = sh < xtol * (xtol + xnorm[b]);
+        const int term = (ft && xt_ok) ? 4 : ft ? 2 : xt_ok ? 3 : 0;
+        if (term) {
+          status[b] = term;
+          trial[b] = 0;
+          continue;
+        }
+        Delta[b] = Dn;
+      }
+    }
+    // accepted steps: x = x_new, J at x (trf.py:522-540)
+    bool anya = false;
+    for (int b = 0; b < B; ++b) {
+      act[b] = state[b] == RUN && actual[b] > 0;
+      if (!act[b]) continue;
+      anya = true;
+      cost[b] = cost_new[b];
+      njev[b]++;
+    }
+    if (anya) {
+      if (!upload_act()) return -3;
+      if (!nops(x, xt, OP_ACCEPT, false)) return -3;
+      // the Jacobian of a terminating animal is not needed (scipy evaluates it, njev counts it)
+      for (int b = 0; b < B; ++b)
+        if (act[b] && status[b] != 0) act[b] = 0;
+      if (!upload_act()) return -3;
+      if (!jac_and_grad()) return -3;
+      if (!nops(x, xt, OP_XNORM, true)) return -3;
+      for (int b = 0; b < B; ++b)
+        if (act[b]) xnorm[b] = std::sqrt(sum_field(part, 4, 0, b));
+    }
+  }
+  for (int b = 0; b < B; ++b) {
+    stats[8 * b + 1] = cost[b];
+    stats[8 * b + 2] = (double)(njev[b] - 1);
+    stats[8 * b + 3] = status[b];
+    stats[8 * b + 4] = (double)nfev[b];
+    stats[8 * b + 5] = (double)njev[b];
+    stats[8 * b + 6] = lsmr_total[b];
+    stats[8 * b + 7] = lsmr_max[b];
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -4;
+}
+
+}  // namespace mq

@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmq_hip.so"))
-ABI_VERSION = 6  # include/mq_hip.h MQ_ABI_VERSION
+ABI_VERSION = 7  # include/mq_hip.h MQ_ABI_VERSION
 
 EXPORTED = [
     "mq_abi_version", "mq_last_error", "mq_set_tuning", "mq_get_tuning", "mq_create", "mq_destroy",
@@ -99,7 +99,7 @@ _SIGS = {
     "mq_viterbi_filter": (i32, [vp, vp, i32, i32, i32, i32, f64, i32, f64, vp, vp]),
     "mq_attention_bf16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "mq_optim_points": (i32, [vp, vp, i32, vp, vp, i32, i32, i32, vp, i32, i32, vp, f64, f64, f64, i32, i32, i32,
-                              i32, f64, vp, vp]),
+                              i32, f64, i32, vp, vp]),
 }
 
 

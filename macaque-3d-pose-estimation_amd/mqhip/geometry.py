@@ -494,15 +494,15 @@ class CameraGroup:
                                  scale_length=2, scale_length_weak=0.5, reproj_error_threshold=15,
                                  reproj_loss='soft_l1', n_deriv_smooth=1, scores=None, verbose=False):
         """cameras.py:1192-1415: lengths fixed to joint_len, p3d only; the reference caps scipy at
-        max_nfev=15 (the initial evaluation + 14 trial steps), mirrored here as at most 14
-        Levenberg-Marquardt trial steps."""
+        max_nfev=15 (the initial evaluation + 14 trial steps): the trf solver takes the same cap, the LM solver
+        at most 14 trial steps."""
         from .optim import optim_points_gpu
         joint_len = np.asarray(joint_len, dtype=np.float64).ravel()
         p3, _ = optim_points_gpu(self, points, p3ds, constraints=constraints, constraints_weak=constraints_weak,
                                  scale_smooth=scale_smooth, scale_length=scale_length,
                                  scale_length_weak=scale_length_weak, reproj_error_threshold=reproj_error_threshold,
                                  reproj_loss=reproj_loss, n_deriv_smooth=n_deriv_smooth, scores=scores,
-                                 verbose=verbose, joint_len=joint_len, max_iter=14)
+                                 verbose=verbose, joint_len=joint_len, max_iter=14, max_nfev=15)
         return p3, joint_len
 
 

@@ -8,6 +8,13 @@ host C++ ``mq_optim_prepare`` (numpy's rounding and summation orders, one thread
 animal); the solve (every residual, Jacobian and linear step) runs in libmq_hip's
 kernels.  There is no CPU solver behind this module.
 
+Two solvers (ABI 7):
+  "trf" (default) -- the reference's own algorithm, scipy's least_squares(method='trf') with lsmr trust-region
+          steps (cameras.py:1166-1180; scipy 1.15.3 trf_no_bounds), restated on the GPU
+          (csrc/optim_trf.hip): the parity mode, it stops where scipy stops;
+  "lm"   -- Levenberg-Marquardt + PCG with its own stop rule (csrc/optim.hip): lands closer to the
+          converged solution than scipy's ftol-1e-3 stop, in fewer, heavier steps.
+
 ``optim_points_batch`` refines several animals in one call (they are
 independent problems sharing the cameras).
 """
@@ -19,6 +26,17 @@ import torch
 from . import _lib
 
 LOSSES = {"linear": 0, "soft_l1": 1, "huber": 2}
+SOLVERS = {"trf": 0, "lm": 1}
+_DEFAULT = {"solver": "trf"}
+
+
+def set_default_solver(name):
+    """Select the solver step 4 and CameraGroup.optim_points use ("trf", the default, or "lm"); returns the
+    previous one (bench.py times config 4 with both)."""
+    if name not in SOLVERS:
+        raise ValueError(f"unknown solver {name!r}")
+    prev, _DEFAULT["solver"] = _DEFAULT["solver"], name
+    return prev
 
 # Set to a list to record every optim_points_batch call (problem size, LM steps per individual, wall ms):
 # the config-3 clip driver (tools/run_clip_sharded.py) reports step 4's solver work from it.
@@ -51,12 +69,17 @@ def _pairs(c):
 
 def optim_points_batch(cgroup, points, p3ds, constraints=(), constraints_weak=(), scale_smooth=4, scale_length=2,
                        scale_length_weak=0.5, reproj_error_threshold=15, reproj_loss="soft_l1", n_deriv_smooth=1,
-                       joint_len=None, max_iter=200, ftol=1e-3, verbose=False, return_stats=False):
+                       joint_len=None, max_iter=200, ftol=1e-3, verbose=False, return_stats=False, solver=None,
+                       max_nfev=None):
     """points (B,C,F,J,2) with NaN for missing, p3ds (B,F,J,3) initial triangulation.
 
     joint_len=None: lengths are optimised (optim_points); a (n_strong+n_weak,) array fixes
     them (optim_points_jointlenfix, cameras.py:1192-1415).
-    Returns p3ds_new (B,F,J,3) and joint_len (B, n_strong+n_weak)."""
+    solver: "trf" (scipy's algorithm; max_nfev as scipy's, None = 100 x parameters) or "lm" (max_iter LM steps);
+    None = the module default (set_default_solver).
+    Returns p3ds_new (B,F,J,3) and joint_len (B, n_strong+n_weak); with return_stats also the (B, 8) stats
+    (initial cost, final cost, iterations, status, nfev, njev, lsmr iterations, longest lsmr run) and
+    scale_smooth_full."""
     points = np.asarray(points, dtype=np.float64)
     p3ds = np.asarray(p3ds, dtype=np.float64)
     B, C, F, J, _ = points.shape
@@ -66,6 +89,10 @@ def optim_points_batch(cgroup, points, p3ds, constraints=(), constraints_weak=()
     assert p3ds.shape == (B, F, J, 3)
     if reproj_loss not in LOSSES:
         raise ValueError(f"unknown reproj_loss {reproj_loss!r}")
+    solver = _DEFAULT["solver"] if solver is None else solver
+    if solver not in SOLVERS:
+        raise ValueError(f"unknown solver {solver!r}")
+    limit = (int(max_nfev) if max_nfev else 0) if solver == "trf" else int(max_iter)
     cons, consw = _pairs(constraints), _pairs(constraints_weak)
     nS, nW = len(cons), len(consw)
     xs, ssf = prepare_batch(p3ds, cons, consw, scale_smooth)
@@ -78,7 +105,7 @@ def optim_points_batch(cgroup, points, p3ds, constraints=(), constraints_weak=()
     cams = cgroup.cams_tensor()
     allc = np.ascontiguousarray(np.vstack([cons, consw]).astype(np.int32)) if nS + nW else np.zeros((1, 2), np.int32)
     ssf_h = np.ascontiguousarray(np.array(ssf, dtype=np.float64))
-    stats = np.zeros((B, 4), dtype=np.float64)
+    stats = np.zeros((B, 8), dtype=np.float64)
     import ctypes
     import time
     t0 = time.perf_counter()
@@ -86,16 +113,18 @@ def optim_points_batch(cgroup, points, p3ds, constraints=(), constraints_weak=()
         ctx.handle, _lib.ptr(cams), C, _lib.ptr(p2_d), _lib.ptr(x_d), B, F, J,
         allc.ctypes.data_as(ctypes.c_void_p), nS, nW, ssf_h.ctypes.data_as(ctypes.c_void_p),
         float(scale_length), float(scale_length_weak), float(reproj_error_threshold), LOSSES[reproj_loss],
-        int(n_deriv_smooth), 0 if joint_len is None else 1, int(max_iter), float(ftol),
+        int(n_deriv_smooth), 0 if joint_len is None else 1, limit, float(ftol), SOLVERS[solver],
         stats.ctypes.data_as(ctypes.c_void_p), _lib.stream_ptr(dev))
     _lib.check(rc, "mq_optim_points")
     x = x_d.cpu().numpy()
     if CALL_LOG is not None:
-        CALL_LOG.append({"B": B, "F": F, "J": J, "lm_steps": stats[:, 2].astype(int).tolist(),
-                         "status": stats[:, 3].astype(int).tolist(), "ms": round((time.perf_counter() - t0) * 1e3, 2)})
+        CALL_LOG.append({"B": B, "F": F, "J": J, "solver": solver, "iterations": stats[:, 2].astype(int).tolist(),
+                         "status": stats[:, 3].astype(int).tolist(), "nfev": stats[:, 4].astype(int).tolist(),
+                         "lsmr": stats[:, 6].astype(int).tolist(), "ms": round((time.perf_counter() - t0) * 1e3, 2)})
     if verbose:
         for b in range(B):
-            print(f"optim_points[{b}]: cost {stats[b, 0]:.6g} -> {stats[b, 1]:.6g} in {int(stats[b, 2])} LM steps")
+            print(f"optim_points[{b}] ({solver}): cost {stats[b, 0]:.6g} -> {stats[b, 1]:.6g} in {int(stats[b, 2])} "
+                  f"iterations, status {int(stats[b, 3])}")
     out = x[:, :F * J * 3].reshape(B, F, J, 3), x[:, F * J * 3:]
     if return_stats:
         return out + (stats, ssf)
@@ -104,7 +133,7 @@ def optim_points_batch(cgroup, points, p3ds, constraints=(), constraints_weak=()
 
 def optim_points_gpu(cgroup, points, p3ds, constraints=(), constraints_weak=(), scale_smooth=4, scale_length=2,
                      scale_length_weak=0.5, reproj_error_threshold=15, reproj_loss="soft_l1", n_deriv_smooth=1,
-                     scores=None, verbose=False, joint_len=None, max_iter=200, ftol=1e-3):
+                     scores=None, verbose=False, joint_len=None, max_iter=200, ftol=1e-3, max_nfev=None):
     """CameraGroup.optim_points signature (cameras.py:1116): points (C,F,J,2), p3ds (F,J,3)
     -> (p3ds_new (F,J,3), joint_len (n_strong + n_weak,))."""
     if scores is not None:
@@ -112,5 +141,5 @@ def optim_points_gpu(cgroup, points, p3ds, constraints=(), constraints_weak=(), 
     p3, jl = optim_points_batch(cgroup, np.asarray(points)[None], np.asarray(p3ds)[None], constraints,
                                 constraints_weak, scale_smooth, scale_length, scale_length_weak,
                                 reproj_error_threshold, reproj_loss, n_deriv_smooth, joint_len=joint_len,
-                                max_iter=max_iter, ftol=ftol, verbose=verbose)
+                                max_iter=max_iter, ftol=ftol, verbose=verbose, max_nfev=max_nfev)
     return p3[0], jl[0]

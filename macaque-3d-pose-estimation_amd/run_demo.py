@@ -58,6 +58,14 @@ def proc(data_name, fps, results_dir_root, device_str, config_path, raw_data_dir
                                      group=group if (world > 1 or sharded) else None,
                                      device=gather_device if (world > 1 or sharded) else None)
         t2 = time.perf_counter()
+        sharded_run = world > 1 or sharded
+        if kp2d is None and sharded_run:
+            # the file path of a sharded run (some cameras' outputs were already on disk): rank r
+            # writes the cameras c = r (mod world), so every rank's writer must have finished before rank 0
+            # reads any file (the decision above is the same on every rank: same stores, same files)
+            if s1out is not None:
+                s1out.wait()
+            _barrier(group)
         if rank != 0:
             return None
         result_dir = os.path.join(results_dir_root, data_name)
@@ -83,6 +91,13 @@ def proc(data_name, fps, results_dir_root, device_str, config_path, raw_data_dir
         if "gather_end" in timings:   # the sharded path: rank 0's timeline after the keypoint all-gather
             timings["after_gather_s"] = t4 - timings.pop("gather_end")
     return out
+
+
+def _barrier(group):
+    """A barrier over the run's ranks when a process group exists (a ``sharded`` run at world 1 has none)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier(group=group)
 
 
 def _dist_from_env(backend=None):

@@ -38,7 +38,8 @@ CONFIG_TMPL = os.path.join(_HERE, "..", "..", "configs", "config_tmpl.toml")
 
 # cameras.py:1250: optim_points_jointlenfix runs scipy with max_nfev=15, i.e. the initial
 # evaluation plus at most 14 trial steps; one LM iteration here is one trial evaluation.
-JOINTLENFIX_MAX_TRIALS = 14
+JOINTLENFIX_MAX_TRIALS = 14   # LM solver: trial steps
+JOINTLENFIX_MAX_NFEV = 15     # trf solver: scipy's max_nfev of optim_points_jointlenfix (cameras.py:1246-1260)
 
 # step4:142-147 -- the filter settings are hard-coded there, not read from the TOML
 FILTER_CONFIG = {"filter": {"score_threshold": 0.3, "n_back": 3, "offset_threshold": 25, "multiprocessing": True}}
@@ -170,7 +171,8 @@ def reconstruct_3d(kp2d_f, cgroup, config, bodyparts=BODYPARTS, joint_len_median
                 cgroup, pts_raw[run], init[run], cons, weak, scale_smooth=tri['scale_smooth'],
                 scale_length=tri['scale_length'], scale_length_weak=tri['scale_length_weak'],
                 reproj_error_threshold=tri['reproj_error_threshold'], n_deriv_smooth=tri['n_deriv_smooth'],
-                joint_len=jl_fix, max_iter=200 if jl_fix is None else JOINTLENFIX_MAX_TRIALS, verbose=verbose)
+                joint_len=jl_fix, max_iter=200 if jl_fix is None else JOINTLENFIX_MAX_TRIALS,
+                max_nfev=None if jl_fix is None else JOINTLENFIX_MAX_NFEV, verbose=verbose)
             for i, a in enumerate(run):
                 p3[a] = res[i]
                 joint_len.append(jls[i] if jl_fix is None else jl_fix)

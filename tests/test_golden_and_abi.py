@@ -114,7 +114,7 @@ def test_library_exports_every_header_symbol(lib):
     for s in syms:
         assert hasattr(lib, s), f"libmq_hip.so does not export {s}"
     assert sorted(_lib.EXPORTED) == syms
-    assert lib.mq_abi_version() == 6
+    assert lib.mq_abi_version() == 7
 
 
 def test_library_is_gfx950_code_object(lib):
@@ -135,17 +135,18 @@ def test_tuning_knobs_only_select_equivalent_variants(lib):
     """mq_set_tuning accepts only routing knobs whose settings are tested equal (GEMM routing,
     attention version, PCG iterations); the timing-ablation keys of earlier builds (which produced
     wrong results on purpose) are rejected.  No HIP call is made, so this runs without a GPU."""
-    for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 17, 22, 99):
+    for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 17, 23, 99):
         assert lib.mq_set_tuning(key, 1) == -2, key
         assert lib.mq_get_tuning(key) == -2, key
     for key, default, other in ((2, 0, 1), (12, 1, 0), (18, 1, 0), (19, 1, 0), (20, 1, 0), (4, 40, 10),
-                                (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1)):
+                                (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1), (22, 8, 1)):
         assert lib.mq_get_tuning(key) == default
         assert lib.mq_set_tuning(key, other) == 0
         assert lib.mq_get_tuning(key) == other
         assert lib.mq_set_tuning(key, default) == 0
     assert lib.mq_set_tuning(4, 0) == -2
     assert lib.mq_set_tuning(21, 8) == -2
+    assert lib.mq_set_tuning(22, 0) == -2 and lib.mq_set_tuning(22, 65) == -2
 
 
 def test_context_ignores_tuning_environment():

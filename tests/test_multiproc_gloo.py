@@ -190,3 +190,117 @@ def test_sharded_tail_world2_equals_single_rank_files(tmp_path):
             a = open(os.path.join(ref_res, "demo", cam, name), "rb").read()
             b = open(os.path.join(res, "demo", cam, name), "rb").read()
             assert a == b, (cam, name)
+
+
+def _demo_worker(rank, world, port, raw, res, cfg, fps, slow_rank, q):
+    """run_demo.proc on one gloo rank with the fake pose model; step 4 is replaced by a probe that returns
+    the kp2d array it would lift (the GPU part; its input is what the sharding must get right)."""
+    import sys
+    import time
+    from types import SimpleNamespace
+    here = os.path.dirname(os.path.abspath(__file__))
+    pkg = os.path.join(os.path.dirname(here), "macaque-3d-pose-estimation_amd")
+    sys.path[:0] = [here, pkg]
+    import torch.distributed as dist
+    from _fakes import fake_pose_batch
+    import run_demo
+    from src.pipeline import step1_proc2d as s1
+    from src.pipeline import step4_aniposefiltering as step4
+    s1.inference_topdown_batch = fake_pose_batch
+    step4.proc = lambda data_name, results_dir_root, config_path, n_kp, redo=True, device=0, kp2d=None: (
+        kp2d if kp2d is not None else __import__("mqhip.io", fromlist=["load_pickle"]).load_pickle(
+            os.path.join(results_dir_root, data_name, "kp2d.pickle")))
+    if rank == slow_rank:          # a slow writer: rank 0 must not read the files before it has finished
+        orig = s1._write_step1_files
+
+        def slow(*a, **k):
+            time.sleep(2.0)
+            return orig(*a, **k)
+        s1._write_step1_files = slow
+    if world > 1:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        stub = SimpleNamespace(cfg=SimpleNamespace(n_joints=17))
+        tm = {}
+        out = run_demo.proc("demo", fps, res, "cuda:0", cfg, raw, 17, n_animal=2, pose_model=stub, id_model=None,
+                            world=world, rank=rank, timings=tm)
+        q.put((rank, out, sorted(tm)))
+    finally:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+
+
+def _run_demo_ranks(world, raw, res, cfg, fps, slow_rank=-1):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_demo_worker, args=(r, world, port, raw, res, cfg, fps, slow_rank, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def _demo_inputs(tmp_path, n_cams, n_frames, steps=None):
+    import yaml
+    from _fakes import make_stores
+    stores = make_stores(str(tmp_path / "raw"), n_cams=n_cams, n_frames=n_frames, seed=5)
+    cams = [str(1000 + c) for c in range(n_cams)][::-1]          # config order differs from the store order
+    cfg = tmp_path / "config.yaml"
+    cfg.write_text(yaml.safe_dump({"camera_id": [int(c) for c in cams]}))
+    t = stores[0].frame_time
+    fps = 24.0 if steps is None else (steps - 0.5) / (t[-1] - t[0])
+    return str(tmp_path / "raw"), str(cfg), fps, np.arange(t[0], t[-1], 1.0 / fps)
+
+
+def _files(res, n_cams):
+    return {(c, n): open(os.path.join(res, "demo", str(1000 + c), n), "rb").read()
+            for c in range(n_cams) for n in ("alldata.json", "frame_num.npy")}
+
+
+def test_run_demo_world8_config3_equals_single_rank(tmp_path):
+    """the whole config-3 sharded path at world 8 (gloo, CPU): a 300-step clip split by
+    frame_block(300, 8) (38 / 37 steps) through pose_clip_sharded, 3 cameras so ranks 3-7 own no camera
+    (camera_shard / gather_cameras with empty parts), rank 0's kp2d.pickle and step-4 input.  Bit for bit the
+    single-rank run: rank 0's step-4 input, kp2d.pickle and every alldata.json / frame_num.npy."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from mqhip.shard import camera_shard, frame_block
+    raw, cfg, fps, T = _demo_inputs(tmp_path, 3, 290, steps=300)
+    assert len(T) == 300 and frame_block(300, 8, 0) == (0, 38) and frame_block(300, 8, 7) == (263, 300)
+    assert [camera_shard(3, 8, r) for r in range(8)][3:] == [[]] * 5
+    ref = _run_demo_ranks(1, raw, str(tmp_path / "res1"), cfg, fps)[0][1]
+    got = _run_demo_ranks(8, raw, str(tmp_path / "res8"), cfg, fps)
+    assert got[0][1] is not None and all(out is None for _, out, _ in got[1:])
+    np.testing.assert_array_equal(got[0][1], ref)
+    assert np.abs(ref[..., 2]).sum() > 0
+    assert _files(str(tmp_path / "res1"), 3) == _files(str(tmp_path / "res8"), 3)
+    a = open(os.path.join(tmp_path, "res1", "demo", "kp2d.pickle"), "rb").read()
+    b = open(os.path.join(tmp_path, "res8", "demo", "kp2d.pickle"), "rb").read()
+    assert a == b
+    assert "after_gather_s" in got[0][2]
+
+
+def test_run_demo_world2_file_path_waits_for_every_writer(tmp_path):
+    """when some cameras' outputs are already on disk, step 1 covers only the others and
+    steps 3-4 read the files; rank 1 writes its cameras from a background thread (slowed down here), so rank 0
+    may read only after every rank's writer has finished (run_demo's barrier).  Rank 0's step-4 input equals
+    the single-rank run's."""
+    import shutil
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    raw, cfg, fps, _ = _demo_inputs(tmp_path, 3, 23)
+    ref = _run_demo_ranks(1, raw, str(tmp_path / "res1"), cfg, fps)[0][1]
+    res = tmp_path / "res2"
+    (res / "demo").mkdir(parents=True)
+    shutil.copytree(tmp_path / "res1" / "demo" / "1001", res / "demo" / "1001")   # one camera already done
+    got = _run_demo_ranks(2, raw, str(res), cfg, fps, slow_rank=1)
+    np.testing.assert_array_equal(got[0][1], ref)
+    assert got[1][1] is None
+    assert _files(str(tmp_path / "res1"), 3) == _files(str(res), 3)
