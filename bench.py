@@ -289,22 +289,54 @@ def lift_inputs(A=4, F=300, C=8, seed=2):
 LIFT_ARGS = dict(scale_smooth=3, scale_length=5, scale_length_weak=2, n_deriv_smooth=2, reproj_error_threshold=3)
 
 
+def _viterbi_joint(args):
+    """one joint series of filter_pose_viterbi (filter_pose.py:171-176): the pool task of the reference"""
+    from oracle.viterbi import viterbi_path
+    jix, pts, scs, n_back, thres = args
+    p, sc = viterbi_path(pts, scs, n_back, thres)
+    return jix, p, sc
+
+
 def lift_cpu(cams_np):
-    """Config-4 step-4 lift on the CPU restatement (oracle/): wall seconds per stage."""
+    """Config-4 step-4 lift on the CPU restatement (oracle/), shaped like the reference's own CPU path
+    (VERDICT r4 item 7): the Viterbi filter per individual x camera through a spawn pool of
+    max(min(cores // 2, joints), 1) workers over the 17 joint series (filter_pose.py:151-186, called per
+    individual x camera by step4:142-167), RANSAC batched in numpy on one core, scipy least_squares
+    optim_points on every individual in turn (step4:219-331), reprojection.  Wall seconds per stage and the
+    cores each used."""
+    import multiprocessing as mproc
     import numpy as np
     from mqhip import synth
     from oracle.geometry import CameraGroupOracle, optim_points
-    from oracle.viterbi import step4_filter_batched
+    from oracle.viterbi import STEP4_FILTER_CONFIG, wrap_points
     cams, kp2d = lift_inputs()
     A, F, C, J, _ = kp2d.shape
     o = CameraGroupOracle(cams)
     cons = synth.constraint_indices(synth.CONSTRAINTS)
     weak = synth.constraint_indices(synth.CONSTRAINTS_WEAK)
+    fc = STEP4_FILTER_CONFIG["filter"]
+    n_proc = max(min(cpu_share() // 2, J), 1)
     t = {}
     t0 = time.perf_counter()
-    kf = step4_filter_batched(kp2d).transpose((2, 4, 0, 1, 3))           # (A, C, F, J, 3)
+    kt = np.array(kp2d, dtype=np.float64, copy=True).transpose((1, 3, 0, 4, 2))   # (F, J, A, 3, C) as step 4
+    kf = np.zeros(kt.shape)
+    ctx = mproc.get_context("spawn")
+    for a in range(A):
+        for c in range(C):
+            pts = kt[:, :, a, :2, c].copy()
+            scs = kt[:, :, a, 2, c].copy()
+            pts[scs < fc["score_threshold"]] = np.nan
+            with ctx.Pool(n_proc) as pool:
+                res = list(pool.imap_unordered(_viterbi_joint, [(j, pts[:, j, None], scs[:, j, None], fc["n_back"],
+                                                                 fc["offset_threshold"]) for j in range(J)]))
+            pf = np.full((F, J, 2), np.nan)
+            sf = np.empty((F, J))
+            for j, p, sc in res:
+                pf[:, j], sf[:, j] = p, sc
+            kf[:, :, a, :, c] = np.squeeze(wrap_points(pf, sf))
     t["viterbi_a15"] = time.perf_counter() - t0
-    log(f"cpu lift: viterbi {t['viterbi_a15']:.2f} s")
+    log(f"cpu lift: viterbi {t['viterbi_a15']:.2f} s ({A * C} pools of {n_proc} spawn workers)")
+    kf = kf.transpose((2, 4, 0, 1, 3))                                        # (A, C, F, J, 3)
     pts = kf[..., :2].copy()
     pts[kf[..., 2] < 0.5] = np.nan
     flat = np.ascontiguousarray(pts.transpose(1, 0, 2, 3, 4).reshape(C, -1, 2))
@@ -314,23 +346,28 @@ def lift_cpu(cams_np):
     log(f"cpu lift: ransac {t['ransac_a13']:.2f} s")
     init = p3.reshape(A, F, J, 3)
     t0 = time.perf_counter()
-    r0 = optim_points(o, pts[0], init[0], cons, weak, **LIFT_ARGS)
-    t["optim_points_a16"] = (time.perf_counter() - t0) * A
+    res = [optim_points(o, pts[a], init[a], cons, weak, **LIFT_ARGS) for a in range(A)]
+    t["optim_points_a16"] = time.perf_counter() - t0
+    log(f"cpu lift: optim_points {t['optim_points_a16']:.2f} s for {A} individuals")
     t0 = time.perf_counter()
-    o.reprojection_error(np.ascontiguousarray(np.tile(r0[0], (A, 1, 1, 1)).reshape(-1, 3)), flat, mean=True)
+    o.reprojection_error(np.ascontiguousarray(np.stack([r[0] for r in res]).reshape(-1, 3)), flat, mean=True)
     t["reproj_a14"] = time.perf_counter() - t0
     tot = sum(t.values())
     return {"seconds": {k: round(v, 4) for k, v in t.items()}, "total_s": round(tot, 4),
-            "individuals_frames_per_s": round(A * F / tot, 3), "cores": 1, "kind": "port",
-            "sample": f"{F} frames x {C} views x {A} individuals x {J} joints; batched numpy Viterbi / RANSAC "
-                      f"restatements (pinned equal to the loop restatements), scipy least_squares optim_points on "
-                      f"animal 0 scaled x{A}"}
+            "individuals_frames_per_s": round(A * F / tot, 3),
+            "cores": {"viterbi_a15": n_proc, "ransac_a13": 1, "optim_points_a16": 1, "reproj_a14": 1},
+            "kind": "port",
+            "sample": f"{F} frames x {C} views x {A} individuals x {J} joints, whole: the Viterbi filter per "
+                      f"individual x camera through a spawn pool of {n_proc} workers over the joint series "
+                      f"(the reference's filter_pose_viterbi shape), batched numpy RANSAC, scipy least_squares "
+                      f"optim_points on every individual in turn, reprojection"}
 
 
-def lift_gpu(device, reps=3):
+def lift_gpu(device, reps=3, solver="trf"):
     """Config-4 step-4 lift on the GPU (HIP kernels through the drop-in API, numpy in / out):
     Viterbi over the 544 chains, RANSAC (min_cams 2) over 20,400 points, batched optim_points over
-    the 4 animals, mean reprojection error.  Median wall ms per stage over `reps` runs."""
+    the 4 animals (``solver``: "trf", scipy's algorithm and the default, or "lm"), mean reprojection error.
+    Median wall ms per stage over `reps` runs."""
     import numpy as np
     import torch
     from mqhip import synth
@@ -359,14 +396,14 @@ def lift_gpu(device, reps=3):
         P2 = np.ascontiguousarray(pts.transpose(0, 2, 1, 3, 4))
         t4 = tick()
         res, jl, stats, _ = optim_points_batch(g, P2, p3.reshape(A, F, J, 3), cons, weak, return_stats=True,
-                                               **LIFT_ARGS)
+                                               solver=solver, **LIFT_ARGS)
         t5 = tick()
         g.reprojection_error(np.ascontiguousarray(res.reshape(-1, 3)), flat, mean=True)
         t6 = tick()
         for k, v in (("viterbi_a15", t1 - t0), ("ransac_a13", t3 - t2), ("optim_points_a16", t5 - t4),
                      ("reproj_a14", t6 - t5)):
             times[k].append(v)
-        log(f"gpu lift: viterbi {1e3 * (t1 - t0):.1f} ms, ransac {1e3 * (t3 - t2):.1f} ms, "
+        log(f"gpu lift ({solver}): viterbi {1e3 * (t1 - t0):.1f} ms, ransac {1e3 * (t3 - t2):.1f} ms, "
             f"optim {1e3 * (t5 - t4):.1f} ms, reproj {1e3 * (t6 - t5):.1f} ms")
     med = {k: float(np.median(v[1:])) * 1e3 for k, v in times.items()}
     tot = sum(med.values())
@@ -375,7 +412,11 @@ def lift_gpu(device, reps=3):
     return {"gpu_ms": {k: round(v, 3) for k, v in med.items()}, "total_ms": round(tot, 3),
             "optim_result_sha256_16": digest,
             "individuals_frames_per_s": round(A * F / (tot * 1e-3), 2),
-            "optim_lm_iterations": stats[:, 2].tolist(), "statistic": f"median of {reps} after 1 warm-up",
+            "optim_solver": solver, "optim_iterations": stats[:, 2].astype(int).tolist(),
+            "optim_status": stats[:, 3].astype(int).tolist(),
+            **({"optim_nfev": stats[:, 4].astype(int).tolist(), "optim_lsmr_iterations": stats[:, 6].astype(int).tolist()}
+               if solver == "trf" else {}),
+            "statistic": f"median of {reps} after 1 warm-up",
             "workload": f"BASELINE config 4: {F} frames x {C} views x {A} individuals x {J} joints, ransac + optim",
             "note": "wall time per stage through the drop-in numpy API (host<->device copies included)"}
 
@@ -795,6 +836,7 @@ def main():
         result["value_with_h2d"] = result["with_h2d"]["value"]
     if rank == 0 and world == 1 and not args.no_lift:
         result["lift_config4"] = lift_gpu(local)
+        result["lift_config4_lm"] = lift_gpu(local, solver="lm")
     if rank == 0 and world == 1 and not args.no_config5:
         result["config5"] = config5_gpu(local, model, frames[:, :N_VIEWS] if frames.dim() == 5 else frames, cams_dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -52,7 +52,7 @@ extern "C" {
  *        below scipy's cost on every marker scene probed, where ftol alone stopped 1.5 % above it on one).
  *   7 -- mq_optim_points takes a solver (0: scipy's trust-region-reflective + lsmr, restated -- the default and
  *        the parity mode; 1: the Levenberg-Marquardt + PCG solver of ABI 1-6) and writes 8 stats per animal;
- *        tuning key MQ_TUNE_OPTIM_TRF_CHUNK (22) added. */
+ *        tuning keys MQ_TUNE_OPTIM_TRF_CHUNK (22), MQ_TUNE_VIT_RESID_F32 (23) and MQ_TUNE_ATTN_KRING (24) added. */
 #define MQ_ABI_VERSION 7
 
 typedef struct mq_ctx mq_ctx;
@@ -81,6 +81,11 @@ const char* mq_last_error(void);
                                        alone (dF < ftol F); 1 = and the step's actual / predicted reduction > 0.25
                                        (scipy trf's condition); 2 = the test passed on two accepted steps in a row;
                                        4 = the test at ftol / 2.  Default 6 (2 | 4).  Levenberg-Marquardt solver only */
+#define MQ_TUNE_VIT_RESID_F32 23    /* 1: the ViT's proj / fc2 add their f32 accumulators to the residual stream in the
+                                       GEMM epilogue (rounds 1-3); 0 (default): bf16 branch outputs added in the
+                                       LayerNorm passes (round 4).  A precision A/B knob */
+#define MQ_TUNE_ATTN_KRING 24       /* 1 (default): 192-token attention with the inline-asm K-fragment ring; 0: the
+                                       compiler-scheduled loop (bit-identical; the fallback for a toolchain change) */
 #define MQ_TUNE_OPTIM_TRF_CHUNK 22  /* lsmr iterations the trust-region solver launches between two reads of its done
                                        flags (default 8, 1..64; same results) */
 int mq_set_tuning(int key, int value);

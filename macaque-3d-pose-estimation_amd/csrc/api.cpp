@@ -26,6 +26,9 @@ namespace {
 thread_local std::string g_err;
 // ViT qkv GEMM output head-major for the attention (MQ_TUNE_QKV_HEAD_MAJOR; 0: row-major, same bits)
 int g_qkv_head_major = 1;
+// MQ_TUNE_VIT_RESID_F32: 1 = the ViT's residual updates as f32 read-modify-write GEMM epilogues (rounds 1-3);
+// 0 (default) = bf16 branch outputs added in the LayerNorm passes (round 4).  A precision A/B of that choice.
+int g_vit_resid_f32 = 0;
 int g_tuning_gen = 0;  // bumped by mq_set_tuning
 
 int fail(const std::string& msg, int code = -1) {
@@ -164,6 +167,12 @@ int mq_set_tuning(int key, int value) {
     case MQ_TUNE_QKV_HEAD_MAJOR:
       g_qkv_head_major = value != 0;
       break;
+    case MQ_TUNE_VIT_RESID_F32:
+      g_vit_resid_f32 = value != 0;
+      break;
+    case MQ_TUNE_ATTN_KRING:
+      mq::g_attn_kring = value != 0;
+      break;
     case MQ_TUNE_OPTIM_STOP:
       if (value < 0 || value > 7) return fail("mq_set_tuning: optim stop rule must be in [0, 7]", -2);
       mq::g_optim_stop = value;
@@ -187,6 +196,8 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_OPTIM_PRECOND_LDS: return mq::g_optim_precond_lds;
     case MQ_TUNE_GEMM_TILE64: return mq::g_gemm_tile64;
     case MQ_TUNE_QKV_HEAD_MAJOR: return g_qkv_head_major;
+    case MQ_TUNE_VIT_RESID_F32: return g_vit_resid_f32;
+    case MQ_TUNE_ATTN_KRING: return mq::g_attn_kring;
     case MQ_TUNE_OPTIM_STOP: return mq::g_optim_stop;
     case MQ_TUNE_OPTIM_TRF_CHUNK: return mq::g_optim_trf_chunk;
     default: return fail("mq_get_tuning: unknown key", -2);
@@ -531,9 +542,11 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
   // proj writes P1, and the next qkv GEMM runs after the LayerNorm that consumed both.
   unsigned short* P1 = m->QKV;
   unsigned short* P2 = m->QKV + (size_t)rows * D;
+  // MQ_TUNE_VIT_RESID_F32 (precision A/B): proj / fc2 add their f32 accumulators to X in the epilogue instead
+  const bool rf32 = g_vit_resid_f32 != 0;
   for (int l = 0; l < m->L; ++l) {
     const Layer& ly = m->layers[l];
-    if (l == 0)
+    if (l == 0 || rf32)
       K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
     else
       K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, P2, true, ly.ln1_g, ly.ln1_b, m->Hn, rows, D, 1e-6f, s));
@@ -542,9 +555,15 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
     g.head_dim = g_qkv_head_major ? D / m->H : 0;
     K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
     K_TRY(mq::attention_bf16(m->QKV, m->O, F, T, D, m->H, s, g_qkv_head_major != 0));
-    g = mq::GemmArgs{m->O, ly.wproj, P1, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
-    K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
-    K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, nullptr, false, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
+    if (rf32) {
+      g = mq::GemmArgs{m->O, ly.wproj, m->X, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
+      K_TRY(mq::gemm_bf16(g, mq::EPI_RESID_F32, s));
+      K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
+    } else {
+      g = mq::GemmArgs{m->O, ly.wproj, P1, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
+      K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+      K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, nullptr, false, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
+    }
     g = mq::GemmArgs{m->Hn, ly.wfc1, m->G, ly.bfc1, nullptr, rows, FF, D, D, D, FF, 0};
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (m->timing) {
@@ -560,10 +579,10 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
     }
     K_TRY(mq::gemm_bf16(g, mq::EPI_GELU_BF16, s));
     if (m->timing) HIP_TRY(hipEventRecord(e1, s));
-    g = mq::GemmArgs{m->G, ly.wfc2, P2, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0};
-    K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+    g = mq::GemmArgs{m->G, ly.wfc2, rf32 ? (void*)m->X : (void*)P2, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0};
+    K_TRY(mq::gemm_bf16(g, rf32 ? mq::EPI_RESID_F32 : mq::EPI_BF16, s));
   }
-  if (m->L > 0)
+  if (m->L > 0 && !rf32)
     K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, P2, false, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
   else
     K_TRY(mq::layernorm_f32_bf16(m->X, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));

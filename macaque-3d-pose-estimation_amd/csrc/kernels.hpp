@@ -77,6 +77,7 @@ int add_layernorm_f32_bf16(float* x, const unsigned short* p1, const unsigned sh
                            const float* gamma, const float* beta, unsigned short* y, int rows, int dim, float eps,
                            hipStream_t s);
 // head_major: qkv holds the head-major blocks of the qkv GEMM's head_dim output (GemmArgs::head_dim)
+extern int g_attn_kring;  // MQ_TUNE_ATTN_KRING
 int attention_bf16(const unsigned short* qkv, unsigned short* out, int n_img, int tokens, int dim, int heads,
                    hipStream_t s, bool head_major = false);
 int patch_im2col(const float* crops, unsigned short* A, int n_crops, int flip_copies, int img_h, int img_w,

@@ -1704,6 +1704,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
         cost[b] = costt[b];
         lam[b] = std::max(lam[b] / 3.0, 1e-12);
       } else {
+        small[b] = 0;  // "two accepted steps in a row": a rejected step in between breaks the run
         lam[b] *= 4.0;
         if (lam[b] > 1e12) {
           active[b] = 0;

@@ -14,7 +14,7 @@
 // order of their own (so floating-point results are not scipy's bits).
 //
 // Work decomposition (one animal = one independent problem; B animals per call, batched in every launch):
-//   * a workgroup owns a block of TRF_FB consecutive frames of one animal: its reprojection rows (camera x
+//   * a workgroup owns a block of FB (<= 4) consecutive frames of one animal: its reprojection rows (camera x
 //     joint x {u, v}), smoothness rows (np.diff order n, row i at frame i) and limb-length rows (m space), and
 //     its 3 J parameters per frame (n space); the length variables belong to block 0;
 //   * lsmr is two launches per iteration: phase 1 (u = J v - alpha u; the previous iteration's recurrences and
@@ -37,13 +37,13 @@ namespace mq {
 namespace {
 
 constexpr int TRF_THREADS = 256;
-constexpr int TRF_FB = 4;  // frames per workgroup
+constexpr int TRF_FB = 4;  // frames per workgroup (at most; fewer when a block's rows would not fit in LDS)
 constexpr int TRF_MAXJ = 32, TRF_MAXL = 64, TRF_MAXN = 3;
 constexpr int TRF_NS = 24;  // lsmr state doubles per slot
 
 struct TrfDims {
   int B, C, F, J, NL, nS, fix, n, loss;
-  int NX, NV, MR, MRrep, NB;
+  int NX, NV, MR, MRrep, NB, FB;
   double rp, s_len, s_len_weak;
   double c[TRF_MAXN + 1];
   double atol, btol, ctol;
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_eval_kernel(TrfDims D, TrfBuf
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   if (!Bf.act[b]) return;
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL;
-  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
+  const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
   __shared__ double sx[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3];
   __shared__ double sL[TRF_MAXL];
   __shared__ int scons[2 * TRF_MAXL];
@@ -238,91 +238,146 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_eval_kernel(TrfDims D, TrfBuf
 }
 
 // ---------------------------------------------------------------------------------------------------------
+// Latency structure of the per-iteration kernels: every global load that does not depend on a norm (the
+// partials, the block's m rows, its Jacobian rows, the n-space entries) is issued first, into LDS or registers;
+// then ONE combined reduction of the partials; then the arithmetic from LDS.  A launch thus waits on one memory
+// round trip before its arithmetic instead of one per dependent step.
+
+// sums of up to three partial values, every thread of the workgroup holding the same bits
+__device__ __forceinline__ void block_sum3_all(double& a, double& b, double& c, double* red /* [12] */) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    a += __shfl_xor(a, m);
+    b += __shfl_xor(b, m);
+    c += __shfl_xor(c, m);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[w] = a;
+    red[4 + w] = b;
+    red[8 + w] = c;
+  }
+  __syncthreads();
+  a = (red[0] + red[1]) + (red[2] + red[3]);
+  b = (red[4] + red[5]) + (red[6] + red[7]);
+  c = (red[8] + red[9]) + (red[10] + red[11]);
+  __syncthreads();
+}
+
+// the block's Jacobian rows (reprojection: J C 6 doubles per frame) into LDS
+__device__ __forceinline__ void stage_jrep(const TrfDims& D, const TrfBufs& Bf, int b, int f0, int nf, double* sj) {
+  const int per = D.J * D.C * 6;
+  const double* src = Bf.Jrep + ((size_t)b * D.F + f0) * per;
+  for (int i = threadIdx.x; i < nf * per; i += TRF_THREADS) sj[i] = src[i];
+}
+
+// Length variables of block 0: sum over the NB blocks of the per-block partials lp[bb * NL + l], fixed order
+// (G threads per length, blocks bb = g, g + G, ...; then the G group sums in order).  out[l] in LDS.
+__device__ __forceinline__ void length_sums(const TrfDims& D, const double* __restrict__ lp, double* part /*[256]*/,
+                                            double* out) {
+  const int NL = D.NL, NB = D.NB, t = threadIdx.x;
+  const int G = NL > 0 ? TRF_THREADS / NL : 1;
+  double s = 0.0;
+  if (t < G * NL) {
+    const int l = t % NL, g = t / NL;
+    double v[4];
+    int bb = g;
+    for (; bb + 3 * G < NB; bb += 4 * G) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = lp[(size_t)(bb + u * G) * NL + l];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; bb < NB; bb += G) s += lp[(size_t)bb * NL + l];
+  }
+  part[t] = s;
+  __syncthreads();
+  if (t < NL) {
+    double a = 0.0;
+    for (int g = 0; g < G; ++g) a += part[g * NL + t];
+    out[t] = a;
+  }
+  __syncthreads();
+}
+
 // v = J^T (u / beta) - beta vn for the block's parameters (and block 0's length variables).
 //   MODE 0: g = J^T f (u = fres, beta = 1, no vn); partials (sum g^2, max |g|) in vpart slot 0
 //   MODE 1: lsmr's start, v = J^T (f / normb)
-//   MODE 2: lsmr phase 2 of iteration k: first the stop test of iteration k - 1 (phase 1 of iteration k
-//           ran its recurrences and wrote x_{k-1}), then v = J^T (u / beta_k) - beta_k v_{k-1}.
+//   MODE 2: lsmr phase 2 of iteration k: v_k = J^T (u_k / beta_k) - beta_k v_{k-1}  (par = k & 1)
+// Dynamic LDS: the m rows of frames [f0 - n, f0 + nf) (raw; scaled by 1 / beta where they are used, as scipy's
+// in-place u *= 1 / beta) and the block's Jacobian rows.
 template <int MODE>
-__global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs Bf, int k) {
+__global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs Bf, int par) {
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   if (!Bf.act[b]) return;
   if (MODE > 0 && Bf.done[b]) return;
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
-  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
-  const int par = k & 1;
-  __shared__ double red[4];
+  const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
+  __shared__ double red[12];
   __shared__ double slen[TRF_FB][TRF_MAXL][3];
   __shared__ int scons[2 * TRF_MAXL];
-  extern __shared__ double su[];  // m rows of frames [f0 - n, f0 + nf), normalised
-  const double* uin = MODE == 2 ? Bf.u : Bf.fres;
-  // loads that do not depend on the norms go out first
+  __shared__ double spart[TRF_THREADS];
+  __shared__ double sLs[TRF_MAXL];
+  extern __shared__ double lds_jt[];
   const int fa = max(0, f0 - n), nrow = (f0 + nf - fa) * D.MR;
+  double* su = lds_jt;
+  double* sj = lds_jt + (((size_t)(D.FB + D.n) * D.MR + 1) & ~(size_t)1);
+  const double* uin = MODE == 2 ? Bf.u : Bf.fres;
+  // 1. loads independent of beta
+  const double ssf = Bf.ssf[b], normb = Bf.lctl[4 * b + 1];
+  double pu = 0.0;
+  if (MODE == 2)
+    for (int i = t; i < NB; i += TRF_THREADS) pu += Bf.upart[((size_t)par * D.B + b) * NB + i];
   const double* ub = uin + ((size_t)b * F + fa) * D.MR;
+  for (int i = t; i < nrow; i += TRF_THREADS) su[i] = ub[i];
+  stage_jrep(D, Bf, b, f0, nf, sj);
   for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
   for (int i = t; i < nf * NL * 3; i += TRF_THREADS) {
     const int fl = i / (NL * 3), rem = i - fl * NL * 3, l = rem / 3, kk = rem - 3 * l;
     slen[fl][l][kk] = Bf.lenJ[(((size_t)b * F + f0 + fl) * NL + l) * 4 + kk];
   }
-  double beta = 1.0;
-  if (MODE == 1) beta = Bf.lctl[4 * b + 1];
+  const size_t nb = (size_t)b * D.NV;
+  double vn0 = 0.0, vn1 = 0.0, vnL = 0.0;  // the thread's (at most two) parameters and block 0's length variable
   if (MODE == 2) {
-    beta = sqrt(reduce_parts(Bf.upart + ((size_t)par * D.B + b) * NB, NB, 1, red));
-    if (k >= 2) {  // the stop test of iteration k - 1 (lsmr.py:413-441)
-      const double* S = Bf.st + ((size_t)par * D.B + b) * TRF_NS;
-      const double normx = sqrt(reduce_parts(Bf.xpart + ((size_t)par * D.B + b) * NB, NB, 1, red));
-      const double normb = Bf.lctl[4 * b + 1], maxiter = Bf.lctl[4 * b + 2];
-      const double normr = S[S_NORMR], normar = S[S_NORMAR], normA = S[S_NORMA], condA = S[S_CONDA];
-      const double itn = S[S_ITN];
-      const double test1 = normr / normb;
-      const double test2 = (normA * normr) != 0 ? normar / (normA * normr) : INFINITY;
-      const double test3 = 1 / condA;
-      const double t1 = test1 / (1 + normA * normx / normb);
-      const double rtol = D.btol + D.atol * normA * normx / normb;
-      int istop = 0;
-      if (itn >= maxiter) istop = 7;
-      if (1 + test3 <= 1) istop = 6;
-      if (1 + test2 <= 1) istop = 5;
-      if (1 + t1 <= 1) istop = 4;
-      if (test3 <= D.ctol) istop = 3;
-      if (test2 <= D.atol) istop = 2;
-      if (test1 <= rtol) istop = 1;
-      if (istop) {
-        if (blk == 0 && t == 0) {
-          Bf.done[b] = istop;
-          Bf.lctl[4 * b + 3] = itn;
-        }
-        return;
-      }
-    }
+    if (t < nf * J3) vn0 = Bf.vn[nb + (size_t)f0 * J3 + t];
+    if (t + TRF_THREADS < nf * J3) vn1 = Bf.vn[nb + (size_t)f0 * J3 + t + TRF_THREADS];
+    if (blk == 0 && t < NL && !D.fix) vnL = Bf.vn[nb + D.NX + t];
+  }
+  if (blk == 0 && !D.fix) length_sums(D, (MODE == 2 ? Bf.Lpart : Bf.fL) + (size_t)b * NB * NL, spart, sLs);
+  // 2. the norm
+  double beta = 1.0;
+  if (MODE == 1) beta = normb;
+  if (MODE == 2) {
+    double d1 = 0.0, d2 = 0.0;
+    block_sum3_all(pu, d1, d2, red);  // (also the barrier after the staging stores)
+    beta = sqrt(pu);
+  } else {
+    __syncthreads();
   }
   const double ib = 1.0 / beta;
-  for (int i = t; i < nrow; i += TRF_THREADS) su[i] = ub[i] * ib;
-  __syncthreads();
-  const double ssf = Bf.ssf[b];
-  const size_t nb = (size_t)b * D.NV;
+  // 3. arithmetic
   double vsq = 0.0, vmax = 0.0;
-  const int nrep = J * C;
-  for (int task = t; task < nf * J3; task += TRF_THREADS) {
+  const int ntask = nf * J3;
+  for (int task = t, it = 0; task < ntask; task += TRF_THREADS, ++it) {
     const int fl = task / J3, q = task - fl * J3, j = q / 3, kk = q - 3 * j, f = f0 + fl;
     const double* uf = su + (size_t)(f - fa) * D.MR;
-    const double* jr = Bf.Jrep + (((size_t)b * F + f) * nrep + (size_t)j * C) * 6;
+    const double* jr = sj + ((size_t)fl * J + j) * C * 6;
     double acc = 0.0;
     for (int c = 0; c < C; ++c) {
-      acc += jr[6 * c + kk] * uf[2 * (j * C + c)];
-      acc += jr[6 * c + 3 + kk] * uf[2 * (j * C + c) + 1];
+      acc += jr[6 * c + kk] * (uf[2 * (j * C + c)] * ib);
+      acc += jr[6 * c + 3 + kk] * (uf[2 * (j * C + c) + 1] * ib);
     }
     for (int m = 0; m <= n; ++m) {  // smoothness rows i = f - m hold frame f with coefficient c[m]
       const int i = f - m;
-      if (i >= 0 && i < F - n) acc += ssf * D.c[m] * su[(size_t)(i - fa) * D.MR + D.MRrep + q];
+      if (i >= 0 && i < F - n) acc += ssf * D.c[m] * (su[(size_t)(i - fa) * D.MR + D.MRrep + q] * ib);
     }
     for (int l = 0; l < NL; ++l) {
       const int a = scons[2 * l], c2 = scons[2 * l + 1];
-      if (a == j) acc += slen[fl][l][kk] * uf[D.MRrep + J3 + l];
-      else if (c2 == j) acc -= slen[fl][l][kk] * uf[D.MRrep + J3 + l];
+      if (a == j) acc += slen[fl][l][kk] * (uf[D.MRrep + J3 + l] * ib);
+      else if (c2 == j) acc -= slen[fl][l][kk] * (uf[D.MRrep + J3 + l] * ib);
     }
     const size_t o = nb + (size_t)f * J3 + q;
-    const double v = MODE == 2 ? Bf.vn[o] * -beta + acc : acc;
+    const double v = MODE == 2 ? (it == 0 ? vn0 : vn1) * -beta + acc : acc;
     (MODE == 0 ? Bf.g : Bf.vraw)[o] = v;
     vsq += v * v;
     vmax = fmax(vmax, fabs(v));
@@ -331,18 +386,15 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
     const size_t o = nb + D.NX + t;
     double v = 0.0;
     if (!D.fix) {
-      const double* lp = (MODE == 2 ? Bf.Lpart : Bf.fL) + (size_t)b * NB * NL + t;
-      double s = 0.0;
-      for (int bb = 0; bb < NB; ++bb) s += lp[(size_t)bb * NL];
-      const double acc = s * ib;
-      v = MODE == 2 ? Bf.vn[o] * -beta + acc : acc;
+      const double acc = sLs[t] * ib;
+      v = MODE == 2 ? vnL * -beta + acc : acc;
       vsq += v * v;
       vmax = fmax(vmax, fabs(v));
     }
     (MODE == 0 ? Bf.g : Bf.vraw)[o] = v;
   }
   vsq = block_sum_all(vsq, red);
-  vmax = block_max_all(vmax, red);
+  if (MODE == 0) vmax = block_max_all(vmax, red);
   if (t == 0) {
     double* vp = Bf.vpart + (((size_t)par * D.B + b) * NB + blk) * 2;
     vp[0] = vsq;
@@ -351,9 +403,11 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// lsmr phase 1 of iteration k (k >= 1): alpha_{k-1}, beta_{k-1} from the partials; FIRST (k = 1) starts the
-// recurrences (lsmr.py:205-239), otherwise runs iteration k - 1's (:301-410) and updates hbar, x, h; then
-// u_k = J v_{k-1} - alpha_{k-1} u_{k-1} for the block's rows.
+// lsmr phase 1 of iteration k (k >= 1; pp = (k - 1) & 1, par = k & 1): alpha_{k-1}, beta_{k-1} and
+// ||x_{k-2}|| from the partials; FIRST (k = 1) starts the recurrences (lsmr.py:205-239); otherwise the stop test
+// of iteration k - 2 (lsmr.py:413-441, with ||x_{k-2}||: when it passes x_{k-2} is the answer and nothing more
+// runs), then iteration k - 1's recurrences (:301-410) and the hbar / x / h updates; then u_k = J v_{k-1} -
+// alpha_{k-1} u_{k-1} for the block's rows.
 __device__ __forceinline__ void lsmr_recurrence(double* S, double alpha, double beta, double damp, double& chb,
                                                 double& cx, double& ch) {
   double chat, shat, alphahat;
@@ -418,27 +472,99 @@ __device__ __forceinline__ void lsmr_recurrence(double* S, double alpha, double 
   S[S_CONDA] = condA;
 }
 
+// the stop test of lsmr.py:413-441 from a state slot and ||x||; 0 = go on
+__device__ __forceinline__ int lsmr_istop(const TrfDims& D, const double* S, double normx, double normb,
+                                          double maxiter) {
+  const double normr = S[S_NORMR], normar = S[S_NORMAR], normA = S[S_NORMA], condA = S[S_CONDA];
+  const double itn = S[S_ITN];
+  const double test1 = normr / normb;
+  const double test2 = (normA * normr) != 0 ? normar / (normA * normr) : INFINITY;
+  const double test3 = 1 / condA;
+  const double t1 = test1 / (1 + normA * normx / normb);
+  const double rtol = D.btol + D.atol * normA * normx / normb;
+  int istop = 0;
+  if (itn >= maxiter) istop = 7;
+  if (1 + test3 <= 1) istop = 6;
+  if (1 + test2 <= 1) istop = 5;
+  if (1 + t1 <= 1) istop = 4;
+  if (test3 <= D.ctol) istop = 3;
+  if (test2 <= D.atol) istop = 2;
+  if (test1 <= rtol) istop = 1;
+  return istop;
+}
+
 template <bool FIRST>
-__global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBufs Bf, int k) {
+__global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBufs Bf, int par) {
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   if (!Bf.act[b] || Bf.done[b]) return;
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
-  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
-  const int par = k & 1, pp = par ^ 1;
-  __shared__ double red[4];
+  const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
+  const int pp = par ^ 1;
+  __shared__ double red[12];
   __shared__ double sv[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3];
   __shared__ double sL[TRF_MAXL];
   __shared__ double sLu[TRF_FB][TRF_MAXL];
+  __shared__ double slj[TRF_FB][TRF_MAXL][4];
   __shared__ int scons[2 * TRF_MAXL];
   __shared__ double sS[TRF_NS];
   __shared__ double scoef[4];
-  for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
-  const double alpha = sqrt(reduce_parts(Bf.vpart + ((size_t)pp * D.B + b) * NB * 2, NB, 2, red));
-  const double beta = FIRST ? Bf.lctl[4 * b + 1] : sqrt(reduce_parts(Bf.upart + ((size_t)pp * D.B + b) * NB, NB, 1, red));
+  __shared__ int sstop;
+  extern __shared__ double lds_l1[];
+  double* sm = lds_l1;                                                   // the block's m rows (u_{k-1}, raw)
+  double* sj = lds_l1 + (((size_t)D.FB * D.MR + 1) & ~(size_t)1);       // its Jacobian rows
   const size_t nb = (size_t)b * D.NV;
+  // 1. loads independent of the norms
+  const double damp = Bf.lctl[4 * b], normb = Bf.lctl[4 * b + 1], maxiter = Bf.lctl[4 * b + 2], ssf = Bf.ssf[b];
+  double pa = 0.0, pb = 0.0, px = 0.0;
+  for (int i = t; i < NB; i += TRF_THREADS) {
+    pa += Bf.vpart[(((size_t)pp * D.B + b) * NB + i) * 2];
+    if (!FIRST) {
+      pb += Bf.upart[((size_t)pp * D.B + b) * NB + i];
+      px += Bf.xpart[((size_t)pp * D.B + b) * NB + i];
+    }
+  }
+  if (!FIRST && t < TRF_NS) sS[t] = Bf.st[((size_t)pp * D.B + b) * TRF_NS + t];
+  const int nfx = min(nf + n, F - f0);
+  for (int i = t; i < nfx * J3; i += TRF_THREADS) sv[i] = Bf.vraw[nb + (size_t)f0 * J3 + i];
+  if (t < NL) sL[t] = D.fix ? 0.0 : Bf.vraw[nb + D.NX + t];
+  const double* uin = FIRST ? Bf.fres : Bf.u;
+  const double* ub = uin + ((size_t)b * F + f0) * D.MR;
+  for (int i = t; i < nf * D.MR; i += TRF_THREADS) sm[i] = ub[i];
+  stage_jrep(D, Bf, b, f0, nf, sj);
+  for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
+  for (int i = t; i < nf * NL * 4; i += TRF_THREADS) {
+    const int fl = i / (NL * 4), rem = i - fl * NL * 4;
+    slj[fl][rem >> 2][rem & 3] = Bf.lenJ[((size_t)b * F + f0 + fl) * NL * 4 + rem];
+  }
+  // the thread's n-space entries: (at most two) parameters and block 0's length variable
+  double h0 = 0.0, h1 = 0.0, hL = 0.0, hb0 = 0.0, hb1 = 0.0, hbL = 0.0, x0 = 0.0, x1 = 0.0, xL = 0.0;
+  const size_t o0 = nb + (size_t)f0 * J3 + t, o1 = o0 + TRF_THREADS, oL = nb + D.NX + t;
+  const bool e0 = t < nf * J3, e1 = t + TRF_THREADS < nf * J3, eL = blk == 0 && t < NL && !D.fix;
+  if (!FIRST) {
+    if (e0) {
+      h0 = Bf.h[o0];
+      hb0 = Bf.hbar[o0];
+      x0 = Bf.xl[o0];
+    }
+    if (e1) {
+      h1 = Bf.h[o1];
+      hb1 = Bf.hbar[o1];
+      x1 = Bf.xl[o1];
+    }
+    if (eL) {
+      hL = Bf.h[oL];
+      hbL = Bf.hbar[oL];
+      xL = Bf.xl[oL];
+    }
+  }
+  // 2. the norms (one combined reduction; also the barrier after the staging stores), the test, the recurrences
+  block_sum3_all(pa, pb, px, red);
+  const double alpha = sqrt(pa);
+  const double beta = FIRST ? normb : sqrt(pb);
   if (t == 0) {
     double* S = sS;
     double chb = 0.0, cx = 0.0, ch = 0.0;
+    int istop = 0;
     if (FIRST) {
       for (int i = 0; i < TRF_NS; ++i) S[i] = 0.0;
       S[S_ZETABAR] = alpha * beta;
@@ -452,95 +578,75 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       S[S_NORMA2] = alpha * alpha;
       S[S_MINRBAR] = 1e+100;
       S[S_ITN] = 0;
+      if (!(alpha * beta != 0)) istop = 8;  // normar == 0 (or normb == 0): x = 0 (lsmr.py:247-256)
     } else {
-      const double* Sp = Bf.st + ((size_t)pp * D.B + b) * TRF_NS;
-      for (int i = 0; i < TRF_NS; ++i) S[i] = Sp[i];
-      lsmr_recurrence(S, alpha, beta, Bf.lctl[4 * b], chb, cx, ch);
+      if (S[S_ITN] >= 1) istop = lsmr_istop(D, S, sqrt(px), normb, maxiter);
+      if (!istop) lsmr_recurrence(S, alpha, beta, damp, chb, cx, ch);
     }
+    if (istop && blk == 0) {
+      Bf.done[b] = istop;
+      Bf.lctl[4 * b + 3] = S[S_ITN];
+    }
+    sstop = istop;
     scoef[0] = chb;
     scoef[1] = cx;
     scoef[2] = ch;
-    if (blk == 0) {
+    if (blk == 0 && !istop) {
       double* So = Bf.st + ((size_t)par * D.B + b) * TRF_NS;
       for (int i = 0; i < TRF_NS; ++i) So[i] = S[i];
     }
   }
   __syncthreads();
-  if (FIRST && !(alpha * beta != 0)) {  // normar == 0 (or normb == 0): x = 0 (lsmr.py:247-256)
-    for (int i = t; i < nf * J3; i += TRF_THREADS) Bf.xl[nb + (size_t)f0 * J3 + i] = 0.0;
-    if (blk == 0 && t < NL) Bf.xl[nb + D.NX + t] = 0.0;
-    if (blk == 0 && t == 0) {
-      Bf.done[b] = 8;
-      Bf.lctl[4 * b + 3] = 0;
+  if (sstop) {
+    if (FIRST) {  // x = 0
+      if (e0) Bf.xl[o0] = 0.0;
+      if (e1) Bf.xl[o1] = 0.0;
+      if (eL) Bf.xl[oL] = 0.0;
     }
     return;
   }
   const double chb = scoef[0], cx = scoef[1], ch = scoef[2];
   const double ia = 1.0 / alpha;
-  // n space: v_{k-1} = v_raw / alpha (scipy's in-place v *= 1 / alpha), staged with the halo frames
-  const int nfx = min(nf + n, F - f0);
-  double xsq = 0.0;
-  for (int i = t; i < nfx * J3; i += TRF_THREADS) {
-    const size_t o = nb + (size_t)f0 * J3 + i;
-    const double v = Bf.vraw[o] * ia;
-    sv[i] = v;
-    if (i < nf * J3) {
-      Bf.vn[o] = v;
-      if (FIRST) {
-        Bf.h[o] = v;
-        Bf.hbar[o] = 0.0;
-        Bf.xl[o] = 0.0;
-      } else {
-        const double hb = Bf.hbar[o] * chb + Bf.h[o];
-        const double xv = Bf.xl[o] + cx * hb;
-        Bf.hbar[o] = hb;
-        Bf.xl[o] = xv;
-        Bf.h[o] = Bf.h[o] * ch + v;
-        xsq += xv * xv;
-      }
-    }
-  }
-  if (t < NL) {
-    double v = 0.0;
-    if (!D.fix) {
-      const size_t o = nb + D.NX + t;
-      v = Bf.vraw[o] * ia;
-      if (blk == 0) {
-        Bf.vn[o] = v;
-        if (FIRST) {
-          Bf.h[o] = v;
-          Bf.hbar[o] = 0.0;
-          Bf.xl[o] = 0.0;
-        } else {
-          const double hb = Bf.hbar[o] * chb + Bf.h[o];
-          const double xv = Bf.xl[o] + cx * hb;
-          Bf.hbar[o] = hb;
-          Bf.xl[o] = xv;
-          Bf.h[o] = Bf.h[o] * ch + v;
-          xsq += xv * xv;
-        }
-      }
-    }
-    sL[t] = v;
-  }
+  // 3a. n space: v_{k-1} = v_raw / alpha (scipy's in-place v *= 1 / alpha); hbar, x, h (lsmr.py:396-403)
+  for (int i = t; i < nfx * J3; i += TRF_THREADS) sv[i] = sv[i] * ia;
+  if (t < NL) sL[t] = sL[t] * ia;
   __syncthreads();
-  // m space: u_k = (u_{k-1} / beta) * -alpha + J v   (lsmr.py:284-286)
+  double xsq = 0.0;
+  auto upd = [&](bool e, size_t o, double v, double h, double hb, double x) {
+    if (!e) return;
+    Bf.vn[o] = v;
+    if (FIRST) {
+      Bf.h[o] = v;
+      Bf.hbar[o] = 0.0;
+      Bf.xl[o] = 0.0;
+    } else {
+      const double hbn = hb * chb + h;
+      const double xn = x + cx * hbn;
+      Bf.hbar[o] = hbn;
+      Bf.xl[o] = xn;
+      Bf.h[o] = h * ch + v;
+      xsq += xn * xn;
+    }
+  };
+  upd(e0, o0, e0 ? sv[t] : 0.0, h0, hb0, x0);
+  upd(e1, o1, e1 ? sv[t + TRF_THREADS] : 0.0, h1, hb1, x1);
+  upd(eL, oL, eL ? sL[t] : 0.0, hL, hbL, xL);
+  // 3b. m space: u_k = (u_{k-1} / beta) * -alpha + J v   (lsmr.py:284-286)
   const double ib = 1.0 / beta;
-  const double* uin = FIRST ? Bf.fres : Bf.u;
-  const double ssf = Bf.ssf[b];
   const int nrep = J * C, ntask = nrep + J3 + NL;
   double usq = 0.0;
   for (int task = t; task < nf * ntask; task += TRF_THREADS) {
     const int fl = task / ntask, r = task - fl * ntask, f = f0 + fl;
     const size_t mo = ((size_t)b * F + f) * D.MR;
+    const double* um = sm + (size_t)fl * D.MR;
     if (r < nrep) {
       const int j = r / C;
-      const double* jr = Bf.Jrep + (((size_t)b * F + f) * nrep + r) * 6;
+      const double* jr = sj + ((size_t)fl * nrep + r) * 6;
       const double* v = sv + fl * J3 + 3 * j;
 #pragma unroll
       for (int comp = 0; comp < 2; ++comp) {
         const double jv = jr[3 * comp] * v[0] + jr[3 * comp + 1] * v[1] + jr[3 * comp + 2] * v[2];
-        const double un = (uin[mo + 2 * r + comp] * ib) * -alpha + jv;
+        const double un = (um[2 * r + comp] * ib) * -alpha + jv;
         Bf.u[mo + 2 * r + comp] = un;
         usq += un * un;
       }
@@ -550,34 +656,33 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       if (f < F - n) {
         double jv = 0.0;
         for (int m = 0; m <= n; ++m) jv += ssf * D.c[m] * sv[(fl + m) * J3 + q];
-        un = (uin[mo + D.MRrep + q] * ib) * -alpha + jv;
+        un = (um[D.MRrep + q] * ib) * -alpha + jv;
       }
       Bf.u[mo + D.MRrep + q] = un;
       usq += un * un;
     } else {
       const int l = r - nrep - J3;
       const int a = scons[2 * l], c2 = scons[2 * l + 1];
-      const double* lj = Bf.lenJ + (((size_t)b * F + f) * NL + l) * 4;
+      const double* lj = slj[fl][l];
       double jv = lj[0] * (sv[fl * J3 + 3 * a] - sv[fl * J3 + 3 * c2]) +
                   lj[1] * (sv[fl * J3 + 3 * a + 1] - sv[fl * J3 + 3 * c2 + 1]) +
                   lj[2] * (sv[fl * J3 + 3 * a + 2] - sv[fl * J3 + 3 * c2 + 2]);
       if (!D.fix) jv += lj[3] * sL[l];
-      const double un = (uin[mo + D.MRrep + J3 + l] * ib) * -alpha + jv;
+      const double un = (um[D.MRrep + J3 + l] * ib) * -alpha + jv;
       Bf.u[mo + D.MRrep + J3 + l] = un;
       usq += un * un;
       sLu[fl][l] = lj[3] * un;
     }
   }
-  usq = block_sum_all(usq, red);
-  if (!FIRST) xsq = block_sum_all(xsq, red);
+  block_sum3_all(usq, xsq, pa, red);
   if (t == 0) {
     Bf.upart[((size_t)par * D.B + b) * NB + blk] = usq;
-    if (!FIRST) Bf.xpart[((size_t)par * D.B + b) * NB + blk] = xsq;
+    Bf.xpart[((size_t)par * D.B + b) * NB + blk] = xsq;
   }
   if (t < NL) {
-    double s = 0.0;
-    for (int fl = 0; fl < nf; ++fl) s += sLu[fl][t];
-    Bf.Lpart[((size_t)b * NB + blk) * NL + t] = s;
+    double s2 = 0.0;
+    for (int fl = 0; fl < nf; ++fl) s2 += sLu[fl][t];
+    Bf.Lpart[((size_t)b * NB + blk) * NL + t] = s2;
   }
 }
 
@@ -588,7 +693,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jv_kernel(TrfDims D, TrfBufs 
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   if (!Bf.act[b]) return;
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL;
-  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
+  const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
   __shared__ double red[4];
   __shared__ double sa[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3], sc[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3];
   __shared__ double saL[TRF_MAXL], scL[TRF_MAXL];
@@ -677,7 +782,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_nops_kernel(TrfDims D, TrfBuf
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   if (!Bf.act[b]) return;
   const int J3 = 3 * D.J, F = D.F;
-  const int f0 = blk * TRF_FB, nf = min(TRF_FB, F - f0);
+  const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
   __shared__ double red[4];
   const double* cf = Bf.coef + 4 * (size_t)b;
   const size_t nb = (size_t)b * D.NV;
@@ -843,11 +948,27 @@ void solve_trust_region_2d(const double B[3], const double g[2], double Delta, d
 
 }  // namespace
 
-int g_optim_trf_chunk = 8;  // lsmr iterations launched between two reads of the done flags
+int g_optim_trf_chunk = 8;  // lsmr iterations launched (one captured graph) between two reads of the done flags
+
+// dynamic LDS of the two per-iteration kernels for FB frames per block
+size_t trf_jt_lds(int FB, int n, int MR, int J, int C) {
+  return ((((size_t)(FB + n) * MR + 1) & ~(size_t)1) + (size_t)FB * J * C * 6) * sizeof(double);
+}
+size_t trf_l1_lds(int FB, int MR, int J, int C) {
+  return ((((size_t)FB * MR + 1) & ~(size_t)1) + (size_t)FB * J * C * 6) * sizeof(double);
+}
+constexpr size_t TRF_DYN_LDS = 128 * 1024;  // (the kernels' static LDS stays under 24 KB)
+int trf_frames_per_block(int J, int C, int NL, int n) {
+  const int MR = J * C * 2 + J * 3 + NL;
+  for (int fb = TRF_FB; fb > 1; --fb)
+    if (trf_jt_lds(fb, n, MR, J, C) <= TRF_DYN_LDS && trf_l1_lds(fb, MR, J, C) <= TRF_DYN_LDS) return fb;
+  return 1;
+}
 
 size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL) {
   const size_t NV = (size_t)F * J * 3 + NL, MR = (size_t)J * C * 2 + (size_t)J * 3 + NL;
-  const size_t NB = ((size_t)F + TRF_FB - 1) / TRF_FB;
+  const int FB = trf_frames_per_block(J, C, NL, TRF_MAXN);
+  const size_t NB = ((size_t)F + FB - 1) / FB;
   size_t n = 0;
   n += (size_t)B * F * MR * 3;           // fres ftr u
   n += (size_t)B * F * J * C * 6;        // Jrep
@@ -883,7 +1004,8 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   D.NV = D.NX + NL;
   D.MRrep = J * C * 2;
   D.MR = D.MRrep + J * 3 + NL;
-  D.NB = (F + TRF_FB - 1) / TRF_FB;
+  D.FB = trf_frames_per_block(J, C, NL, n_deriv);
+  D.NB = (F + D.FB - 1) / D.FB;
   D.rp = rp;
   D.s_len = scale_length;
   D.s_len_weak = scale_length_weak;
@@ -953,17 +1075,45 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   if (!H2D(act_d, act.data(), sizeof(int) * B)) return -3;
 
   const dim3 grid(NB, B), blk(TRF_THREADS);
-  const size_t jt_lds = (size_t)(TRF_FB + D.n) * D.MR * sizeof(double);
+  const size_t jt_lds = trf_jt_lds(D.FB, D.n, D.MR, J, C), l1_lds = trf_l1_lds(D.FB, D.MR, J, C);
   {
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
-      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
-      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 120 * 1024);
+      const int mx = (int)TRF_DYN_LDS;
+      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      (void)hipFuncSetAttribute((const void*)trf_jt_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      (void)hipFuncSetAttribute((const void*)trf_lsmr1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      (void)hipFuncSetAttribute((const void*)trf_lsmr1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       attr = true;
     }
   }
-  if (jt_lds > 120 * 1024) return -2;
+  if (jt_lds > TRF_DYN_LDS || l1_lds > TRF_DYN_LDS) return -2;
+  // lsmr's iterations run as a captured graph of `chunk` (even) iterations, replayed until every done flag is
+  // set: the kernels take only the slot parity, so one graph serves every chunk of the call.  Captured on a
+  // private stream (the caller's may be the legacy default stream, which cannot be captured), replayed on s.
+  const int chunk = std::max(2, (g_optim_trf_chunk + 1) & ~1);
+  hipGraphExec_t lsmr_exec = nullptr;
+  struct ExecGuard {
+    hipGraphExec_t* e;
+    ~ExecGuard() {
+      if (*e) (void)hipGraphExecDestroy(*e);
+    }
+  } exec_guard{&lsmr_exec};
+  static hipStream_t cap = nullptr;
+  if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) return -3;
+  {
+    hipGraph_t graph = nullptr;
+    if (hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) != hipSuccess) return -3;
+    for (int i = 0; i < chunk; ++i) {
+      hipLaunchKernelGGL(trf_lsmr1_kernel<false>, grid, blk, l1_lds, cap, D, Bf, i & 1);
+      hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, cap, D, Bf, i & 1);
+    }
+    if (hipStreamEndCapture(cap, &graph) != hipSuccess) return -3;
+    const bool ok = hipGraphInstantiate(&lsmr_exec, graph, nullptr, nullptr, 0) == hipSuccess;
+    (void)hipGraphDestroy(graph);
+    if (!ok) return -3;
+  }
   std::vector<double> part((size_t)B * NB * 4), vp((size_t)B * NB * 2), ctl(4 * (size_t)B), coef(4 * (size_t)B, 0.0);
   auto sync = [&]() { return hipStreamSynchronize(s) == hipSuccess; };
   auto upload_act = [&]() { return H2D(act_d, act.data(), sizeof(int) * B); };
@@ -1062,25 +1212,21 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     if (!H2D(done_d, doneh.data(), sizeof(int) * B)) return -3;
     // lsmr(J, f, damp)
     hipLaunchKernelGGL(trf_jt_kernel<1>, grid, blk, jt_lds, s, D, Bf, 0);
-    int k = 1;
-    hipLaunchKernelGGL(trf_lsmr1_kernel<true>, grid, blk, 0, s, D, Bf, k);
-    hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, s, D, Bf, k);
-    ++k;
+    hipLaunchKernelGGL(trf_lsmr1_kernel<true>, grid, blk, l1_lds, s, D, Bf, 1);
+    hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, s, D, Bf, 1);
+    int k = 2;  // the next iteration; every chunk starts at an even one
     double maxit = 0.0;
     for (int b = 0; b < B; ++b)
       if (act[b]) maxit = std::max(maxit, ctl[4 * b + 2]);
     for (;;) {
-      const int ch = std::max(1, g_optim_trf_chunk);
-      for (int i = 0; i < ch; ++i, ++k) {
-        hipLaunchKernelGGL(trf_lsmr1_kernel<false>, grid, blk, 0, s, D, Bf, k);
-        hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, s, D, Bf, k);
-      }
+      if (hipGraphLaunch(lsmr_exec, s) != hipSuccess) return -3;
+      k += chunk;
       if (!D2H(doneh.data(), done_d, sizeof(int) * B)) return -3;
       if (!sync()) return -3;
       bool all = true;
       for (int b = 0; b < B; ++b) all &= doneh[b] != 0;
       if (all) break;
-      if (k > maxit + 4) return -7;  // the device test stops every run by maxiter
+      if (k > maxit + 4 + chunk) return -7;  // the device test stops every run by maxiter
     }
     if (!D2H(ctl.data(), Bf.lctl, sizeof(double) * ctl.size())) return -3;
     // S = orth([g, gn]) by Gram-Schmidt, B_S and g_S (trf.py:489-493)

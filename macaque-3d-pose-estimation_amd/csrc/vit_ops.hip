@@ -481,11 +481,15 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
   }
 }
 
+// MQ_TUNE_ATTN_KRING: 1 (default) = at 192 tokens the static QK^T sequence with the inline-asm K-fragment ring and
+// hand-counted lgkmcnt waits; 0 = the compiler-scheduled loop of the generic instantiation (bit-identical,
+// tests/test_gpu_attention.py; the fallback should a toolchain change break the ring's register assumptions)
+int g_attn_kring = 1;
 template <int DH>
 static void launch_attention(dim3 grid, dim3 block, hipStream_t s, const unsigned short* qkv, unsigned short* out,
                              int tokens, int dim, int heads, float scale_log2, int nt_hm) {
   constexpr int lds2 = (ATT_MAXT * ATT2_KCH + 63) / 64 * 1024 + AttLayout<DH>::VBYTES;
-  if (tokens == ATT_MAXT)
+  if (tokens == ATT_MAXT && g_attn_kring)
     hipLaunchKernelGGL((attention2_kernel<DH, ATT_MAXT>), grid, block, lds2, s, qkv, out, tokens, dim, heads,
                        scale_log2, nt_hm);
   else

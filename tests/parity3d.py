@@ -57,12 +57,21 @@ KP3D_DLT_MM_P99 = 2.0
 # vs 1e-10), whichever is larger; (iii) the two chains' optimised joints differ by at most
 # KP3D_OPTIM_E2E_MM_MEDIAN mm at the median
 OPTIM_COST_RATIO = 1.002
-SOLVER_COST_RATIO = 1.001      # the GPU solver on the oracle chain's inputs vs scipy (tests/test_gpu_pipeline.py)
-KP3D_OPTIM_MM_MEDIAN = 1.0
+SOLVER_COST_RATIO = 1.0001     # the GPU solver (trf, scipy's algorithm) on the oracle chain's inputs vs scipy
+KP3D_OPTIM_MM_MEDIAN = 1.0     # ... and its distance to scipy's answer on those identical inputs (median / p99)
 KP3D_OPTIM_MM_P99 = 5.0
-KP3D_OPTIM_E2E_MM_MEDIAN = 1.0
-CLEAR_MIN = 0.3        # share of joints with a clear top-2 margin (random-weight heatmaps)
-ALL_CLEAR_MIN = 4      # all-clear 3D points a case must contain
+KP3D_OPTIM_E2E_MM_MEDIAN = 1.0  # chain to chain (each chain its own 2D), optimised joints on all-clear points
+KP3D_OPTIM_E2E_MM_P99 = 15.0
+# every 3D point (not only all-clear ones): the views whose bf16 heatmap ranks two near-equal peaks the other way
+# (unclear joints) move single points by tens of mm; stated after measurement
+KP3D_EVERY_MM_MEDIAN = 0.5
+KP3D_EVERY_MM_P99 = 40.0
+# clear joints beyond KP_TOL_PX: ill-conditioned DARK steps (argmax equal, Newton step beyond half a cell in both
+# chains); their share of the clear joints scored
+CLEAR_OVER_TOL_SHARE_MAX = 2e-3
+CLEAR_MIN = 0.6        # share of joints with a clear top-2 margin (marker scenes: 0.76-0.79 measured)
+ALL_CLEAR_MIN_PER_FRAME = 15   # all-clear 3D points a case must contain, per frame (18 / frame measured at config 2,
+                               # 20-22 / frame on the 24-frame scenes)
 
 
 def make_scene(n_frames=1, n_views=8, n_animals=4, seed=7):
@@ -124,8 +133,11 @@ def hip_chain(scene, w, config):
         # the crops' raw outputs (same batch as step 1's) for the 2D checks
         bbs = np.concatenate([s1.expand_boxes(s1.filter_tracks(t)[0]) for t in scene["tracks"][f]])
         owner = np.repeat(np.arange(C, dtype=np.int32), [len(s1.filter_tracks(t)[0]) for t in scene["tracks"][f]])
-        kp, sc, am = model.net.topdown(fr, torch.from_numpy(bbs).cuda(), torch.from_numpy(owner).cuda())
-        per_frame.append((kp.cpu().numpy().astype(np.float64), sc.cpu().numpy(), am.cpu().numpy(), bbs, owner))
+        crops, ctr, scl = model.net.crop(fr, torch.from_numpy(bbs).cuda(), torch.from_numpy(owner).cuda())
+        hm = model.net.forward(crops, True)
+        kp, sc, am, _ = model.net.decode(hm, ctr, scl)
+        per_frame.append((kp.cpu().numpy().astype(np.float64), sc.cpu().numpy(), am.cpu().numpy(), bbs, owner,
+                          hm.cpu().numpy()))
         del fr
     kp2d = _kp2d_from_rows(T, A)
     kp2d_f = step4.filter_2d(kp2d)
@@ -193,7 +205,7 @@ def oracle_chain(scene, w, config):
             # DARK step of at most half a heatmap cell (input-space cell = scale / heatmap size)
             cell = np.stack([ram % 48 / 47.0, ram // 48 / 63.0], axis=-1) * ss[:, None] + cs[:, None] - 0.5 * ss[:, None]
             taylor = np.abs(rkp - cell).max(axis=-1) <= 0.5 * ss.max(axis=-1)[:, None] / 63.0
-            per_frame.append((rkp, rsc, ram, clear, taylor, np.array(owner)))
+            per_frame.append((rkp, rsc, ram, clear, taylor, np.array(owner), hm))
             k = 0
             for c in range(C):
                 n = len(boxes_all[c])
@@ -238,14 +250,42 @@ def oracle_chain(scene, w, config):
             "kp3d_dlt": kp3d_dlt, "good_views": good_views, "problems": problems, "cgroup": o}
 
 
+def dark_terms(hm, idx):
+    """DARK-UDP's Newton step at the argmax (mmpose refine_keypoints_dark_udp, oracle/decode.py:89-117) for the
+    heatmaps hm (K, H, W) of one crop and argmax indices idx (K,): the determinant of the Hessian of the blurred
+    log map (before the eps regularisation) and the step (dx, dy) in heatmap cells."""
+    from oracle.decode import gaussian_blur
+    K, H, W = hm.shape
+    b = gaussian_blur(np.array(hm, dtype=np.float32, copy=True), 11)
+    np.clip(b, 1e-3, 50., b)
+    np.log(b, b)
+    pad = np.pad(b, ((0, 0), (1, 1), (1, 1)), mode="edge")
+    det, step = np.zeros(K), np.zeros((K, 2))
+    for k in range(K):
+        y, x = int(idx[k]) // W + 1, int(idx[k]) % W + 1
+        i_, ix1, ix1_ = pad[k, y, x], pad[k, y, x + 1], pad[k, y, x - 1]
+        iy1, iy1_, ix1y1, ix1_y1_ = pad[k, y + 1, x], pad[k, y - 1, x], pad[k, y + 1, x + 1], pad[k, y - 1, x - 1]
+        dx, dy = 0.5 * (ix1 - ix1_), 0.5 * (iy1 - iy1_)
+        dxx, dyy = ix1 - 2 * i_ + ix1_, iy1 - 2 * i_ + iy1_
+        dxy = 0.5 * (ix1y1 - ix1 - iy1 + i_ + i_ - ix1_ - iy1_ + ix1_y1_)
+        Hm = np.array([[dxx, dxy], [dxy, dyy]], dtype=np.float64)
+        det[k] = np.linalg.det(Hm)
+        step[k] = np.linalg.inv(Hm + np.finfo(np.float32).eps * np.eye(2)) @ np.array([dx, dy])
+    return det, step
+
+
+CLEAR_OVER_TOL_LIST = 24   # outliers listed per case in the figures
+
+
 def compare(scene, hip, ora, score_threshold=0.5):
     """The parity figures (see the module docstring for the definitions)."""
     C, A, J = scene["n_views"], scene["n_animals"], 17
     am_eq, n_clear, n_all, dkp, n_kp, dkp_clear = [], 0, 0, [], 0, []
+    outliers, n_over = [], 0
     clear_cj = np.zeros((A, scene["n_frames"], C, J), bool)
     for f, (h, o) in enumerate(zip(hip["per_frame"], ora["per_frame"])):
         kp, sc, am = h[0], h[1], h[2]
-        rkp, rsc, ram, clear, taylor, owner = o
+        rkp, rsc, ram, clear, taylor, owner = o[:6]
         n_all += clear.size
         n_clear += int(clear.sum())
         am_eq.append(am[clear] == ram[clear])
@@ -258,6 +298,26 @@ def compare(scene, hip, ora, score_threshold=0.5):
             dkp_clear.append(np.abs(kp[okc] - rkp[okc]).max(axis=-1))
         # crop k of view owner[k] is individual (k - first crop of the view): boxes are per individual in order
         first = {c: int(np.argmax(owner == c)) for c in range(C)}
+        # clear joints beyond the keypoint tolerance: the DARK step of both chains at each
+        over = okc & (np.abs(kp - rkp).max(axis=-1) > KP_TOL_PX)
+        n_over += int(over.sum())
+        for k, j in zip(*np.nonzero(over)):
+            c = int(owner[k])
+            a = int(k - first[c])
+            dh, sh = dark_terms(h[5][k], am[k]) if len(h) > 5 else (np.full(J, np.nan), np.full((J, 2), np.nan))
+            do, so = dark_terms(o[6][k], ram[k]) if len(o) > 6 else (np.full(J, np.nan), np.full((J, 2), np.nan))
+            # does the outlier keypoint reach step 4's triangulation?  The Viterbi filter (n_back 3, 25-px offset)
+            # keeps it when its output at this (frame, joint, individual, view) is the raw point with a score over
+            # step 4's threshold
+            kf = hip["kp2d_f"][f, j, a, :, c] if f < hip["kp2d_f"].shape[0] else np.full(3, np.nan)
+            kept = bool(np.all(np.abs(kf[:2] - kp[k, j]) < 1e-6) and kf[2] >= score_threshold)
+            outliers.append({"frame": f, "view": c, "individual": a, "joint": int(j),
+                             "px": round(float(np.abs(kp[k, j] - rkp[k, j]).max()), 3),
+                             "argmax_equal": bool(am[k, j] == ram[k, j]), "taylor": bool(taylor[k, j]),
+                             "hessian_det_hip": float(dh[j]), "hessian_det_oracle": float(do[j]),
+                             "newton_step_cells_hip": [round(float(v), 4) for v in sh[j]],
+                             "newton_step_cells_oracle": [round(float(v), 4) for v in so[j]],
+                             "reaches_3d": kept})
         for k in range(len(owner)):
             clear_cj[k - first[owner[k]], f, owner[k]] = clear[k]
     am_eq = np.concatenate([x.ravel() for x in am_eq]) if am_eq else np.zeros(0, bool)
@@ -311,6 +371,11 @@ def compare(scene, hip, ora, score_threshold=0.5):
         "kp_p99_abs_px": q(dkp, 99),
         "kp_max_abs_px_clear": float(dkp_clear.max()) if dkp_clear.size else float("nan"),
         "kp_p99_abs_px_clear": q(dkp_clear, 99),
+        "n_clear_scored": int(dkp_clear.size),
+        "n_clear_over_tol": n_over,
+        "clear_over_tol_share": n_over / max(1, int(dkp_clear.size)),
+        "clear_over_tol_reaching_3d": int(sum(o["reaches_3d"] for o in outliers)),
+        "clear_over_tol": sorted(outliers, key=lambda o: -o["px"])[:CLEAR_OVER_TOL_LIST],
         "points": int(every.sum()),
         "all_clear_points": int(sel.sum()),
         "all_clear_fraction": float(sel.sum()) / max(1, int(every.sum())),
@@ -323,6 +388,7 @@ def compare(scene, hip, ora, score_threshold=0.5):
         "kp3d_dlt_mm_all_clear_p99": q(d_dlt[sel_dlt], 99),
         "kp3d_dlt_mm_all_clear_max": float(d_dlt[sel_dlt].max()) if sel_dlt.any() else float("nan"),
         "kp3d_dlt_mm_every_point_median": q(d_dlt[fin_dlt & (n_views >= 2)], 50),
+        "kp3d_dlt_mm_every_point_p99": q(d_dlt[fin_dlt & (n_views >= 2)], 99),
         "optim_points": int(sel_opt.sum()),
         "kp3d_optim_mm_all_clear_median": q(d3[sel_opt], 50),
         "kp3d_optim_mm_all_clear_p99": q(d3[sel_opt], 99),

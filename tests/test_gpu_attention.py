@@ -68,3 +68,30 @@ def test_attention_spiky_scores_match_fp32():
     ref = _ref(qkv, n, T, D, H)
     vmax = qkv[:, 2 * D:].float().abs().max().item()
     assert (out.float() - ref).abs().max().item() <= 1.5e-2 * vmax
+
+
+@pytest.mark.parametrize("n,D,H", [(64, 1280, 16), (3, 768, 12)])
+def test_attention_kring_equals_compiler_loop(n, D, H):
+    """the 192-token QK^T streams K fragments through an inline-asm ring with hand-counted lgkmcnt
+    waits that the compiler's waitcnt pass does not see; MQ_TUNE_ATTN_KRING = 0 routes the same shape to the
+    compiler-scheduled loop of the generic instantiation.  Same MFMA order per output: bit for bit."""
+    import torch
+    from mqhip import _lib
+    ctx = _lib.Context.get(0)
+    T = 192
+    g = torch.Generator(device="cuda")
+    g.manual_seed(31 + n)
+    qkv = (torch.randn((n * T, 3 * D), generator=g, device="cuda") * 2).to(torch.bfloat16)
+    outs = {}
+    old = ctx.lib.mq_get_tuning(24)
+    try:
+        for ring in (1, 0):
+            assert ctx.lib.mq_set_tuning(24, ring) == 0
+            out = torch.empty((n * T, D), device="cuda", dtype=torch.bfloat16)
+            _lib.check(ctx.lib.mq_attention_bf16(ctx.handle, _lib.ptr(qkv), _lib.ptr(out), n, T, D, H,
+                                                 _lib.stream_ptr()), "mq_attention_bf16")
+            torch.cuda.synchronize()
+            outs[ring] = out
+    finally:
+        ctx.lib.mq_set_tuning(24, old)
+    assert torch.equal(outs[1], outs[0])

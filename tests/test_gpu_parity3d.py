@@ -10,13 +10,16 @@ default step 4 (Viterbi -> DLT -> optim_points, ``ransac = false``).  Stated tol
   * keypoints within 0.5 px (SURVEY 8(d)) on clear, Taylor-regime joints;
   * on all-clear points (every kept view clear, both chains keep the same views; at least ALL_CLEAR_MIN):
     the DLT of the score-thresholded views within KP3D_DLT_MM_MEDIAN / KP3D_DLT_MM_P99 mm (median / p99) --
-    the bf16 path's 2D differences carried into 3D; and, where optim_points ran (the reference default,
-    >= 20 points per individual), GPU LM and scipy TRF stop early at different points of the same problem,
-    so: the GPU solver on the oracle chain's own 2D costs at most SOLVER_COST_RATIO x scipy's; the HIP
-    chain's solution, scored by the oracle's objective on the oracle's inputs, at most OPTIM_COST_RATIO x;
-    both lie within max(scipy's own ftol 1e-3 vs 1e-10 band, KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99) of
-    the converged (ftol 1e-10) solution; the chains' optimised joints differ by at most
-    KP3D_OPTIM_E2E_MM_MEDIAN mm (median).
+    the bf16 path's 2D differences carried into 3D;
+  * clear joints beyond 0.5 px: at most CLEAR_OVER_TOL_SHARE_MAX of the clear joints, each an ill-conditioned
+    DARK step (argmax equal, not in the Taylor regime) -- their Hessian determinants and Newton steps in both
+    chains and whether they reach the triangulation are listed in the figures;
+  * every 3D point (median / p99 of the DLT and of the final kp3d) within KP3D_EVERY_MM_*;
+  * where optim_points ran (the reference default, >= 20 points per individual): the GPU solver (trf, scipy's own
+    algorithm) on the oracle chain's 2D lands within KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99 of scipy's answer
+    with a cost within SOLVER_COST_RATIO; the HIP chain's solution, scored by the oracle's objective on the
+    oracle's inputs, costs at most OPTIM_COST_RATIO x scipy's; the chains' optimised joints on all-clear points
+    differ by at most KP3D_OPTIM_E2E_MM_MEDIAN / KP3D_OPTIM_E2E_MM_P99 mm (median / p99).
 """
 import json
 
@@ -45,18 +48,27 @@ def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames, seed):
     assert fig["argmax_equal_on_clear"] == 1.0
     assert fig["clear_fraction"] >= parity3d.CLEAR_MIN
     assert fig["n_clear_taylor_scored"] > 0 and fig["kp_max_abs_px"] <= parity3d.KP_TOL_PX
-    assert fig["all_clear_points"] >= parity3d.ALL_CLEAR_MIN
+    assert fig["all_clear_points"] >= parity3d.ALL_CLEAR_MIN_PER_FRAME * n_frames
     assert fig["kp3d_dlt_mm_all_clear_median"] <= parity3d.KP3D_DLT_MM_MEDIAN
     assert fig["kp3d_dlt_mm_all_clear_p99"] <= parity3d.KP3D_DLT_MM_P99
+    # clear joints beyond the keypoint tolerance: a small share, every one an ill-conditioned DARK step (argmax equal,
+    # Newton step beyond half a heatmap cell, both chains' steps of the same size and sign) -- VERDICT r4 item 2
+    assert fig["clear_over_tol_share"] <= parity3d.CLEAR_OVER_TOL_SHARE_MAX
+    for o in fig["clear_over_tol"]:
+        assert o["argmax_equal"] and not o["taylor"], o
+    # every 3D point (median / p99), final kp3d and the DLT alone
+    assert fig["kp3d_dlt_mm_every_point_median"] <= parity3d.KP3D_EVERY_MM_MEDIAN
+    assert fig["kp3d_dlt_mm_every_point_p99"] <= parity3d.KP3D_EVERY_MM_P99
+    assert fig["kp3d_mm_every_point_median"] <= parity3d.KP3D_EVERY_MM_MEDIAN
+    assert fig["kp3d_mm_every_point_p99"] <= parity3d.KP3D_EVERY_MM_P99
     if fig["optim_points"]:
-        # the GPU optim_points against scipy on the oracle chain's own (ViT-derived) 2D inputs: cost within
-        # 0.1 % of scipy's, and no farther from the converged solution than scipy's own ftol-1e-3 stop is
+        # the GPU optim_points (trf: scipy's algorithm) against scipy on the oracle chain's own (ViT-derived) 2D:
+        # scipy's answer within 1 mm (median) / 5 mm (p99), cost within 1e-4
         assert fig["solver_cost_ratio_max"] <= parity3d.SOLVER_COST_RATIO
-        assert fig["solver_to_converged_mm_median"] <= max(fig["scipy_band_all_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
-        assert fig["solver_to_converged_mm_p99"] <= max(fig["scipy_band_all_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
-        # end to end (each chain its own 2D): the same two statements on all-clear points, and the median
-        # distance between the chains' optimised joints
+        assert fig["solver_vs_scipy_mm_median"] <= parity3d.KP3D_OPTIM_MM_MEDIAN
+        assert fig["solver_vs_scipy_mm_p99"] <= parity3d.KP3D_OPTIM_MM_P99
+        # end to end (each chain its own 2D): the HIP chain's solution scored on the oracle's inputs, and the
+        # distance between the chains' optimised joints on all-clear points (median and p99)
         assert fig["optim_cost_ratio_max"] <= parity3d.OPTIM_COST_RATIO
-        assert fig["kp3d_optim_to_converged_mm_median"] <= max(fig["scipy_band_mm_median"], parity3d.KP3D_OPTIM_MM_MEDIAN)
-        assert fig["kp3d_optim_to_converged_mm_p99"] <= max(fig["scipy_band_mm_p99"], parity3d.KP3D_OPTIM_MM_P99)
         assert fig["kp3d_optim_mm_all_clear_median"] <= parity3d.KP3D_OPTIM_E2E_MM_MEDIAN
+        assert fig["kp3d_optim_mm_all_clear_p99"] <= parity3d.KP3D_OPTIM_E2E_MM_P99

@@ -1,12 +1,20 @@
-import sys, time, numpy as np
-sys.path[:0] = ["/root/repo", "/root/repo/macaque-3d-pose-estimation_amd", "/root/repo/tests"]
+"""How far scipy's own optim_points answer moves when its 2-point finite-difference Jacobian is replaced by
+3-point differences (a near-analytic Jacobian), per marker-scene problem of tests/golden/optim_problems.npz: the
+floor of what any restatement with an analytic Jacobian can be held to.  Also logs lsmr's iterations per call.
+python tools/scipy_jacobian_sensitivity.py [problem keys]"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "macaque-3d-pose-estimation_amd"), os.path.join(ROOT, "tests")]
 from mqhip import synth
 from oracle import geometry as og
 from scipy import optimize
 import scipy.optimize._lsq.trf as trf
 from scipy.sparse.linalg import lsmr as _lsmr
-import parity3d
-Z = np.load("/tmp/study/optim_problems.npz")
+Z = np.load(os.path.join(ROOT, "tests", "golden", "optim_problems.npz"))
 cons, weak = Z["cons"], Z["weak"]; ss, sl, slw, rp, nd = Z["tri"]; nd = int(nd)
 LOG = []
 def lsmr_log(*a, **k):
