@@ -293,3 +293,43 @@ def test_vitpose_h_config2_marker_keypoints():
           f"all clear joints: max {dall[clear].max():.4f} px, p99 {np.percentile(dall[clear], 99):.4f} px")
     assert ok.mean() >= KP_TAYLOR_MIN and d.max() <= KP_TOL_PX
     np.testing.assert_allclose(score.cpu().numpy()[clear], rsc[clear], rtol=HM_TOL)
+
+
+# precision budget of the round-4 residual path (bf16 branch outputs added in the LayerNorm passes) against the
+# f32 read-modify-write epilogues of rounds 1-3 (MQ_TUNE_VIT_RESID_F32), full-scale random-weight ViT-H
+# (tools/precision_ab.py, profiles/r05e_precision_ab.log)
+RESID_BF16_ERR_BUDGET = 1.25   # max rel heatmap error of the bf16 path <= this x the f32-epilogue path's
+
+
+def test_vit_residual_precision_ab_full_scale_branches():
+    """the same crops and full-scale random ViT-H weights (every residual update at its natural size)
+    through both residual paths in one process, against the fp32 oracle: both within HM_TOL per crop, and the
+    bf16-branch path's worst error within RESID_BF16_ERR_BUDGET of the f32-epilogue path's."""
+    import torch
+    from mqhip import _lib
+    from mqhip.pose import VitPoseHip
+    from mqhip.weights import VIT_H, make_random_weights
+    from oracle.vitpose import forward_flip_test
+    ctx = _lib.Context.get(0)
+    w = make_random_weights(VIT_H, seed=3, device="cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    crops = torch.randn((8, 3, 256, 192), generator=g, device="cuda", dtype=torch.float32)
+    with torch.no_grad():
+        torch.backends.cuda.matmul.allow_tf32 = False
+        torch.backends.cudnn.allow_tf32 = False
+        ref = forward_flip_test(crops, w, VIT_H)[0].float().cpu().numpy()
+    errs = {}
+    old = ctx.lib.mq_get_tuning(23)
+    try:
+        for knob in (1, 0):
+            assert ctx.lib.mq_set_tuning(23, knob) == 0
+            model = VitPoseHip(VIT_H, w, graph=False)
+            got = model.forward(crops, flip_test=True).float().cpu().numpy()
+            del model
+            errs[knob] = np.array([np.abs(got[i] - ref[i]).max() / np.abs(ref[i]).max() for i in range(8)])
+    finally:
+        ctx.lib.mq_set_tuning(23, old)
+    print("max rel err: f32 epilogue %.5f, bf16 branches %.5f" % (errs[1].max(), errs[0].max()))
+    assert errs[1].max() <= HM_TOL and errs[0].max() <= HM_TOL
+    assert errs[0].max() <= RESID_BF16_ERR_BUDGET * errs[1].max()
