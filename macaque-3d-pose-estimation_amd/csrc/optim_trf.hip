@@ -124,6 +124,46 @@ __device__ __forceinline__ void sym_ortho(double a, double b, double& c, double&
   }
 }
 
+
+// Global -> LDS staging with every load of a thread issued before its LDS stores (a plain copy loop waits on
+// each load before the next iteration's: one memory round trip per element a thread copies).  stage16: 16-B
+// loads, src and dst 16-B aligned, n even; stage8: 8-B loads, any alignment.
+template <int U = 8>
+__device__ __forceinline__ void stage16(double* __restrict__ dst, const double* __restrict__ src, int n) {
+  const int n2 = n >> 1;
+  const double2* s2 = reinterpret_cast<const double2*>(src);
+  double2* d2 = reinterpret_cast<double2*>(dst);
+  for (int base = 0; base < n2; base += TRF_THREADS * U) {
+    double2 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * TRF_THREADS + (int)threadIdx.x;
+      if (i < n2) r[u] = s2[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * TRF_THREADS + (int)threadIdx.x;
+      if (i < n2) d2[i] = r[u];
+    }
+  }
+}
+template <int U = 8>
+__device__ __forceinline__ void stage8(double* __restrict__ dst, const double* __restrict__ src, int n) {
+  for (int base = 0; base < n; base += TRF_THREADS * U) {
+    double r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * TRF_THREADS + (int)threadIdx.x;
+      if (i < n) r[u] = src[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = base + u * TRF_THREADS + (int)threadIdx.x;
+      if (i < n) dst[i] = r[u];
+    }
+  }
+}
+
 // lsmr state slot
 enum {
   S_ALPHABAR, S_RHO, S_RHOBAR, S_CBAR, S_SBAR, S_ZETABAR, S_ZETA, S_BETADD, S_BETAD, S_RHODOLD, S_TAUTILDEOLD,
@@ -147,7 +187,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_eval_kernel(TrfDims D, TrfBuf
   __shared__ double red[4];
   const double* xb = x + (size_t)b * D.NV;
   const int nfx = min(nf + n, F - f0);
-  for (int i = t; i < nfx * J3; i += TRF_THREADS) sx[i] = xb[(size_t)f0 * J3 + i];
+  stage8(sx, xb + (size_t)f0 * J3, nfx * J3);
   if (t < NL) sL[t] = xb[D.NX + t];
   if (t < 2 * NL) scons[t] = Bf.cons[t];
   __syncthreads();
@@ -267,8 +307,7 @@ __device__ __forceinline__ void block_sum3_all(double& a, double& b, double& c, 
 // the block's Jacobian rows (reprojection: J C 6 doubles per frame) into LDS
 __device__ __forceinline__ void stage_jrep(const TrfDims& D, const TrfBufs& Bf, int b, int f0, int nf, double* sj) {
   const int per = D.J * D.C * 6;
-  const double* src = Bf.Jrep + ((size_t)b * D.F + f0) * per;
-  for (int i = threadIdx.x; i < nf * per; i += TRF_THREADS) sj[i] = src[i];
+  stage16(sj, Bf.Jrep + ((size_t)b * D.F + f0) * per, nf * per);
 }
 
 // Length variables of block 0: sum over the NB blocks of the per-block partials lp[bb * NL + l], fixed order
@@ -329,7 +368,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
   if (MODE == 2)
     for (int i = t; i < NB; i += TRF_THREADS) pu += Bf.upart[((size_t)par * D.B + b) * NB + i];
   const double* ub = uin + ((size_t)b * F + fa) * D.MR;
-  for (int i = t; i < nrow; i += TRF_THREADS) su[i] = ub[i];
+  stage16(su, ub, nrow);
   stage_jrep(D, Bf, b, f0, nf, sj);
   for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
   for (int i = t; i < nf * NL * 3; i += TRF_THREADS) {
@@ -525,11 +564,11 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
   }
   if (!FIRST && t < TRF_NS) sS[t] = Bf.st[((size_t)pp * D.B + b) * TRF_NS + t];
   const int nfx = min(nf + n, F - f0);
-  for (int i = t; i < nfx * J3; i += TRF_THREADS) sv[i] = Bf.vraw[nb + (size_t)f0 * J3 + i];
+  stage8(sv, Bf.vraw + nb + (size_t)f0 * J3, nfx * J3);
   if (t < NL) sL[t] = D.fix ? 0.0 : Bf.vraw[nb + D.NX + t];
   const double* uin = FIRST ? Bf.fres : Bf.u;
   const double* ub = uin + ((size_t)b * F + f0) * D.MR;
-  for (int i = t; i < nf * D.MR; i += TRF_THREADS) sm[i] = ub[i];
+  stage16(sm, ub, nf * D.MR);
   stage_jrep(D, Bf, b, f0, nf, sj);
   for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
   for (int i = t; i < nf * NL * 4; i += TRF_THREADS) {
@@ -959,14 +998,14 @@ size_t trf_l1_lds(int FB, int MR, int J, int C) {
 }
 constexpr size_t TRF_DYN_LDS = 128 * 1024;  // (the kernels' static LDS stays under 24 KB)
 int trf_frames_per_block(int J, int C, int NL, int n) {
-  const int MR = J * C * 2 + J * 3 + NL;
+  const int MR = (J * C * 2 + J * 3 + NL + 1) & ~1;
   for (int fb = TRF_FB; fb > 1; --fb)
     if (trf_jt_lds(fb, n, MR, J, C) <= TRF_DYN_LDS && trf_l1_lds(fb, MR, J, C) <= TRF_DYN_LDS) return fb;
   return 1;
 }
 
 size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL) {
-  const size_t NV = (size_t)F * J * 3 + NL, MR = (size_t)J * C * 2 + (size_t)J * 3 + NL;
+  const size_t NV = (size_t)F * J * 3 + NL, MR = ((size_t)J * C * 2 + (size_t)J * 3 + NL + 1) & ~(size_t)1;
   const int FB = trf_frames_per_block(J, C, NL, TRF_MAXN);
   const size_t NB = ((size_t)F + FB - 1) / FB;
   size_t n = 0;
@@ -1003,7 +1042,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   D.NX = F * J * 3;
   D.NV = D.NX + NL;
   D.MRrep = J * C * 2;
-  D.MR = D.MRrep + J * 3 + NL;
+  D.MR = (D.MRrep + J * 3 + NL + 1) & ~1;  // even: 16-B aligned rows for the LDS staging
   D.FB = trf_frames_per_block(J, C, NL, n_deriv);
   D.NB = (F + D.FB - 1) / D.FB;
   D.rp = rp;
@@ -1102,6 +1141,17 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   } exec_guard{&lsmr_exec};
   static hipStream_t cap = nullptr;
   if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) return -3;
+  static int* pinned_done = nullptr;
+  static int pinned_cap = 0;
+  static hipEvent_t done_ev[2] = {nullptr, nullptr};
+  if (pinned_cap < 2 * B) {
+    if (pinned_done) (void)hipHostFree(pinned_done);
+    pinned_done = nullptr;
+    if (hipHostMalloc((void**)&pinned_done, sizeof(int) * 2 * (size_t)B, hipHostMallocDefault) != hipSuccess) return -3;
+    pinned_cap = 2 * B;
+  }
+  for (auto& e : done_ev)
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -3;
   {
     hipGraph_t graph = nullptr;
     if (hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) != hipSuccess) return -3;
@@ -1218,15 +1268,22 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     double maxit = 0.0;
     for (int b = 0; b < B; ++b)
       if (act[b]) maxit = std::max(maxit, ctl[4 * b + 2]);
-    for (;;) {
+    // chunks run back to back: the done flags of chunk i are copied to pinned memory behind it and read
+    // while chunk i + 1 runs (a finished animal's kernels return at once), so no chunk waits on the host
+    int ci = 0;
+    for (;; ++ci) {
       if (hipGraphLaunch(lsmr_exec, s) != hipSuccess) return -3;
       k += chunk;
-      if (!D2H(doneh.data(), done_d, sizeof(int) * B)) return -3;
-      if (!sync()) return -3;
+      int* slot = pinned_done + (size_t)(ci & 1) * B;
+      if (hipMemcpyAsync(slot, done_d, sizeof(int) * B, hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
+      if (hipEventRecord(done_ev[ci & 1], s) != hipSuccess) return -3;
+      if (ci == 0) continue;
+      if (hipEventSynchronize(done_ev[(ci - 1) & 1]) != hipSuccess) return -3;
+      const int* prev = pinned_done + (size_t)((ci - 1) & 1) * B;
       bool all = true;
-      for (int b = 0; b < B; ++b) all &= doneh[b] != 0;
+      for (int b = 0; b < B; ++b) all &= prev[b] != 0;
       if (all) break;
-      if (k > maxit + 4 + chunk) return -7;  // the device test stops every run by maxiter
+      if (k > maxit + 4 + 2 * chunk) return -7;  // the device test stops every run by maxiter
     }
     if (!D2H(ctl.data(), Bf.lctl, sizeof(double) * ctl.size())) return -3;
     // S = orth([g, gn]) by Gram-Schmidt, B_S and g_S (trf.py:489-493)

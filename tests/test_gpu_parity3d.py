@@ -18,8 +18,10 @@ default step 4 (Viterbi -> DLT -> optim_points, ``ransac = false``).  Stated tol
   * where optim_points ran (the reference default, >= 20 points per individual): the GPU solver (trf, scipy's own
     algorithm) on the oracle chain's 2D lands within KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99 of scipy's answer
     with a cost within SOLVER_COST_RATIO; the HIP chain's solution, scored by the oracle's objective on the
-    oracle's inputs, costs at most OPTIM_COST_RATIO x scipy's; the chains' optimised joints on all-clear points
-    differ by at most KP3D_OPTIM_E2E_MM_MEDIAN / KP3D_OPTIM_E2E_MM_P99 mm (median / p99).
+    oracle's inputs, and the chains' optimised joints on all-clear points (median / p99), are held to scipy's own
+    move under the same 2D differences (scipy run on the HIP chain's 2D against scipy on the oracle chain's) plus
+    E2E_COST_OVER_SCIPY_SENSITIVITY / E2E_OVER_SCIPY_SENSITIVITY_MM; on the HIP chain's own 2D the GPU solver lands
+    within KP3D_OPTIM_MM_MEDIAN / KP3D_OPTIM_MM_P99 of scipy.
 """
 import json
 
@@ -67,8 +69,14 @@ def test_parity_3d_hip_chain_vs_oracle_chain(weights, n_frames, seed):
         assert fig["solver_cost_ratio_max"] <= parity3d.SOLVER_COST_RATIO
         assert fig["solver_vs_scipy_mm_median"] <= parity3d.KP3D_OPTIM_MM_MEDIAN
         assert fig["solver_vs_scipy_mm_p99"] <= parity3d.KP3D_OPTIM_MM_P99
-        # end to end (each chain its own 2D): the HIP chain's solution scored on the oracle's inputs, and the
-        # distance between the chains' optimised joints on all-clear points (median and p99)
-        assert fig["optim_cost_ratio_max"] <= parity3d.OPTIM_COST_RATIO
-        assert fig["kp3d_optim_mm_all_clear_median"] <= parity3d.KP3D_OPTIM_E2E_MM_MEDIAN
-        assert fig["kp3d_optim_mm_all_clear_p99"] <= parity3d.KP3D_OPTIM_E2E_MM_P99
+        # ... and on the HIP chain's own 2D: scipy's answer there within the same bounds
+        assert fig["hip_vs_scipy_on_hip_mm_median"] <= parity3d.KP3D_OPTIM_MM_MEDIAN
+        assert fig["hip_vs_scipy_on_hip_mm_p99"] <= parity3d.KP3D_OPTIM_MM_P99
+        # end to end (each chain its own 2D): an early-stopped solver moves with its inputs, so the chains'
+        # optimised joints are held to scipy's own move under the same 2D differences (scipy on the HIP chain's 2D
+        # vs scipy on the oracle chain's), median and p99 on all-clear points, and the HIP chain's solution scored
+        # on the oracle's inputs to the score of scipy's own solution on the HIP chain's inputs
+        s = parity3d.E2E_OVER_SCIPY_SENSITIVITY_MM
+        assert fig["kp3d_optim_mm_all_clear_median"] <= fig["scipy_sensitivity_mm_all_clear_median"] + s
+        assert fig["kp3d_optim_mm_all_clear_p99"] <= fig["scipy_sensitivity_mm_all_clear_p99"] + s
+        assert fig["optim_cost_ratio_max"] <= fig["scipy_on_hip_cost_ratio_max"] + parity3d.E2E_COST_OVER_SCIPY_SENSITIVITY

@@ -36,7 +36,7 @@ def main():
         from src.pipeline.step4_aniposefiltering import BODYPARTS, load_constraints
         cons = np.array(load_constraints(config, BODYPARTS))
         weak = np.array(load_constraints(config, BODYPARTS, "constraints_weak"))
-        for ind, (p2, targs, cost) in sorted(ora["problems"].items()):
+        for ind, (p2, targs, cost, _) in sorted(ora["problems"].items()):
             C, F, J, _ = p2.shape
             init = o.triangulate(p2.reshape(C, -1, 2)).reshape(F, J, 3)
             args = dict(scale_smooth=tri["scale_smooth"], scale_length=tri["scale_length"],

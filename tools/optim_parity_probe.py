@@ -59,7 +59,7 @@ def probe_scene(a, parity3d, config, scene, ora, seed):
         ms = (time.perf_counter() - t0) * 1e3
         rows = []
         for b, i in enumerate(run):
-            p2, targs, cost = ora["problems"][i]
+            p2, targs, cost, _ = ora["problems"][i]
             r = ora["cgroup"]._error_fun_triangulation(np.hstack([p3[b].ravel(), jl[b]]), p2, *targs)
             d = np.linalg.norm(p3[b] - ora["kp3d_tight"][i], axis=-1)
             d = d[np.isfinite(d)]
