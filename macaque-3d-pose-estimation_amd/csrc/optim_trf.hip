@@ -128,17 +128,18 @@ __device__ __forceinline__ void sym_ortho(double a, double b, double& c, double&
 // Global -> LDS staging with every load of a thread issued before its LDS stores (a plain copy loop waits on
 // each load before the next iteration's: one memory round trip per element a thread copies).  stage16: 16-B
 // loads, src and dst 16-B aligned, n even; stage8: 8-B loads, any alignment.
+typedef double trf_d2 __attribute__((ext_vector_type(2)));
 template <int U = 8>
 __device__ __forceinline__ void stage16(double* __restrict__ dst, const double* __restrict__ src, int n) {
   const int n2 = n >> 1;
-  const double2* s2 = reinterpret_cast<const double2*>(src);
-  double2* d2 = reinterpret_cast<double2*>(dst);
+  const trf_d2* s2 = reinterpret_cast<const trf_d2*>(src);
+  trf_d2* d2 = reinterpret_cast<trf_d2*>(dst);
   for (int base = 0; base < n2; base += TRF_THREADS * U) {
-    double2 r[U];
+    trf_d2 r[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < U; ++u) {  // (an out-of-range lane re-reads element 0: no conditional array writes)
       const int i = base + u * TRF_THREADS + (int)threadIdx.x;
-      if (i < n2) r[u] = s2[i];
+      r[u] = s2[i < n2 ? i : 0];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -154,7 +155,7 @@ __device__ __forceinline__ void stage8(double* __restrict__ dst, const double* _
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = base + u * TRF_THREADS + (int)threadIdx.x;
-      if (i < n) r[u] = src[i];
+      r[u] = src[i < n ? i : 0];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -162,6 +163,12 @@ __device__ __forceinline__ void stage8(double* __restrict__ dst, const double* _
       if (i < n) dst[i] = r[u];
     }
   }
+}
+
+// np.diff coefficient m of the kernel arguments by constant indices (a runtime index into the by-value
+// TrfDims made the compiler copy it to scratch: a memory round trip per use)
+__device__ __forceinline__ double dcoef(const TrfDims& D, int m) {
+  return m == 0 ? D.c[0] : (m == 1 ? D.c[1] : (m == 2 ? D.c[2] : D.c[3]));
 }
 
 // lsmr state slot
@@ -231,11 +238,20 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_eval_kernel(TrfDims D, TrfBuf
       const int q = r - nrep;
       double val = 0.0;
       if (f < F - n) {
-        double d[TRF_MAXN + 1];
-        for (int m = 0; m <= n; ++m) d[m] = sx[(fl + m) * J3 + q];
-        for (int o = 0; o < n; ++o)
-          for (int m = 0; m < n - o; ++m) d[m] = d[m + 1] - d[m];
-        val = d[0] * ssf;
+        // np.diff applied n times (numpy's order of the differences), in registers
+        const double x0 = sx[fl * J3 + q], x1 = sx[(fl + 1) * J3 + q];
+        double dd = x1 - x0;
+        if (n >= 2) {
+          const double x2 = sx[(fl + 2) * J3 + q];
+          const double e1 = x2 - x1;
+          if (n == 2) {
+            dd = e1 - dd;
+          } else {
+            const double x3 = sx[(fl + 3) * J3 + q];
+            dd = ((x3 - x2) - e1) - (e1 - dd);
+          }
+        }
+        val = dd * ssf;
         cost += val * val;
         rows += 1.0;
       }
@@ -408,7 +424,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
     }
     for (int m = 0; m <= n; ++m) {  // smoothness rows i = f - m hold frame f with coefficient c[m]
       const int i = f - m;
-      if (i >= 0 && i < F - n) acc += ssf * D.c[m] * (su[(size_t)(i - fa) * D.MR + D.MRrep + q] * ib);
+      if (i >= 0 && i < F - n) acc += ssf * dcoef(D, m) * (su[(size_t)(i - fa) * D.MR + D.MRrep + q] * ib);
     }
     for (int l = 0; l < NL; ++l) {
       const int a = scons[2 * l], c2 = scons[2 * l + 1];
@@ -694,7 +710,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       double un = 0.0;
       if (f < F - n) {
         double jv = 0.0;
-        for (int m = 0; m <= n; ++m) jv += ssf * D.c[m] * sv[(fl + m) * J3 + q];
+        for (int m = 0; m <= n; ++m) jv += ssf * dcoef(D, m) * sv[(fl + m) * J3 + q];
         un = (um[D.MRrep + q] * ib) * -alpha + jv;
       }
       Bf.u[mo + D.MRrep + q] = un;
@@ -772,8 +788,8 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jv_kernel(TrfDims D, TrfBufs 
       if (f < F - n) {
         double ja = 0.0, jc = 0.0;
         for (int m = 0; m <= n; ++m) {
-          ja += ssf * D.c[m] * sa[(fl + m) * J3 + q];
-          jc += ssf * D.c[m] * sc[(fl + m) * J3 + q];
+          ja += ssf * dcoef(D, m) * sa[(fl + m) * J3 + q];
+          jc += ssf * dcoef(D, m) * sc[(fl + m) * J3 + q];
         }
         saa += ja * ja;
         scc += jc * jc;
