@@ -24,6 +24,7 @@
 //     workgroup.  The host checks the per-animal done flags every few iterations;
 //   * the trust-region logic (2x2 subproblem, radius, termination) runs on the host from the partials.
 #include <algorithm>
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -40,6 +41,27 @@ constexpr int TRF_THREADS = 256;
 constexpr int TRF_FB = 4;  // frames per workgroup (at most; fewer when a block's rows would not fit in LDS)
 constexpr int TRF_MAXJ = 32, TRF_MAXL = 64, TRF_MAXN = 3;
 constexpr int TRF_NS = 24;  // lsmr state doubles per slot
+
+// -DTRF_PROFILE builds (tools only, never the shipped library): wall-clock time per phase of the two lsmr
+// kernels, block 0 of animal 0, summed over launches and printed at the end of optim_points_trf.
+#ifdef TRF_PROFILE
+__device__ unsigned long long g_trf_prof[2][8];
+#define TRF_PROF_BEGIN() \
+  unsigned long long prof_t[8]; \
+  prof_t[0] = wall_clock64()
+#define TRF_PROF(k) prof_t[k] = wall_clock64()
+#define TRF_PROF_END(kern, last)                                                       \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {                       \
+      for (int k = 1; k <= last; ++k) atomicAdd(&g_trf_prof[kern][k], prof_t[k] - prof_t[k - 1]); \
+      atomicAdd(&g_trf_prof[kern][0], 1ull);                                           \
+    }                                                                                   \
+  } while (0)
+#else
+#define TRF_PROF_BEGIN() (void)0
+#define TRF_PROF(k) (void)0
+#define TRF_PROF_END(kern, last) (void)0
+#endif
 
 struct TrfDims {
   int B, C, F, J, NL, nS, fix, n, loss;
@@ -363,9 +385,11 @@ __device__ __forceinline__ void length_sums(const TrfDims& D, const double* __re
 // in-place u *= 1 / beta) and the block's Jacobian rows.
 template <int MODE>
 __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs Bf, int par) {
+  TRF_PROF_BEGIN();
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   if (!Bf.act[b]) return;
   if (MODE > 0 && Bf.done[b]) return;
+  TRF_PROF(1);
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
   const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
   __shared__ double red[12];
@@ -399,6 +423,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
     if (blk == 0 && t < NL && !D.fix) vnL = Bf.vn[nb + D.NX + t];
   }
   if (blk == 0 && !D.fix) length_sums(D, (MODE == 2 ? Bf.Lpart : Bf.fL) + (size_t)b * NB * NL, spart, sLs);
+  TRF_PROF(2);
   // 2. the norm
   double beta = 1.0;
   if (MODE == 1) beta = normb;
@@ -410,6 +435,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
     __syncthreads();
   }
   const double ib = 1.0 / beta;
+  TRF_PROF(3);
   // 3. arithmetic
   double vsq = 0.0, vmax = 0.0;
   const int ntask = nf * J3;
@@ -448,6 +474,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
     }
     (MODE == 0 ? Bf.g : Bf.vraw)[o] = v;
   }
+  TRF_PROF(4);
   vsq = block_sum_all(vsq, red);
   if (MODE == 0) vmax = block_max_all(vmax, red);
   if (t == 0) {
@@ -455,6 +482,8 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
     vp[0] = vsq;
     vp[1] = vmax;
   }
+  TRF_PROF(5);
+  if (MODE == 2) TRF_PROF_END(1, 5);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -550,8 +579,10 @@ __device__ __forceinline__ int lsmr_istop(const TrfDims& D, const double* S, dou
 
 template <bool FIRST>
 __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBufs Bf, int par) {
+  TRF_PROF_BEGIN();
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
   if (!Bf.act[b] || Bf.done[b]) return;
+  TRF_PROF(1);
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
   const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
   const int pp = par ^ 1;
@@ -612,8 +643,10 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       xL = Bf.xl[oL];
     }
   }
+  TRF_PROF(2);
   // 2. the norms (one combined reduction; also the barrier after the staging stores), the test, the recurrences
   block_sum3_all(pa, pb, px, red);
+  TRF_PROF(3);
   const double alpha = sqrt(pa);
   const double beta = FIRST ? normb : sqrt(pb);
   if (t == 0) {
@@ -660,6 +693,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
     }
     return;
   }
+  TRF_PROF(4);
   const double chb = scoef[0], cx = scoef[1], ch = scoef[2];
   const double ia = 1.0 / alpha;
   // 3a. n space: v_{k-1} = v_raw / alpha (scipy's in-place v *= 1 / alpha); hbar, x, h (lsmr.py:396-403)
@@ -729,6 +763,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       sLu[fl][l] = lj[3] * un;
     }
   }
+  TRF_PROF(5);
   block_sum3_all(usq, xsq, pa, red);
   if (t == 0) {
     Bf.upart[((size_t)par * D.B + b) * NB + blk] = usq;
@@ -739,6 +774,8 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
     for (int fl = 0; fl < nf; ++fl) s2 += sLu[fl][t];
     Bf.Lpart[((size_t)b * NB + blk) * NL + t] = s2;
   }
+  TRF_PROF(6);
+  if (!FIRST) TRF_PROF_END(0, 6);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1417,6 +1454,18 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
         if (act[b]) xnorm[b] = std::sqrt(sum_field(part, 4, 0, b));
     }
   }
+#ifdef TRF_PROFILE
+  {
+    unsigned long long h[2][8];
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_trf_prof), sizeof(h));
+    for (int kk = 0; kk < 2; ++kk) {
+      const double nn = h[kk][0] ? (double)h[kk][0] : 1.0;
+      fprintf(stderr, "trf_prof %s launches %llu us/launch:", kk ? "jt2" : "lsmr1", h[kk][0]);
+      for (int k = 1; k < 8; ++k) fprintf(stderr, " %.2f", h[kk][k] / nn / 100.0);  // wall clock: 100 MHz
+      fprintf(stderr, "\n");
+    }
+  }
+#endif
   for (int b = 0; b < B; ++b) {
     stats[8 * b + 1] = cost[b];
     stats[8 * b + 2] = (double)(njev[b] - 1);

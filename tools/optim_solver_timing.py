@@ -50,9 +50,12 @@ def main():
     ap.add_argument("--solvers", default="trf,lm")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--cases", default="config4,s7f24,s8f24,s9f24")
+    ap.add_argument("--lib", default="", help="another build of libmq_hip.so (e.g. the -DTRF_PROFILE one in lib_prof/)")
     a = ap.parse_args()
     import torch
     from mqhip import _lib
+    if a.lib:
+        _lib.load(os.path.join(ROOT, a.lib))
     from mqhip.optim import optim_points_batch
     if a.chunk:
         _lib.check(_lib.Context.get(0).lib.mq_set_tuning(22, a.chunk), "chunk")
