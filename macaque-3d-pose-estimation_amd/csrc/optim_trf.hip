@@ -45,9 +45,9 @@ constexpr int TRF_NS = 24;  // lsmr state doubles per slot
 // -DTRF_PROFILE builds (tools only, never the shipped library): wall-clock time per phase of the two lsmr
 // kernels, block 0 of animal 0, summed over launches and printed at the end of optim_points_trf.
 #ifdef TRF_PROFILE
-__device__ unsigned long long g_trf_prof[2][8];
+__device__ unsigned long long g_trf_prof[2][12];
 #define TRF_PROF_BEGIN() \
-  unsigned long long prof_t[8]; \
+  unsigned long long prof_t[12]; \
   prof_t[0] = wall_clock64()
 #define TRF_PROF(k) prof_t[k] = wall_clock64()
 #define TRF_PROF_END(kern, last)                                                       \
@@ -75,6 +75,7 @@ struct TrfBufs {
   const double* cams;
   const double* p2d;
   const int* cons;
+  const int* jadj;  // per joint the constraints touching it, ascending l: [J + 1] offsets, then codes 2 l + (second end)
   const double* ssf;
   const int* act;  // [B] the animal takes part in this launch
   int* done;       // [B] lsmr finished
@@ -187,6 +188,80 @@ __device__ __forceinline__ void stage8(double* __restrict__ dst, const double* _
   }
 }
 
+// Several copies at once, in two halves: load() issues the first U8 * TRF_THREADS doubles of s8 (8-B loads) and
+// U* * TRF_THREADS 16-B vectors of a, b, c into registers; store() writes them to LDS, then copies whatever is
+// left of a larger array (more joints or cameras than the sizes chosen) in further rounds.  Everything a
+// kernel loads goes between the two halves, so the launch waits on one memory round trip (a load whose value
+// is stored or summed right away costs a round trip of its own: the wait sits before the use).  U = 0 leaves a
+// segment to the further rounds alone.
+struct StageSeg {
+  double* dst;
+  const double* src;
+  int n;
+};
+template <int U8, int UA, int UB, int UC>
+struct Stager {
+  StageSeg s8, a, b, c;
+  double r8[U8 > 0 ? U8 : 1];
+  trf_d2 ra[UA > 0 ? UA : 1], rb[UB > 0 ? UB : 1], rc[UC > 0 ? UC : 1];
+  __device__ __forceinline__ void load() {
+    const int t = threadIdx.x;
+    const int na = a.n >> 1, nb = b.n >> 1, nc = c.n >> 1;
+    const trf_d2 *sa = reinterpret_cast<const trf_d2*>(a.src), *sb = reinterpret_cast<const trf_d2*>(b.src),
+                 *sc = reinterpret_cast<const trf_d2*>(c.src);
+#pragma unroll
+    for (int u = 0; u < U8; ++u) {  // (an out-of-range lane re-reads element 0: no conditional loads)
+      const int i = u * TRF_THREADS + t;
+      r8[u] = s8.src[i < s8.n ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < UA; ++u) {
+      const int i = u * TRF_THREADS + t;
+      ra[u] = sa[i < na ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int i = u * TRF_THREADS + t;
+      rb[u] = sb[i < nb ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+      const int i = u * TRF_THREADS + t;
+      rc[u] = sc[i < nc ? i : 0];
+    }
+  }
+  __device__ __forceinline__ void store() {
+    const int t = threadIdx.x;
+    const int na = a.n >> 1, nb = b.n >> 1, nc = c.n >> 1;
+#pragma unroll
+    for (int u = 0; u < U8; ++u) {
+      const int i = u * TRF_THREADS + t;
+      if (i < s8.n) s8.dst[i] = r8[u];
+    }
+#pragma unroll
+    for (int u = 0; u < UA; ++u) {
+      const int i = u * TRF_THREADS + t;
+      if (i < na) reinterpret_cast<trf_d2*>(a.dst)[i] = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int i = u * TRF_THREADS + t;
+      if (i < nb) reinterpret_cast<trf_d2*>(b.dst)[i] = rb[u];
+    }
+#pragma unroll
+    for (int u = 0; u < UC; ++u) {
+      const int i = u * TRF_THREADS + t;
+      if (i < nc) reinterpret_cast<trf_d2*>(c.dst)[i] = rc[u];
+    }
+    constexpr int D8 = U8 * TRF_THREADS, DA = 2 * UA * TRF_THREADS, DB = 2 * UB * TRF_THREADS,
+                  DC = 2 * UC * TRF_THREADS;
+    if (s8.n > D8) stage8(s8.dst + D8, s8.src + D8, s8.n - D8);
+    if (a.n > DA) stage16(a.dst + DA, a.src + DA, a.n - DA);
+    if (b.n > DB) stage16(b.dst + DB, b.src + DB, b.n - DB);
+    if (c.n > DC) stage16(c.dst + DC, c.src + DC, c.n - DC);
+  }
+};
+
 // np.diff coefficient m of the kernel arguments by constant indices (a runtime index into the by-value
 // TrfDims made the compiler copy it to scratch: a memory round trip per use)
 __device__ __forceinline__ double dcoef(const TrfDims& D, int m) {
@@ -196,8 +271,10 @@ __device__ __forceinline__ double dcoef(const TrfDims& D, int m) {
 // lsmr state slot
 enum {
   S_ALPHABAR, S_RHO, S_RHOBAR, S_CBAR, S_SBAR, S_ZETABAR, S_ZETA, S_BETADD, S_BETAD, S_RHODOLD, S_TAUTILDEOLD,
-  S_THETATILDE, S_D, S_NORMA2, S_MAXRBAR, S_MINRBAR, S_ITN, S_NORMR, S_NORMAR, S_NORMA, S_CONDA
+  S_THETATILDE, S_D, S_NORMA2, S_MAXRBAR, S_MINRBAR, S_ITN, S_NORMR, S_NORMAR, S_NORMA, S_CONDA,
+  S_CHAT, S_SHAT, S_ALPHAHAT  // sym_ortho(alphabar, damp) of the next iteration (depends on neither norm)
 };
+static_assert(S_ALPHAHAT < TRF_NS, "lsmr state slot");
 
 // ---------------------------------------------------------------------------------------------------------
 // Residuals (and, mode 1, the Jacobian) at x for the block's frames.  fout: m vector [B][F][MR]:
@@ -342,30 +419,32 @@ __device__ __forceinline__ void block_sum3_all(double& a, double& b, double& c, 
   __syncthreads();
 }
 
-// the block's Jacobian rows (reprojection: J C 6 doubles per frame) into LDS
-__device__ __forceinline__ void stage_jrep(const TrfDims& D, const TrfBufs& Bf, int b, int f0, int nf, double* sj) {
-  const int per = D.J * D.C * 6;
-  stage16(sj, Bf.Jrep + ((size_t)b * D.F + f0) * per, nf * per);
-}
-
 // Length variables of block 0: sum over the NB blocks of the per-block partials lp[bb * NL + l], fixed order
-// (G threads per length, blocks bb = g, g + G, ...; then the G group sums in order).  out[l] in LDS.
-__device__ __forceinline__ void length_sums(const TrfDims& D, const double* __restrict__ lp, double* part /*[256]*/,
-                                            double* out) {
+// (G threads per length, blocks bb = g, g + G, ...; then the G group sums in order).  The first LEN_U partials
+// of a thread are loaded early (length_preload, issued with the kernel's other loads); length_sums adds them,
+// then any further ones, and leaves out[l] in LDS.
+constexpr int LEN_U = 16;
+__device__ __forceinline__ void length_preload(const TrfDims& D, const double* __restrict__ lp, double* v) {
+  const int NL = D.NL, NB = D.NB, t = threadIdx.x;
+  const int G = NL > 0 ? TRF_THREADS / NL : 1;
+  const int l = NL > 0 ? t % NL : 0, g = NL > 0 ? t / NL : 0;
+#pragma unroll
+  for (int u = 0; u < LEN_U; ++u) {
+    const int bb = g + u * G;
+    v[u] = lp[(size_t)(bb < NB ? bb : 0) * NL + l];
+  }
+}
+__device__ __forceinline__ void length_sums(const TrfDims& D, const double* __restrict__ lp, const double* v,
+                                            double* part /*[256]*/, double* out) {
   const int NL = D.NL, NB = D.NB, t = threadIdx.x;
   const int G = NL > 0 ? TRF_THREADS / NL : 1;
   double s = 0.0;
   if (t < G * NL) {
     const int l = t % NL, g = t / NL;
-    double v[4];
-    int bb = g;
-    for (; bb + 3 * G < NB; bb += 4 * G) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = lp[(size_t)(bb + u * G) * NL + l];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) s += v[u];
-    }
-    for (; bb < NB; bb += G) s += lp[(size_t)bb * NL + l];
+    for (int u = 0; u < LEN_U; ++u)
+      if (g + u * G < NB) s += v[u];
+    for (int bb = g + LEN_U * G; bb < NB; bb += G) s += lp[(size_t)bb * NL + l];
   }
   part[t] = s;
   __syncthreads();
@@ -382,7 +461,7 @@ __device__ __forceinline__ void length_sums(const TrfDims& D, const double* __re
 //   MODE 1: lsmr's start, v = J^T (f / normb)
 //   MODE 2: lsmr phase 2 of iteration k: v_k = J^T (u_k / beta_k) - beta_k v_{k-1}  (par = k & 1)
 // Dynamic LDS: the m rows of frames [f0 - n, f0 + nf) (raw; scaled by 1 / beta where they are used, as scipy's
-// in-place u *= 1 / beta) and the block's Jacobian rows.
+// in-place u *= 1 / beta), the block's Jacobian rows and the per-camera products of 3a.
 template <int MODE>
 __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs Bf, int par) {
   TRF_PROF_BEGIN();
@@ -393,28 +472,21 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
   const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
   __shared__ double red[12];
-  __shared__ double slen[TRF_FB][TRF_MAXL][3];
-  __shared__ int scons[2 * TRF_MAXL];
+  __shared__ __attribute__((aligned(16))) double slj[TRF_FB * TRF_MAXL * 4];
+  __shared__ int sadj[TRF_MAXJ + 1 + 2 * TRF_MAXL];
   __shared__ double spart[TRF_THREADS];
   __shared__ double sLs[TRF_MAXL];
   extern __shared__ double lds_jt[];
   const int fa = max(0, f0 - n), nrow = (f0 + nf - fa) * D.MR;
   double* su = lds_jt;
   double* sj = lds_jt + (((size_t)(D.FB + D.n) * D.MR + 1) & ~(size_t)1);
+  double* sprod = sj + (size_t)D.FB * J * C * 6;
   const double* uin = MODE == 2 ? Bf.u : Bf.fres;
-  // 1. loads independent of beta
+  // 1. loads independent of beta, all issued before the first wait
   const double ssf = Bf.ssf[b], normb = Bf.lctl[4 * b + 1];
+  const double* up = Bf.upart + ((size_t)par * D.B + b) * NB;
   double pu = 0.0;
-  if (MODE == 2)
-    for (int i = t; i < NB; i += TRF_THREADS) pu += Bf.upart[((size_t)par * D.B + b) * NB + i];
-  const double* ub = uin + ((size_t)b * F + fa) * D.MR;
-  stage16(su, ub, nrow);
-  stage_jrep(D, Bf, b, f0, nf, sj);
-  for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
-  for (int i = t; i < nf * NL * 3; i += TRF_THREADS) {
-    const int fl = i / (NL * 3), rem = i - fl * NL * 3, l = rem / 3, kk = rem - 3 * l;
-    slen[fl][l][kk] = Bf.lenJ[(((size_t)b * F + f0 + fl) * NL + l) * 4 + kk];
-  }
+  if (MODE == 2 && t < NB) pu = up[t];
   const size_t nb = (size_t)b * D.NV;
   double vn0 = 0.0, vn1 = 0.0, vnL = 0.0;  // the thread's (at most two) parameters and block 0's length variable
   if (MODE == 2) {
@@ -422,7 +494,25 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
     if (t + TRF_THREADS < nf * J3) vn1 = Bf.vn[nb + (size_t)f0 * J3 + t + TRF_THREADS];
     if (blk == 0 && t < NL && !D.fix) vnL = Bf.vn[nb + D.NX + t];
   }
-  if (blk == 0 && !D.fix) length_sums(D, (MODE == 2 ? Bf.Lpart : Bf.fL) + (size_t)b * NB * NL, spart, sLs);
+  const bool lens = blk == 0 && !D.fix && NL > 0;
+  const double* lp = (MODE == 2 ? Bf.Lpart : Bf.fL) + (size_t)b * NB * NL;
+  double lv[LEN_U];
+  if (lens) length_preload(D, lp, lv);
+  const int nadj = J + 1 + 2 * NL;
+  const int adj = Bf.jadj[t < nadj ? t : 0];
+  // the m rows (FB + n frames of MR: up to 2560 doubles in the first round, 7 x 354 for 17 joints, 8 cameras,
+  // 31 constraints), the Jacobian rows (3584: 4 frames x 17 joints x 8 cameras x 6) and the length rows (512:
+  // 4 frames x 32 constraints x 4)
+  Stager<0, 5, 7, 1> st{StageSeg{nullptr, nullptr, 0}, StageSeg{su, uin + ((size_t)b * F + fa) * D.MR, nrow},
+                        StageSeg{sj, Bf.Jrep + ((size_t)b * F + f0) * J * C * 6, nf * J * C * 6},
+                        StageSeg{slj, Bf.lenJ + ((size_t)b * F + f0) * NL * 4, nf * NL * 4}};
+  st.load();
+  // then the stores (and the rare second rounds)
+  if (t < nadj) sadj[t] = adj;
+  st.store();
+  if (MODE == 2)
+    for (int i = t + TRF_THREADS; i < NB; i += TRF_THREADS) pu += up[i];
+  if (lens) length_sums(D, lp, lv, spart, sLs);
   TRF_PROF(2);
   // 2. the norm
   double beta = 1.0;
@@ -436,26 +526,48 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
   }
   const double ib = 1.0 / beta;
   TRF_PROF(3);
-  // 3. arithmetic
+  // 3a. the reprojection products, one thread per (frame, joint, camera) row pair: lanes read consecutive rows
+  // (a thread per parameter summing over the cameras read rows 96 dwords apart, all in two LDS banks); the
+  // three products per row pair go to sprod[fl][c][3 j + k]
+  {
+    const int JC = J * C, NT = nf * JC;
+    const float iC = 1.0f / (float)C;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {  // (NT <= 3 TRF_THREADS for 4 frames x 17 joints x 8 cameras; more loop)
+      for (int i = k * TRF_THREADS + t; i < NT; i += 3 * TRF_THREADS) {
+        const int fl = (i >= JC) + (i >= 2 * JC) + (i >= 3 * JC), jc = i - fl * JC;
+        const int j = (int)(((float)jc + 0.5f) * iC), c = jc - j * C;
+        const trf_d2* jr2 = reinterpret_cast<const trf_d2*>(sj + (size_t)i * 6);
+        const trf_d2 ju = *reinterpret_cast<const trf_d2*>(su + (size_t)(f0 + fl - fa) * D.MR + 2 * jc);
+        const trf_d2 a0 = jr2[0], a1 = jr2[1], a2 = jr2[2];  // (d/dX, d/dY, d/dZ of u; then of v)
+        const double u0 = ju.x * ib, u1 = ju.y * ib;
+        double* pr = sprod + ((size_t)fl * C + c) * J3 + 3 * j;
+        pr[0] = a0.x * u0 + a1.y * u1;
+        pr[1] = a0.y * u0 + a2.x * u1;
+        pr[2] = a1.x * u0 + a2.y * u1;
+      }
+    }
+  }
+  __syncthreads();
+  // 3b. one thread per parameter: the camera products in camera order, the smoothness and length terms
   double vsq = 0.0, vmax = 0.0;
   const int ntask = nf * J3;
   for (int task = t, it = 0; task < ntask; task += TRF_THREADS, ++it) {
     const int fl = task / J3, q = task - fl * J3, j = q / 3, kk = q - 3 * j, f = f0 + fl;
     const double* uf = su + (size_t)(f - fa) * D.MR;
-    const double* jr = sj + ((size_t)fl * J + j) * C * 6;
     double acc = 0.0;
-    for (int c = 0; c < C; ++c) {
-      acc += jr[6 * c + kk] * (uf[2 * (j * C + c)] * ib);
-      acc += jr[6 * c + 3 + kk] * (uf[2 * (j * C + c) + 1] * ib);
-    }
+    const double* pr = sprod + (size_t)fl * C * J3 + q;
+#pragma unroll 4
+    for (int c = 0; c < C; ++c) acc += pr[(size_t)c * J3];
     for (int m = 0; m <= n; ++m) {  // smoothness rows i = f - m hold frame f with coefficient c[m]
       const int i = f - m;
       if (i >= 0 && i < F - n) acc += ssf * dcoef(D, m) * (su[(size_t)(i - fa) * D.MR + D.MRrep + q] * ib);
     }
-    for (int l = 0; l < NL; ++l) {
-      const int a = scons[2 * l], c2 = scons[2 * l + 1];
-      if (a == j) acc += slen[fl][l][kk] * (uf[D.MRrep + J3 + l] * ib);
-      else if (c2 == j) acc -= slen[fl][l][kk] * (uf[D.MRrep + J3 + l] * ib);
+    for (int e = sadj[j], ee = sadj[j + 1]; e < ee; ++e) {  // the constraints touching joint j, ascending l
+      const int code = sadj[J + 1 + e], l = code >> 1;
+      const double term = slj[(fl * NL + l) * 4 + kk] * (uf[D.MRrep + J3 + l] * ib);
+      if (code & 1) acc -= term;
+      else acc += term;
     }
     const size_t o = nb + (size_t)f * J3 + q;
     const double v = MODE == 2 ? (it == 0 ? vn0 : vn1) * -beta + acc : acc;
@@ -494,13 +606,15 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
 // alpha_{k-1} u_{k-1} for the block's rows.
 __device__ __forceinline__ void lsmr_recurrence(double* S, double alpha, double beta, double damp, double& chb,
                                                 double& cx, double& ch) {
-  double chat, shat, alphahat;
-  sym_ortho(S[S_ALPHABAR], damp, chat, shat, alphahat);
+  // (lsmr.py:305's rotation of alphabar and damp was computed with the previous iteration's recurrences, off
+  // the chain that waits on this iteration's norms)
+  const double chat = S[S_CHAT], shat = S[S_SHAT], alphahat = S[S_ALPHAHAT];
   const double rhoold = S[S_RHO];
   double c, s, rho;
   sym_ortho(alphahat, beta, c, s, rho);
   const double thetanew = s * alpha;
   S[S_ALPHABAR] = c * alpha;
+  sym_ortho(S[S_ALPHABAR], damp, S[S_CHAT], S[S_SHAT], S[S_ALPHAHAT]);
   const double rhobarold = S[S_RHOBAR];
   const double zetaold = S[S_ZETA];
   const double thetabar = S[S_SBAR] * rho;
@@ -590,7 +704,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
   __shared__ double sv[(TRF_FB + TRF_MAXN) * TRF_MAXJ * 3];
   __shared__ double sL[TRF_MAXL];
   __shared__ double sLu[TRF_FB][TRF_MAXL];
-  __shared__ double slj[TRF_FB][TRF_MAXL][4];
+  __shared__ __attribute__((aligned(16))) double slj[TRF_FB * TRF_MAXL * 4];
   __shared__ int scons[2 * TRF_MAXL];
   __shared__ double sS[TRF_NS];
   __shared__ double scoef[4];
@@ -599,29 +713,21 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
   double* sm = lds_l1;                                                   // the block's m rows (u_{k-1}, raw)
   double* sj = lds_l1 + (((size_t)D.FB * D.MR + 1) & ~(size_t)1);       // its Jacobian rows
   const size_t nb = (size_t)b * D.NV;
-  // 1. loads independent of the norms
+  // 1. loads independent of the norms, all issued before the first wait
   const double damp = Bf.lctl[4 * b], normb = Bf.lctl[4 * b + 1], maxiter = Bf.lctl[4 * b + 2], ssf = Bf.ssf[b];
+  const double* vp = Bf.vpart + ((size_t)pp * D.B + b) * NB * 2;
+  const double* upp = Bf.upart + ((size_t)pp * D.B + b) * NB;
+  const double* xp = Bf.xpart + ((size_t)pp * D.B + b) * NB;
   double pa = 0.0, pb = 0.0, px = 0.0;
-  for (int i = t; i < NB; i += TRF_THREADS) {
-    pa += Bf.vpart[(((size_t)pp * D.B + b) * NB + i) * 2];
+  if (t < NB) {
+    pa = vp[2 * t];
     if (!FIRST) {
-      pb += Bf.upart[((size_t)pp * D.B + b) * NB + i];
-      px += Bf.xpart[((size_t)pp * D.B + b) * NB + i];
+      pb = upp[t];
+      px = xp[t];
     }
   }
-  if (!FIRST && t < TRF_NS) sS[t] = Bf.st[((size_t)pp * D.B + b) * TRF_NS + t];
+  const double stv = (!FIRST && t < TRF_NS) ? Bf.st[((size_t)pp * D.B + b) * TRF_NS + t] : 0.0;
   const int nfx = min(nf + n, F - f0);
-  stage8(sv, Bf.vraw + nb + (size_t)f0 * J3, nfx * J3);
-  if (t < NL) sL[t] = D.fix ? 0.0 : Bf.vraw[nb + D.NX + t];
-  const double* uin = FIRST ? Bf.fres : Bf.u;
-  const double* ub = uin + ((size_t)b * F + f0) * D.MR;
-  stage16(sm, ub, nf * D.MR);
-  stage_jrep(D, Bf, b, f0, nf, sj);
-  for (int i = t; i < 2 * NL; i += TRF_THREADS) scons[i] = Bf.cons[i];
-  for (int i = t; i < nf * NL * 4; i += TRF_THREADS) {
-    const int fl = i / (NL * 4), rem = i - fl * NL * 4;
-    slj[fl][rem >> 2][rem & 3] = Bf.lenJ[((size_t)b * F + f0 + fl) * NL * 4 + rem];
-  }
   // the thread's n-space entries: (at most two) parameters and block 0's length variable
   double h0 = 0.0, h1 = 0.0, hL = 0.0, hb0 = 0.0, hb1 = 0.0, hbL = 0.0, x0 = 0.0, x1 = 0.0, xL = 0.0;
   const size_t o0 = nb + (size_t)f0 * J3 + t, o1 = o0 + TRF_THREADS, oL = nb + D.NX + t;
@@ -643,20 +749,55 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       xL = Bf.xl[oL];
     }
   }
+  const double lv = (t < NL && !D.fix) ? Bf.vraw[nb + D.NX + t] : 0.0;
+  const int cv = Bf.cons[t < 2 * NL ? t : 0];
+  const double* uin = FIRST ? Bf.fres : Bf.u;
+  // v_raw of frames [f0, f0 + nf + n) (up to 512 doubles: 7 frames x 17 joints x 3), the m rows (up to 1536:
+  // 4 frames x 384), the Jacobian rows (3584) and the length rows (512)
+  Stager<2, 3, 7, 1> st{StageSeg{sv, Bf.vraw + nb + (size_t)f0 * J3, nfx * J3},
+                        StageSeg{sm, uin + ((size_t)b * F + f0) * D.MR, nf * D.MR},
+                        StageSeg{sj, Bf.Jrep + ((size_t)b * F + f0) * J * C * 6, nf * J * C * 6},
+                        StageSeg{slj, Bf.lenJ + ((size_t)b * F + f0) * NL * 4, nf * NL * 4}};
+  st.load();
+  // then the stores (and the rare second rounds)
+  if (!FIRST && t < TRF_NS) sS[t] = stv;
+  if (t < NL) sL[t] = lv;
+  if (t < 2 * NL) scons[t] = cv;
+  st.store();
+  for (int i = t + TRF_THREADS; i < NB; i += TRF_THREADS) {
+    pa += vp[2 * i];
+    if (!FIRST) {
+      pb += upp[i];
+      px += xp[i];
+    }
+  }
   TRF_PROF(2);
-  // 2. the norms (one combined reduction; also the barrier after the staging stores), the test, the recurrences
+  // 2. the norms (one combined reduction; also the barrier after the staging stores)
   block_sum3_all(pa, pb, px, red);
   TRF_PROF(3);
   const double alpha = sqrt(pa);
   const double beta = FIRST ? normb : sqrt(pb);
-  if (t == 0) {
-    double* S = sS;
+  const double ia = 1.0 / alpha;
+  // v_{k-1} = v_raw / alpha (scipy's in-place v *= 1 / alpha)
+  for (int i = t; i < nfx * J3; i += TRF_THREADS) sv[i] = sv[i] * ia;
+  if (t < NL) sL[t] = sL[t] * ia;
+  __syncthreads();
+  // 3. lane 0 of the last wave: the stop test and the recurrences (a serial chain of divisions and square
+  // roots, in registers); meanwhile the other waves compute the m-space rows, which need only alpha and beta:
+  // u_k = (u_{k-1} / beta) * -alpha + J v_{k-1}   (lsmr.py:284-286).  (If the test stops the run, the rows
+  // written here are never read: every later lsmr launch returns on the done flag.)
+  constexpr int RT = TRF_THREADS - 64;  // the recurrence thread; m-space workers t < MW
+  const int MW = FIRST ? TRF_THREADS : RT;
+  if (t == RT) {
+    double S[TRF_NS];
+#pragma unroll
+    for (int i = 0; i < TRF_NS; ++i) S[i] = FIRST ? 0.0 : sS[i];
     double chb = 0.0, cx = 0.0, ch = 0.0;
     int istop = 0;
     if (FIRST) {
-      for (int i = 0; i < TRF_NS; ++i) S[i] = 0.0;
       S[S_ZETABAR] = alpha * beta;
       S[S_ALPHABAR] = alpha;
+      sym_ortho(alpha, damp, S[S_CHAT], S[S_SHAT], S[S_ALPHAHAT]);
       S[S_RHO] = 1;
       S[S_RHOBAR] = 1;
       S[S_CBAR] = 1;
@@ -668,8 +809,12 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       S[S_ITN] = 0;
       if (!(alpha * beta != 0)) istop = 8;  // normar == 0 (or normb == 0): x = 0 (lsmr.py:247-256)
     } else {
-      if (S[S_ITN] >= 1) istop = lsmr_istop(D, S, sqrt(px), normb, maxiter);
-      if (!istop) lsmr_recurrence(S, alpha, beta, damp, chb, cx, ch);
+      // the test and the recurrences side by side (independent chains; the recurrence's results are dropped
+      // when the test stops the run)
+      const double itn0 = S[S_ITN];
+      if (itn0 >= 1) istop = lsmr_istop(D, S, sqrt(px), normb, maxiter);
+      lsmr_recurrence(S, alpha, beta, damp, chb, cx, ch);
+      if (istop) S[S_ITN] = itn0;
     }
     if (istop && blk == 0) {
       Bf.done[b] = istop;
@@ -681,10 +826,90 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
     scoef[2] = ch;
     if (blk == 0 && !istop) {
       double* So = Bf.st + ((size_t)par * D.B + b) * TRF_NS;
+#pragma unroll
       for (int i = 0; i < TRF_NS; ++i) So[i] = S[i];
     }
+#ifdef TRF_PROFILE
+    if (!FIRST && blk == 0 && b == 0) atomicAdd(&g_trf_prof[1][8], wall_clock64() - prof_t[3]);  // the recurrence
+#endif
   }
+  const double ib = 1.0 / beta;
+  const int nrep = J * C;
+  double usq = 0.0;
+  if (t < MW) {
+    // reprojection rows, up to three row pairs per thread with their LDS reads issued together (frame and joint
+    // from comparisons and a float reciprocal instead of integer divisions)
+    const int NR = nf * nrep;
+    const float iC = 1.0f / (float)C;
+    for (int base = t; base < NR; base += 3 * MW) {
+      trf_d2 a0[3], a1[3], a2[3], um[3];
+      double v0[3], v1[3], v2[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int i0 = base + k * MW, i = i0 < NR ? i0 : 0;
+        const int fl = (i >= nrep) + (i >= 2 * nrep) + (i >= 3 * nrep), r = i - fl * nrep;
+        const int j = (int)(((float)r + 0.5f) * iC);
+        const trf_d2* jr2 = reinterpret_cast<const trf_d2*>(sj + (size_t)i * 6);
+        a0[k] = jr2[0];
+        a1[k] = jr2[1];
+        a2[k] = jr2[2];
+        um[k] = *reinterpret_cast<const trf_d2*>(sm + (size_t)fl * D.MR + 2 * r);
+        const double* v = sv + fl * J3 + 3 * j;
+        v0[k] = v[0];
+        v1[k] = v[1];
+        v2[k] = v[2];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int i = base + k * MW;
+        if (i < NR) {
+          const int fl = (i >= nrep) + (i >= 2 * nrep) + (i >= 3 * nrep), r = i - fl * nrep;
+          const double ju = a0[k].x * v0[k] + a0[k].y * v1[k] + a1[k].x * v2[k];
+          const double jv = a1[k].y * v0[k] + a2[k].x * v1[k] + a2[k].y * v2[k];
+          const double un0 = (um[k].x * ib) * -alpha + ju, un1 = (um[k].y * ib) * -alpha + jv;
+          trf_d2 o;
+          o.x = un0;
+          o.y = un1;
+          *reinterpret_cast<trf_d2*>(Bf.u + ((size_t)b * F + f0 + fl) * D.MR + 2 * r) = o;
+          usq += un0 * un0;
+          usq += un1 * un1;
+        }
+      }
+    }
+    TRF_PROF(8);
+    // smoothness rows
+    const float iJ3 = 1.0f / (float)J3;
+    for (int i = t; i < nf * J3; i += MW) {
+      const int fl = (int)(((float)i + 0.5f) * iJ3), q = i - fl * J3, f = f0 + fl;
+      double un = 0.0;
+      if (f < F - n) {
+        double jv = 0.0;
+        for (int m = 0; m <= n; ++m) jv += ssf * dcoef(D, m) * sv[(fl + m) * J3 + q];
+        un = (sm[(size_t)fl * D.MR + D.MRrep + q] * ib) * -alpha + jv;
+      }
+      Bf.u[((size_t)b * F + f) * D.MR + D.MRrep + q] = un;
+      usq += un * un;
+    }
+    TRF_PROF(9);
+    // limb-length rows
+    const float iNL = NL > 0 ? 1.0f / (float)NL : 0.0f;
+    for (int i = t; i < nf * NL; i += MW) {
+      const int fl = (int)(((float)i + 0.5f) * iNL), l = i - fl * NL, f = f0 + fl;
+      const int a = scons[2 * l], c2 = scons[2 * l + 1];
+      const double* lj = slj + (fl * NL + l) * 4;
+      double jv = lj[0] * (sv[fl * J3 + 3 * a] - sv[fl * J3 + 3 * c2]) +
+                  lj[1] * (sv[fl * J3 + 3 * a + 1] - sv[fl * J3 + 3 * c2 + 1]) +
+                  lj[2] * (sv[fl * J3 + 3 * a + 2] - sv[fl * J3 + 3 * c2 + 2]);
+      if (!D.fix) jv += lj[3] * sL[l];
+      const double un = (sm[(size_t)fl * D.MR + D.MRrep + J3 + l] * ib) * -alpha + jv;
+      Bf.u[((size_t)b * F + f) * D.MR + D.MRrep + J3 + l] = un;
+      usq += un * un;
+      sLu[fl][l] = lj[3] * un;
+    }
+  }
+  TRF_PROF(4);
   __syncthreads();
+  TRF_PROF(5);
   if (sstop) {
     if (FIRST) {  // x = 0
       if (e0) Bf.xl[o0] = 0.0;
@@ -693,13 +918,8 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
     }
     return;
   }
-  TRF_PROF(4);
+  // 4. n space: hbar, x, h (lsmr.py:396-403)
   const double chb = scoef[0], cx = scoef[1], ch = scoef[2];
-  const double ia = 1.0 / alpha;
-  // 3a. n space: v_{k-1} = v_raw / alpha (scipy's in-place v *= 1 / alpha); hbar, x, h (lsmr.py:396-403)
-  for (int i = t; i < nfx * J3; i += TRF_THREADS) sv[i] = sv[i] * ia;
-  if (t < NL) sL[t] = sL[t] * ia;
-  __syncthreads();
   double xsq = 0.0;
   auto upd = [&](bool e, size_t o, double v, double h, double hb, double x) {
     if (!e) return;
@@ -720,50 +940,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
   upd(e0, o0, e0 ? sv[t] : 0.0, h0, hb0, x0);
   upd(e1, o1, e1 ? sv[t + TRF_THREADS] : 0.0, h1, hb1, x1);
   upd(eL, oL, eL ? sL[t] : 0.0, hL, hbL, xL);
-  // 3b. m space: u_k = (u_{k-1} / beta) * -alpha + J v   (lsmr.py:284-286)
-  const double ib = 1.0 / beta;
-  const int nrep = J * C, ntask = nrep + J3 + NL;
-  double usq = 0.0;
-  for (int task = t; task < nf * ntask; task += TRF_THREADS) {
-    const int fl = task / ntask, r = task - fl * ntask, f = f0 + fl;
-    const size_t mo = ((size_t)b * F + f) * D.MR;
-    const double* um = sm + (size_t)fl * D.MR;
-    if (r < nrep) {
-      const int j = r / C;
-      const double* jr = sj + ((size_t)fl * nrep + r) * 6;
-      const double* v = sv + fl * J3 + 3 * j;
-#pragma unroll
-      for (int comp = 0; comp < 2; ++comp) {
-        const double jv = jr[3 * comp] * v[0] + jr[3 * comp + 1] * v[1] + jr[3 * comp + 2] * v[2];
-        const double un = (um[2 * r + comp] * ib) * -alpha + jv;
-        Bf.u[mo + 2 * r + comp] = un;
-        usq += un * un;
-      }
-    } else if (r < nrep + J3) {
-      const int q = r - nrep;
-      double un = 0.0;
-      if (f < F - n) {
-        double jv = 0.0;
-        for (int m = 0; m <= n; ++m) jv += ssf * dcoef(D, m) * sv[(fl + m) * J3 + q];
-        un = (um[D.MRrep + q] * ib) * -alpha + jv;
-      }
-      Bf.u[mo + D.MRrep + q] = un;
-      usq += un * un;
-    } else {
-      const int l = r - nrep - J3;
-      const int a = scons[2 * l], c2 = scons[2 * l + 1];
-      const double* lj = slj[fl][l];
-      double jv = lj[0] * (sv[fl * J3 + 3 * a] - sv[fl * J3 + 3 * c2]) +
-                  lj[1] * (sv[fl * J3 + 3 * a + 1] - sv[fl * J3 + 3 * c2 + 1]) +
-                  lj[2] * (sv[fl * J3 + 3 * a + 2] - sv[fl * J3 + 3 * c2 + 2]);
-      if (!D.fix) jv += lj[3] * sL[l];
-      const double un = (um[D.MRrep + J3 + l] * ib) * -alpha + jv;
-      Bf.u[mo + D.MRrep + J3 + l] = un;
-      usq += un * un;
-      sLu[fl][l] = lj[3] * un;
-    }
-  }
-  TRF_PROF(5);
+  TRF_PROF(6);
   block_sum3_all(usq, xsq, pa, red);
   if (t == 0) {
     Bf.upart[((size_t)par * D.B + b) * NB + blk] = usq;
@@ -774,8 +951,15 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
     for (int fl = 0; fl < nf; ++fl) s2 += sLu[fl][t];
     Bf.Lpart[((size_t)b * NB + blk) * NL + t] = s2;
   }
-  TRF_PROF(6);
-  if (!FIRST) TRF_PROF_END(0, 6);
+  TRF_PROF(7);
+  if (!FIRST) TRF_PROF_END(0, 7);
+#ifdef TRF_PROFILE
+  if (!FIRST && t == 0 && blk == 0 && b == 0) {  // the m-space split: rows from phase 3's start
+    atomicAdd(&g_trf_prof[0][8], prof_t[8] - prof_t[3]);
+    atomicAdd(&g_trf_prof[0][9], prof_t[9] - prof_t[8]);
+    atomicAdd(&g_trf_prof[0][10], prof_t[4] - prof_t[9]);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -1044,7 +1228,7 @@ int g_optim_trf_chunk = 8;  // lsmr iterations launched (one captured graph) bet
 
 // dynamic LDS of the two per-iteration kernels for FB frames per block
 size_t trf_jt_lds(int FB, int n, int MR, int J, int C) {
-  return ((((size_t)(FB + n) * MR + 1) & ~(size_t)1) + (size_t)FB * J * C * 6) * sizeof(double);
+  return ((((size_t)(FB + n) * MR + 1) & ~(size_t)1) + (size_t)FB * J * C * 9) * sizeof(double);
 }
 size_t trf_l1_lds(int FB, int MR, int J, int C) {
   return ((((size_t)FB * MR + 1) & ~(size_t)1) + (size_t)FB * J * C * 6) * sizeof(double);
@@ -1069,6 +1253,7 @@ size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL) {
   n += (size_t)B * NB * (4 + NL + 2 + 4 + 2 + NL + 4 + 4);  // fpart fL upart vpart xpart Lpart npart jpart
   n += 2 * (size_t)B * TRF_NS + (size_t)B * 8;
   n += (size_t)NL + 2 + 2 * (size_t)B + 16;  // cons, act, done, ssf
+  n += ((size_t)J + 1 + 2 * (size_t)NL) / 2 + 1;  // jadj
   return n * sizeof(double) + 256;
 }
 
@@ -1146,12 +1331,14 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   Bf.lctl = take(4 * (size_t)B);
   Bf.coef = take(4 * (size_t)B);
   int* cons_d = reinterpret_cast<int*>(take(((size_t)NL * 2 + 1) / 2 + 1));
+  int* jadj_d = reinterpret_cast<int*>(take(((size_t)J + 1 + 2 * (size_t)NL) / 2 + 1));
   int* act_d = reinterpret_cast<int*>(take(((size_t)B + 1) / 2 + 1));
   int* done_d = reinterpret_cast<int*>(take(((size_t)B + 1) / 2 + 1));
   double* ssf_d = take(B);
   Bf.cams = cams;
   Bf.p2d = p2d;
   Bf.cons = cons_d;
+  Bf.jadj = jadj_d;
   Bf.ssf = ssf_d;
   Bf.act = act_d;
   Bf.done = done_d;
@@ -1162,6 +1349,18 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s) == hipSuccess;
   };
   if (NL && !H2D(cons_d, cons_host, sizeof(int) * 2 * NL)) return -3;
+  // J^T's constraint terms per joint (trf_jt_kernel): the constraints with the joint as their first end (+) or,
+  // failing that, their second end (-), in ascending order of l
+  std::vector<int> jadj(J + 1 + 2 * NL, 0);
+  for (int j = 0, e = 0; j < J; ++j) {
+    jadj[j] = e;
+    for (int l = 0; l < NL; ++l) {
+      if (cons_host[2 * l] == j) jadj[J + 1 + e++] = 2 * l;
+      else if (cons_host[2 * l + 1] == j) jadj[J + 1 + e++] = 2 * l + 1;
+    }
+    jadj[j + 1] = e;
+  }
+  if (!H2D(jadj_d, jadj.data(), sizeof(int) * jadj.size())) return -3;
   if (!H2D(ssf_d, ssf_host, sizeof(double) * B)) return -3;
   std::vector<int> act(B, 1), doneh(B, 1);
   if (!H2D(act_d, act.data(), sizeof(int) * B)) return -3;
@@ -1456,12 +1655,12 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   }
 #ifdef TRF_PROFILE
   {
-    unsigned long long h[2][8];
+    unsigned long long h[2][12];
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_trf_prof), sizeof(h));
     for (int kk = 0; kk < 2; ++kk) {
       const double nn = h[kk][0] ? (double)h[kk][0] : 1.0;
       fprintf(stderr, "trf_prof %s launches %llu us/launch:", kk ? "jt2" : "lsmr1", h[kk][0]);
-      for (int k = 1; k < 8; ++k) fprintf(stderr, " %.2f", h[kk][k] / nn / 100.0);  // wall clock: 100 MHz
+      for (int k = 1; k < 12; ++k) fprintf(stderr, " %.2f", h[kk][k] / nn / 100.0);  // wall clock: 100 MHz
       fprintf(stderr, "\n");
     }
   }
