@@ -87,7 +87,7 @@ const char* mq_last_error(void);
 #define MQ_TUNE_ATTN_KRING 24       /* 1 (default): 192-token attention with the inline-asm K-fragment ring; 0: the
                                        compiler-scheduled loop (bit-identical; the fallback for a toolchain change) */
 #define MQ_TUNE_OPTIM_TRF_CHUNK 22  /* lsmr iterations the trust-region solver launches between two reads of its done
-                                       flags (default 8, 1..64; same results) */
+                                       flags (default 16, 1..64; same results) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

@@ -81,14 +81,17 @@ struct TrfBufs {
   int* done;       // [B] lsmr finished
   double *fres, *ftr, *Jrep, *lenJ;
   double *g, *u, *vraw, *vn, *h, *hbar, *xl, *s1, *s2;
-  double* fpart;  // [B][NB][4]: sum r^2 at x, sum r^2 at the trial point, rows
+  double* fpart;  // [B][NB][4]: sum r^2 at x, sum r^2 at the trial point, rows (host-mapped)
   double* fL;     // [B][NB][NL]: sum over the block's frames of dL * r_len at x
   double* upart;  // [2][B][NB]
   double* vpart;  // [2][B][NB][2]: sum v^2, max |v|
   double* xpart;  // [2][B][NB]
   double* Lpart;  // [B][NB][NL]
-  double* npart;  // [B][NB][4]
-  double* jpart;  // [B][NB][4]
+  double* npart;  // [B][NB][TRF_NPF] (host-mapped)
+  double* jpart;  // [B][NB][4] (host-mapped)
+  double* gpart;  // [B][NB][2]: |g|^2, max |g| (host-mapped)
+  double* hitn;   // [B]: lsmr's final iteration count (host-mapped)
+  int* hdone;     // [B]: copy of done (host-mapped), polled by the host between chunks
   double* st;     // [2][B][TRF_NS]
   double* lctl;   // [B][4]: damp, normb, maxiter, final lsmr itn
   double* coef;   // [B][4]
@@ -457,7 +460,7 @@ __device__ __forceinline__ void length_sums(const TrfDims& D, const double* __re
 }
 
 // v = J^T (u / beta) - beta vn for the block's parameters (and block 0's length variables).
-//   MODE 0: g = J^T f (u = fres, beta = 1, no vn); partials (sum g^2, max |g|) in vpart slot 0
+//   MODE 0: g = J^T f (u = fres, beta = 1, no vn); partials (sum g^2, max |g|) in gpart
 //   MODE 1: lsmr's start, v = J^T (f / normb)
 //   MODE 2: lsmr phase 2 of iteration k: v_k = J^T (u_k / beta_k) - beta_k v_{k-1}  (par = k & 1)
 // Dynamic LDS: the m rows of frames [f0 - n, f0 + nf) (raw; scaled by 1 / beta where they are used, as scipy's
@@ -466,9 +469,6 @@ template <int MODE>
 __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs Bf, int par) {
   TRF_PROF_BEGIN();
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
-  if (!Bf.act[b]) return;
-  if (MODE > 0 && Bf.done[b]) return;
-  TRF_PROF(1);
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
   const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
   __shared__ double red[12];
@@ -507,6 +507,10 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
                         StageSeg{sj, Bf.Jrep + ((size_t)b * F + f0) * J * C * 6, nf * J * C * 6},
                         StageSeg{slj, Bf.lenJ + ((size_t)b * F + f0) * NL * 4, nf * NL * 4}};
   st.load();
+  // the animal's flags, read with the rest (a block of a finished animal has loaded for nothing; every address
+  // above is inside the workspace whatever the flags)
+  if (!Bf.act[b] || (MODE > 0 && Bf.done[b])) return;
+  TRF_PROF(1);
   // then the stores (and the rare second rounds)
   if (t < nadj) sadj[t] = adj;
   st.store();
@@ -590,7 +594,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
   vsq = block_sum_all(vsq, red);
   if (MODE == 0) vmax = block_max_all(vmax, red);
   if (t == 0) {
-    double* vp = Bf.vpart + (((size_t)par * D.B + b) * NB + blk) * 2;
+    double* vp = MODE == 0 ? Bf.gpart + ((size_t)b * NB + blk) * 2 : Bf.vpart + (((size_t)par * D.B + b) * NB + blk) * 2;
     vp[0] = vsq;
     vp[1] = vmax;
   }
@@ -695,8 +699,6 @@ template <bool FIRST>
 __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBufs Bf, int par) {
   TRF_PROF_BEGIN();
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
-  if (!Bf.act[b] || Bf.done[b]) return;
-  TRF_PROF(1);
   const int J = D.J, C = D.C, J3 = 3 * J, n = D.n, F = D.F, NL = D.NL, NB = D.NB;
   const int f0 = blk * D.FB, nf = min(D.FB, F - f0);
   const int pp = par ^ 1;
@@ -759,6 +761,9 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
                         StageSeg{sj, Bf.Jrep + ((size_t)b * F + f0) * J * C * 6, nf * J * C * 6},
                         StageSeg{slj, Bf.lenJ + ((size_t)b * F + f0) * NL * 4, nf * NL * 4}};
   st.load();
+  // the animal's flags, read with the rest (as in trf_jt_kernel)
+  if (!Bf.act[b] || Bf.done[b]) return;
+  TRF_PROF(1);
   // then the stores (and the rare second rounds)
   if (!FIRST && t < TRF_NS) sS[t] = stv;
   if (t < NL) sL[t] = lv;
@@ -777,11 +782,9 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
   TRF_PROF(3);
   const double alpha = sqrt(pa);
   const double beta = FIRST ? normb : sqrt(pb);
+  // v_{k-1} = v_raw / alpha: scipy's in-place v *= 1 / alpha, applied by every reader of sv / sL to the raw
+  // value it reads (the same product, so the same bits, with no pass over LDS and no barrier before the rows)
   const double ia = 1.0 / alpha;
-  // v_{k-1} = v_raw / alpha (scipy's in-place v *= 1 / alpha)
-  for (int i = t; i < nfx * J3; i += TRF_THREADS) sv[i] = sv[i] * ia;
-  if (t < NL) sL[t] = sL[t] * ia;
-  __syncthreads();
   // 3. lane 0 of the last wave: the stop test and the recurrences (a serial chain of divisions and square
   // roots, in registers); meanwhile the other waves compute the m-space rows, which need only alpha and beta:
   // u_k = (u_{k-1} / beta) * -alpha + J v_{k-1}   (lsmr.py:284-286).  (If the test stops the run, the rows
@@ -819,6 +822,8 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
     if (istop && blk == 0) {
       Bf.done[b] = istop;
       Bf.lctl[4 * b + 3] = S[S_ITN];
+      Bf.hitn[b] = S[S_ITN];
+      Bf.hdone[b] = istop;
     }
     sstop = istop;
     scoef[0] = chb;
@@ -855,9 +860,9 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
         a2[k] = jr2[2];
         um[k] = *reinterpret_cast<const trf_d2*>(sm + (size_t)fl * D.MR + 2 * r);
         const double* v = sv + fl * J3 + 3 * j;
-        v0[k] = v[0];
-        v1[k] = v[1];
-        v2[k] = v[2];
+        v0[k] = v[0] * ia;
+        v1[k] = v[1] * ia;
+        v2[k] = v[2] * ia;
       }
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
@@ -884,7 +889,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       double un = 0.0;
       if (f < F - n) {
         double jv = 0.0;
-        for (int m = 0; m <= n; ++m) jv += ssf * dcoef(D, m) * sv[(fl + m) * J3 + q];
+        for (int m = 0; m <= n; ++m) jv += ssf * dcoef(D, m) * (sv[(fl + m) * J3 + q] * ia);
         un = (sm[(size_t)fl * D.MR + D.MRrep + q] * ib) * -alpha + jv;
       }
       Bf.u[((size_t)b * F + f) * D.MR + D.MRrep + q] = un;
@@ -897,10 +902,11 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       const int fl = (int)(((float)i + 0.5f) * iNL), l = i - fl * NL, f = f0 + fl;
       const int a = scons[2 * l], c2 = scons[2 * l + 1];
       const double* lj = slj + (fl * NL + l) * 4;
-      double jv = lj[0] * (sv[fl * J3 + 3 * a] - sv[fl * J3 + 3 * c2]) +
-                  lj[1] * (sv[fl * J3 + 3 * a + 1] - sv[fl * J3 + 3 * c2 + 1]) +
-                  lj[2] * (sv[fl * J3 + 3 * a + 2] - sv[fl * J3 + 3 * c2 + 2]);
-      if (!D.fix) jv += lj[3] * sL[l];
+      const double* va = sv + fl * J3 + 3 * a;
+      const double* vc = sv + fl * J3 + 3 * c2;
+      double jv = lj[0] * (va[0] * ia - vc[0] * ia) + lj[1] * (va[1] * ia - vc[1] * ia) +
+                  lj[2] * (va[2] * ia - vc[2] * ia);
+      if (!D.fix) jv += lj[3] * (sL[l] * ia);
       const double un = (sm[(size_t)fl * D.MR + D.MRrep + J3 + l] * ib) * -alpha + jv;
       Bf.u[((size_t)b * F + f) * D.MR + D.MRrep + J3 + l] = un;
       usq += un * un;
@@ -937,9 +943,9 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       xsq += xn * xn;
     }
   };
-  upd(e0, o0, e0 ? sv[t] : 0.0, h0, hb0, x0);
-  upd(e1, o1, e1 ? sv[t + TRF_THREADS] : 0.0, h1, hb1, x1);
-  upd(eL, oL, eL ? sL[t] : 0.0, hL, hbL, xL);
+  upd(e0, o0, e0 ? sv[t] * ia : 0.0, h0, hb0, x0);
+  upd(e1, o1, e1 ? sv[t + TRF_THREADS] * ia : 0.0, h1, hb1, x1);
+  upd(eL, oL, eL ? sL[t] * ia : 0.0, hL, hbL, xL);
   TRF_PROF(6);
   block_sum3_all(usq, xsq, pa, red);
   if (t == 0) {
@@ -1045,14 +1051,17 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jv_kernel(TrfDims D, TrfBufs 
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// n-space operations of the trust-region step, with per-block partials in npart[b][blk][0..2]:
-//   0 XNORM  x.x
-//   1 DOTS   g.gn, gn.gn                            (gn = lsmr's x)
-//   2 S1T    s1 = g * c0;  s2 = gn - c1 * s1;  s2.s2  (Gram-Schmidt of [g, gn])
-//   3 S2     s2 = s2 * c2;  g.s1, g.s2
-//   4 STEP   xt = x + (s1 p0 + s2 p1);  step.step
+// n-space operations of the trust-region step, with per-block partials in npart[b][blk][field] (a field per
+// operation, so an operation can read the previous one's partials while it writes its own):
+//   0 XNORM  x.x                                                     field 0
+//   1 DOTS   g.gn                                                    field 1  (gn = lsmr's x)
+//   2 S1T    s1 = g * c0;  s2 = gn - c1 * s1;  s2.s2                 field 2  (Gram-Schmidt of [g, gn]; c0 = 1 / |g|,
+//            c1 = (g.gn) / |g| from gpart and field 1, reduced by every workgroup)
+//   3 S2     s2 = s2 * c2;  g.s1, g.s2                                fields 3, 4  (c2 = 1 / |s2| from field 2, 0 if 0)
+//   4 STEP   xt = x + (s1 p0 + s2 p1);  step.step                    field 5  (p = coef[0..1], from the host)
 //   5 ACCEPT x = xt
 enum { OP_XNORM, OP_DOTS, OP_S1T, OP_S2, OP_STEP, OP_ACCEPT };
+constexpr int TRF_NPF = 8;  // npart fields
 __global__ void __launch_bounds__(TRF_THREADS) trf_nops_kernel(TrfDims D, TrfBufs Bf, double* __restrict__ x,
                                                               double* __restrict__ xt, int op) {
   const int blk = blockIdx.x, b = blockIdx.y, t = threadIdx.x;
@@ -1062,21 +1071,31 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_nops_kernel(TrfDims D, TrfBuf
   __shared__ double red[4];
   const double* cf = Bf.coef + 4 * (size_t)b;
   const size_t nb = (size_t)b * D.NV;
+  const double* nbp = Bf.npart + (size_t)b * D.NB * TRF_NPF;
+  double c0 = 0.0, c1 = 0.0, c2 = 0.0;
+  if (op == OP_S1T) {
+    const double ng = sqrt(reduce_parts(Bf.gpart + (size_t)b * D.NB * 2, D.NB, 2, red));
+    c0 = 1.0 / ng;
+    c1 = reduce_parts(nbp + 1, D.NB, TRF_NPF, red) / ng;
+  } else if (op == OP_S2) {
+    const double nt = sqrt(reduce_parts(nbp + 2, D.NB, TRF_NPF, red));
+    c2 = nt > 0 ? 1.0 / nt : 0.0;
+  }
   double p0 = 0.0, p1 = 0.0;
   auto one = [&](size_t o) {
     switch (op) {
       case OP_XNORM: p0 += x[o] * x[o]; break;
-      case OP_DOTS: p0 += Bf.g[o] * Bf.xl[o]; p1 += Bf.xl[o] * Bf.xl[o]; break;
+      case OP_DOTS: p0 += Bf.g[o] * Bf.xl[o]; break;
       case OP_S1T: {
-        const double s1 = Bf.g[o] * cf[0];
-        const double tt = Bf.xl[o] - cf[1] * s1;
+        const double s1 = Bf.g[o] * c0;
+        const double tt = Bf.xl[o] - c1 * s1;
         Bf.s1[o] = s1;
         Bf.s2[o] = tt;
         p0 += tt * tt;
         break;
       }
       case OP_S2: {
-        const double s2 = Bf.s2[o] * cf[2];
+        const double s2 = Bf.s2[o] * c2;
         Bf.s2[o] = s2;
         p0 += Bf.g[o] * Bf.s1[o];
         p1 += Bf.g[o] * s2;
@@ -1101,9 +1120,10 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_nops_kernel(TrfDims D, TrfBuf
   p0 = block_sum_all(p0, red);
   p1 = block_sum_all(p1, red);
   if (t == 0) {
-    double* np = Bf.npart + ((size_t)b * D.NB + blk) * 4;
+    const int fld = op <= OP_S2 ? op : 5 + (op - OP_STEP);
+    double* np = Bf.npart + ((size_t)b * D.NB + blk) * TRF_NPF + fld;
     np[0] = p0;
-    np[1] = p1;
+    if (op == OP_S2) np[1] = p1;
   }
 }
 
@@ -1224,7 +1244,30 @@ void solve_trust_region_2d(const double B[3], const double g[2], double Delta, d
 
 }  // namespace
 
-int g_optim_trf_chunk = 8;  // lsmr iterations launched (one captured graph) between two reads of the done flags
+int g_optim_trf_chunk = 16;
+
+namespace {
+constexpr size_t TRF_UP_ARENA = 64 * 1024;
+struct TrfHostStage {  // per host thread: pinned staging of optim_points_trf's small transfers (never freed)
+  char* up = nullptr;
+  size_t up_cap = 0, up_off = 0;
+  double* down = nullptr;  // host-mapped, coherent: the partials the host reads, written there by the kernels
+  double* down_dev = nullptr;
+  size_t down_cap = 0;
+};
+thread_local TrfHostStage g_trf_stage;
+constexpr int TRF_MAX_DEV = 16;
+struct TrfDevCache {  // per host thread and device: capture stream, polling events, the lsmr chunk graph
+  hipStream_t cap = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipGraphExec_t exec = nullptr;
+  int chunk = 0;
+  size_t jt_lds = 0, l1_lds = 0;
+  TrfDims D{};
+  TrfBufs Bf{};
+};
+thread_local TrfDevCache g_trf_dev[TRF_MAX_DEV];
+}  // namespace  // lsmr iterations launched (one captured graph) between two reads of the done flags
 
 // dynamic LDS of the two per-iteration kernels for FB frames per block
 size_t trf_jt_lds(int FB, int n, int MR, int J, int C) {
@@ -1250,7 +1293,7 @@ size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL) {
   n += (size_t)B * F * J * C * 6;        // Jrep
   n += (size_t)B * F * NL * 4;           // lenJ
   n += (size_t)B * NV * 10;              // g vraw vn h hbar xl s1 s2 xt (+1)
-  n += (size_t)B * NB * (4 + NL + 2 + 4 + 2 + NL + 4 + 4);  // fpart fL upart vpart xpart Lpart npart jpart
+  n += (size_t)B * NB * (NL + 2 + 4 + 2 + NL);  // fL upart vpart xpart Lpart (the host-read partials are host-mapped)
   n += 2 * (size_t)B * TRF_NS + (size_t)B * 8;
   n += (size_t)NL + 2 + 2 * (size_t)B + 16;  // cons, act, done, ssf
   n += ((size_t)J + 1 + 2 * (size_t)NL) / 2 + 1;  // jadj
@@ -1319,14 +1362,11 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   Bf.s1 = take(NVB);
   Bf.s2 = take(NVB);
   double* xt = take(NVB);
-  Bf.fpart = take((size_t)B * NB * 4);
   Bf.fL = take((size_t)B * NB * NL);
   Bf.upart = take(2 * (size_t)B * NB);
   Bf.vpart = take(2 * (size_t)B * NB * 2);
   Bf.xpart = take(2 * (size_t)B * NB);
   Bf.Lpart = take((size_t)B * NB * NL);
-  Bf.npart = take((size_t)B * NB * 4);
-  Bf.jpart = take((size_t)B * NB * 4);
   Bf.st = take(2 * (size_t)B * TRF_NS);
   Bf.lctl = take(4 * (size_t)B);
   Bf.coef = take(4 * (size_t)B);
@@ -1342,11 +1382,57 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   Bf.ssf = ssf_d;
   Bf.act = act_d;
   Bf.done = done_d;
-  auto H2D = [&](void* d, const void* h, size_t bytes) {
-    return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
+  // Every small transfer of the driver goes through pinned memory: a copy from or to pageable memory waits for
+  // the stream (tens of microseconds per copy, several per trust-region iteration).  Uploads are staged in an
+  // arena that is recycled at each stream synchronisation (a copy still queued reads its own slot); downloads
+  // land in pinned arrays read after the synchronisation that follows them.
+  TrfHostStage& hs = g_trf_stage;
+  const size_t down_n = (size_t)B * NB * (4 + 2 + TRF_NPF + 4) + 2 * (size_t)B;
+  if (hs.up_cap < TRF_UP_ARENA) {
+    if (hs.up) (void)hipHostFree(hs.up);
+    hs.up = nullptr;
+    if (hipHostMalloc((void**)&hs.up, TRF_UP_ARENA, hipHostMallocPortable) != hipSuccess) return -3;
+    hs.up_cap = TRF_UP_ARENA;
+  }
+  if (hs.down_cap < down_n) {
+    if (hs.down) (void)hipHostFree(hs.down);
+    hs.down = hs.down_dev = nullptr;
+    hs.down_cap = 0;
+    if (hipHostMalloc((void**)&hs.down, sizeof(double) * down_n,
+                      hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) !=
+        hipSuccess)
+      return -3;
+    if (hipHostGetDevicePointer((void**)&hs.down_dev, hs.down, 0) != hipSuccess) return -3;
+    hs.down_cap = down_n;
+  }
+  // the partials the host reads: written by the kernels straight into host memory (no copy, no copy kernel)
+  double* hf = hs.down;                      // [B][NB][4] eval: sum r^2 at x, at the trial point, rows
+  double* hg = hf + (size_t)B * NB * 4;      // [B][NB][2] J^T f: |g|^2, max |g|
+  double* hn = hg + (size_t)B * NB * 2;      // [B][NB][TRF_NPF] n-space operations
+  double* hj = hn + (size_t)B * NB * TRF_NPF;  // [B][NB][4] J a, J c products
+  double* hitn = hj + (size_t)B * NB * 4;    // [B] lsmr iterations
+  volatile int* hdone = reinterpret_cast<volatile int*>(hitn + B);  // [B] lsmr's done flags
+  {
+    const size_t o_g = (size_t)(hg - hf), o_n = (size_t)(hn - hf), o_j = (size_t)(hj - hf), o_i = (size_t)(hitn - hf);
+    Bf.fpart = hs.down_dev;
+    Bf.gpart = hs.down_dev + o_g;
+    Bf.npart = hs.down_dev + o_n;
+    Bf.jpart = hs.down_dev + o_j;
+    Bf.hitn = hs.down_dev + o_i;
+    Bf.hdone = reinterpret_cast<int*>(hs.down_dev + o_i + B);
+  }
+  hs.up_off = 0;
+  auto sync = [&]() {
+    hs.up_off = 0;
+    return hipStreamSynchronize(s) == hipSuccess;
   };
-  auto D2H = [&](void* h, const void* d, size_t bytes) {
-    return hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s) == hipSuccess;
+  auto H2D = [&](void* d, const void* h, size_t bytes) {
+    if (bytes > TRF_UP_ARENA) return false;
+    if (hs.up_off + bytes > hs.up_cap && !sync()) return false;
+    char* st = hs.up + hs.up_off;
+    std::memcpy(st, h, bytes);
+    hs.up_off += (bytes + 255) & ~(size_t)255;
+    return hipMemcpyAsync(d, st, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
   };
   if (NL && !H2D(cons_d, cons_host, sizeof(int) * 2 * NL)) return -3;
   // J^T's constraint terms per joint (trf_jt_kernel): the constraints with the joint as their first end (+) or,
@@ -1383,77 +1469,69 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   // lsmr's iterations run as a captured graph of `chunk` (even) iterations, replayed until every done flag is
   // set: the kernels take only the slot parity, so one graph serves every chunk of the call.  Captured on a
   // private stream (the caller's may be the legacy default stream, which cannot be captured), replayed on s.
+  // The instantiated graph is kept per host thread and device and reused while the call's dimensions, buffers and
+  // chunk are the same (instantiating costs a few hundred microseconds).
   const int chunk = std::max(2, (g_optim_trf_chunk + 1) & ~1);
-  hipGraphExec_t lsmr_exec = nullptr;
-  struct ExecGuard {
-    hipGraphExec_t* e;
-    ~ExecGuard() {
-      if (*e) (void)hipGraphExecDestroy(*e);
-    }
-  } exec_guard{&lsmr_exec};
-  static hipStream_t cap = nullptr;
-  if (!cap && hipStreamCreateWithFlags(&cap, hipStreamNonBlocking) != hipSuccess) return -3;
-  static int* pinned_done = nullptr;
-  static int pinned_cap = 0;
-  static hipEvent_t done_ev[2] = {nullptr, nullptr};
-  if (pinned_cap < 2 * B) {
-    if (pinned_done) (void)hipHostFree(pinned_done);
-    pinned_done = nullptr;
-    if (hipHostMalloc((void**)&pinned_done, sizeof(int) * 2 * (size_t)B, hipHostMallocDefault) != hipSuccess) return -3;
-    pinned_cap = 2 * B;
-  }
-  for (auto& e : done_ev)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= TRF_MAX_DEV) return -3;
+  TrfDevCache& dc = g_trf_dev[dev];
+  if (!dc.cap && hipStreamCreateWithFlags(&dc.cap, hipStreamNonBlocking) != hipSuccess) return -3;
+  for (auto& e : dc.ev)
     if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -3;
-  {
+  hipEvent_t* done_ev = dc.ev;
+  if (!dc.exec || dc.chunk != chunk || dc.jt_lds != jt_lds || dc.l1_lds != l1_lds ||
+      std::memcmp(&dc.D, &D, sizeof(D)) != 0 || std::memcmp(&dc.Bf, &Bf, sizeof(Bf)) != 0) {
+    if (dc.exec) (void)hipGraphExecDestroy(dc.exec);
+    dc.exec = nullptr;
     hipGraph_t graph = nullptr;
-    if (hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal) != hipSuccess) return -3;
+    if (hipStreamBeginCapture(dc.cap, hipStreamCaptureModeThreadLocal) != hipSuccess) return -3;
     for (int i = 0; i < chunk; ++i) {
-      hipLaunchKernelGGL(trf_lsmr1_kernel<false>, grid, blk, l1_lds, cap, D, Bf, i & 1);
-      hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, cap, D, Bf, i & 1);
+      hipLaunchKernelGGL(trf_lsmr1_kernel<false>, grid, blk, l1_lds, dc.cap, D, Bf, i & 1);
+      hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, dc.cap, D, Bf, i & 1);
     }
-    if (hipStreamEndCapture(cap, &graph) != hipSuccess) return -3;
-    const bool ok = hipGraphInstantiate(&lsmr_exec, graph, nullptr, nullptr, 0) == hipSuccess;
+    if (hipStreamEndCapture(dc.cap, &graph) != hipSuccess) return -3;
+    const bool ok = hipGraphInstantiate(&dc.exec, graph, nullptr, nullptr, 0) == hipSuccess;
     (void)hipGraphDestroy(graph);
-    if (!ok) return -3;
+    if (!ok) {
+      dc.exec = nullptr;
+      return -3;
+    }
+    dc.chunk = chunk;
+    dc.jt_lds = jt_lds;
+    dc.l1_lds = l1_lds;
+    std::memcpy(&dc.D, &D, sizeof(D));
+    std::memcpy(&dc.Bf, &Bf, sizeof(Bf));
   }
-  std::vector<double> part((size_t)B * NB * 4), vp((size_t)B * NB * 2), ctl(4 * (size_t)B), coef(4 * (size_t)B, 0.0);
-  auto sync = [&]() { return hipStreamSynchronize(s) == hipSuccess; };
+  const hipGraphExec_t lsmr_exec = dc.exec;
+  std::vector<double> ctl(4 * (size_t)B), coef(4 * (size_t)B, 0.0);
   auto upload_act = [&]() { return H2D(act_d, act.data(), sizeof(int) * B); };
   // per-animal sums of a partial field over the blocks (fixed order)
-  auto sum_field = [&](const std::vector<double>& p, int stride, int field, int b) {
+  auto sum_field = [&](const double* p, int stride, int field, int b) {
     double v = 0.0;
     for (int k = 0; k < NB; ++k) v += p[((size_t)b * NB + k) * stride + field];
     return v;
   };
-  // J, f, cost at x (mode 1) and g = J^T f with its norms, for the animals in act
-  std::vector<double> cost(B), gnorm2(B), ginf(B), rows(B);
+  // At an accepted x, for the animals in act, with one synchronisation: J, f, cost (mode 1), g = J^T f with its
+  // norms, |x|, and J g (the next iteration's `regularize`)
+  std::vector<double> cost(B), gnorm2(B), ginf(B), rows(B), xnorm(B), areg(B);
   auto jac_and_grad = [&]() -> bool {
     hipLaunchKernelGGL(trf_eval_kernel, grid, blk, 0, s, D, Bf, x, Bf.fres, 1);
     hipLaunchKernelGGL(trf_jt_kernel<0>, grid, blk, jt_lds, s, D, Bf, 0);
-    if (!D2H(part.data(), Bf.fpart, sizeof(double) * part.size())) return false;
-    if (!D2H(vp.data(), Bf.vpart, sizeof(double) * vp.size())) return false;
+    hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_XNORM);
+    hipLaunchKernelGGL(trf_jv_kernel, grid, blk, 0, s, D, Bf, (const double*)Bf.g, (const double*)nullptr);
     if (!sync()) return false;
     for (int b = 0; b < B; ++b) {
       if (!act[b]) continue;
-      cost[b] = 0.5 * sum_field(part, 4, 0, b);
-      rows[b] = sum_field(part, 4, 2, b);
-      gnorm2[b] = sum_field(vp, 2, 0, b);
+      cost[b] = 0.5 * sum_field(hf, 4, 0, b);
+      rows[b] = sum_field(hf, 4, 2, b);
+      gnorm2[b] = sum_field(hg, 2, 0, b);
       double m = 0.0;
-      for (int k = 0; k < NB; ++k) m = std::max(m, vp[((size_t)b * NB + k) * 2 + 1]);
+      for (int k = 0; k < NB; ++k) m = std::max(m, hg[((size_t)b * NB + k) * 2 + 1]);
       ginf[b] = m;
+      xnorm[b] = std::sqrt(sum_field(hn, TRF_NPF, 0, b));
+      areg[b] = 0.5 * sum_field(hj, 4, 0, b);
     }
     return true;
-  };
-  auto nops = [&](double* xx, double* xtt, int op, bool read) -> bool {
-    hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, xx, xtt, op);
-    if (!read) return true;
-    if (!D2H(part.data(), Bf.npart, sizeof(double) * part.size())) return false;
-    return sync();
-  };
-  auto jv = [&](const double* a, const double* c) -> bool {
-    hipLaunchKernelGGL(trf_jv_kernel, grid, blk, 0, s, D, Bf, a, c);
-    if (!D2H(part.data(), Bf.jpart, sizeof(double) * part.size())) return false;
-    return sync();
   };
 
   const int nparam = fix_lengths ? D.NX : D.NV;
@@ -1462,12 +1540,10 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   enum { RUN, STOP };
   std::vector<int> state(B, RUN), status(B, 0), lsmr_total(B, 0), lsmr_max(B, 0);
   std::vector<long long> nfev(B, 1), njev(B, 1);
-  std::vector<double> Delta(B), xnorm(B), damp(B), BS(3 * (size_t)B), gS(2 * (size_t)B), cost_new(B), actual(B);
+  std::vector<double> Delta(B), damp(B), BS(3 * (size_t)B), gS(2 * (size_t)B), cost_new(B), actual(B);
   if (!jac_and_grad()) return -3;
-  if (!nops(x, xt, OP_XNORM, true)) return -3;
   for (int b = 0; b < B; ++b) {
     stats[8 * b + 0] = cost[b];
-    xnorm[b] = std::sqrt(sum_field(part, 4, 0, b));
     Delta[b] = xnorm[b] == 0 ? 1.0 : xnorm[b];
   }
   for (;;) {
@@ -1485,13 +1561,12 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     }
     if (!any) break;
     if (!upload_act()) return -3;
-    // regularize: the 1-D quadratic along -g inside the trust region (trf.py:480-484)
-    if (!jv(Bf.g, nullptr)) return -3;
+    // regularize: the 1-D quadratic along -g inside the trust region (trf.py:480-484; J g from jac_and_grad)
     for (int b = 0; b < B; ++b) {
       ctl[4 * b] = ctl[4 * b + 1] = ctl[4 * b + 2] = ctl[4 * b + 3] = 0.0;
       doneh[b] = act[b] ? 0 : 1;
       if (!act[b]) continue;
-      const double a = 0.5 * sum_field(part, 4, 0, b);
+      const double a = areg[b];
       const double bq = -gnorm2[b];
       const double to_tr = Delta[b] / std::sqrt(gnorm2[b]);
       double ag = 0.0 * (a * 0.0 + bq);
@@ -1512,6 +1587,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     }
     if (!H2D(Bf.lctl, ctl.data(), sizeof(double) * ctl.size())) return -3;
     if (!H2D(done_d, doneh.data(), sizeof(int) * B)) return -3;
+    for (int b = 0; b < B; ++b) hdone[b] = doneh[b];  // (no kernel writes it before this iteration's lsmr)
     // lsmr(J, f, damp)
     hipLaunchKernelGGL(trf_jt_kernel<1>, grid, blk, jt_lds, s, D, Bf, 0);
     hipLaunchKernelGGL(trf_lsmr1_kernel<true>, grid, blk, l1_lds, s, D, Bf, 1);
@@ -1520,55 +1596,38 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     double maxit = 0.0;
     for (int b = 0; b < B; ++b)
       if (act[b]) maxit = std::max(maxit, ctl[4 * b + 2]);
-    // chunks run back to back: the done flags of chunk i are copied to pinned memory behind it and read
-    // while chunk i + 1 runs (a finished animal's kernels return at once), so no chunk waits on the host
+    // chunks run back to back: the kernels write the done flags into host memory too, and the host reads them
+    // once chunk i - 1 has finished, while chunk i runs (a finished animal's kernels return at once), so no
+    // chunk waits on the host
     int ci = 0;
     for (;; ++ci) {
       if (hipGraphLaunch(lsmr_exec, s) != hipSuccess) return -3;
       k += chunk;
-      int* slot = pinned_done + (size_t)(ci & 1) * B;
-      if (hipMemcpyAsync(slot, done_d, sizeof(int) * B, hipMemcpyDeviceToHost, s) != hipSuccess) return -3;
       if (hipEventRecord(done_ev[ci & 1], s) != hipSuccess) return -3;
       if (ci == 0) continue;
       if (hipEventSynchronize(done_ev[(ci - 1) & 1]) != hipSuccess) return -3;
-      const int* prev = pinned_done + (size_t)((ci - 1) & 1) * B;
       bool all = true;
-      for (int b = 0; b < B; ++b) all &= prev[b] != 0;
+      for (int b = 0; b < B; ++b) all &= hdone[b] != 0;
       if (all) break;
       if (k > maxit + 4 + 2 * chunk) return -7;  // the device test stops every run by maxiter
     }
-    if (!D2H(ctl.data(), Bf.lctl, sizeof(double) * ctl.size())) return -3;
-    // S = orth([g, gn]) by Gram-Schmidt, B_S and g_S (trf.py:489-493)
-    if (!nops(x, xt, OP_DOTS, true)) return -3;
+    // S = orth([g, gn]) by Gram-Schmidt (its coefficients reduced on the device), g_S and B_S (trf.py:489-493),
+    // with one synchronisation
+    hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_DOTS);
+    hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_S1T);
+    hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_S2);
+    hipLaunchKernelGGL(trf_jv_kernel, grid, blk, 0, s, D, Bf, (const double*)Bf.s1, (const double*)Bf.s2);
+    if (!sync()) return -3;
     for (int b = 0; b < B; ++b) {
       if (!act[b]) continue;
-      const int it = (int)ctl[4 * b + 3];
+      const int it = (int)hitn[b];
       lsmr_total[b] += it;
       lsmr_max[b] = std::max(lsmr_max[b], it);
-      const double ng = std::sqrt(gnorm2[b]);
-      coef[4 * b] = 1.0 / ng;
-      coef[4 * b + 1] = sum_field(part, 4, 0, b) / ng;  // s1 . gn
-    }
-    if (!H2D(Bf.coef, coef.data(), sizeof(double) * coef.size())) return -3;
-    if (!nops(x, xt, OP_S1T, true)) return -3;
-    for (int b = 0; b < B; ++b) {
-      if (!act[b]) continue;
-      const double nt = std::sqrt(sum_field(part, 4, 0, b));
-      coef[4 * b + 2] = nt > 0 ? 1.0 / nt : 0.0;
-    }
-    if (!H2D(Bf.coef, coef.data(), sizeof(double) * coef.size())) return -3;
-    if (!nops(x, xt, OP_S2, true)) return -3;
-    for (int b = 0; b < B; ++b) {
-      if (!act[b]) continue;
-      gS[2 * b] = sum_field(part, 4, 0, b);
-      gS[2 * b + 1] = sum_field(part, 4, 1, b);
-    }
-    if (!jv(Bf.s1, Bf.s2)) return -3;
-    for (int b = 0; b < B; ++b) {
-      if (!act[b]) continue;
-      BS[3 * b] = sum_field(part, 4, 0, b);
-      BS[3 * b + 1] = sum_field(part, 4, 2, b);
-      BS[3 * b + 2] = sum_field(part, 4, 1, b);
+      gS[2 * b] = sum_field(hn, TRF_NPF, 3, b);
+      gS[2 * b + 1] = sum_field(hn, TRF_NPF, 4, b);
+      BS[3 * b] = sum_field(hj, 4, 0, b);
+      BS[3 * b + 1] = sum_field(hj, 4, 2, b);
+      BS[3 * b + 2] = sum_field(hj, 4, 1, b);
     }
     // the trial steps (trf.py:496-540), every animal until it accepts, terminates or runs out of evaluations
     std::vector<int> trial(B, 0);
@@ -1595,17 +1654,14 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
       if (!upload_act()) return -3;
       if (!H2D(Bf.coef, coef.data(), sizeof(double) * coef.size())) return -3;
       hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_STEP);
-      std::vector<double> stp((size_t)B * NB * 4);
-      if (!D2H(stp.data(), Bf.npart, sizeof(double) * stp.size())) return -3;
       hipLaunchKernelGGL(trf_eval_kernel, grid, blk, 0, s, D, Bf, xt, Bf.ftr, 0);
-      if (!D2H(part.data(), Bf.fpart, sizeof(double) * part.size())) return -3;
       if (!sync()) return -3;
       for (int b = 0; b < B; ++b) {
         if (!act[b]) continue;
         nfev[b]++;
-        const double sh = std::sqrt(sum_field(stp, 4, 0, b));
+        const double sh = std::sqrt(sum_field(hn, TRF_NPF, 5, b));
         step_norm[b] = sh;
-        const double cn = 0.5 * sum_field(part, 4, 1, b);
+        const double cn = 0.5 * sum_field(hf, 4, 1, b);
         if (!std::isfinite(cn)) {
           Delta[b] = 0.25 * sh;
           actual[b] = -1;
@@ -1642,15 +1698,12 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     }
     if (anya) {
       if (!upload_act()) return -3;
-      if (!nops(x, xt, OP_ACCEPT, false)) return -3;
+      hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_ACCEPT);
       // the Jacobian of a terminating animal is not needed (scipy evaluates it, njev counts it)
       for (int b = 0; b < B; ++b)
         if (act[b] && status[b] != 0) act[b] = 0;
       if (!upload_act()) return -3;
       if (!jac_and_grad()) return -3;
-      if (!nops(x, xt, OP_XNORM, true)) return -3;
-      for (int b = 0; b < B; ++b)
-        if (act[b]) xnorm[b] = std::sqrt(sum_field(part, 4, 0, b));
     }
   }
 #ifdef TRF_PROFILE
@@ -1665,6 +1718,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     }
   }
 #endif
+  if (!sync()) return -3;  // (the staging arena is the next call's)
   for (int b = 0; b < B; ++b) {
     stats[8 * b + 1] = cost[b];
     stats[8 * b + 2] = (double)(njev[b] - 1);

@@ -139,7 +139,7 @@ def test_tuning_knobs_only_select_equivalent_variants(lib):
         assert lib.mq_set_tuning(key, 1) == -2, key
         assert lib.mq_get_tuning(key) == -2, key
     for key, default, other in ((2, 0, 1), (12, 1, 0), (18, 1, 0), (19, 1, 0), (20, 1, 0), (4, 40, 10),
-                                (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1), (22, 8, 1), (23, 0, 1), (24, 1, 0)):
+                                (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1), (22, 16, 1), (23, 0, 1), (24, 1, 0)):
         assert lib.mq_get_tuning(key) == default
         assert lib.mq_set_tuning(key, other) == 0
         assert lib.mq_get_tuning(key) == other
