@@ -52,7 +52,8 @@ extern "C" {
  *        below scipy's cost on every marker scene probed, where ftol alone stopped 1.5 % above it on one).
  *   7 -- mq_optim_points takes a solver (0: scipy's trust-region-reflective + lsmr, restated -- the default and
  *        the parity mode; 1: the Levenberg-Marquardt + PCG solver of ABI 1-6) and writes 8 stats per animal;
- *        tuning keys MQ_TUNE_OPTIM_TRF_CHUNK (22), MQ_TUNE_VIT_RESID_F32 (23) and MQ_TUNE_ATTN_KRING (24) added. */
+ *        tuning keys MQ_TUNE_OPTIM_TRF_CHUNK (22), MQ_TUNE_VIT_RESID_F32 (23), MQ_TUNE_ATTN_KRING (24) and
+ *        MQ_TUNE_OPTIM_TRF_FB (25) added. */
 #define MQ_ABI_VERSION 7
 
 typedef struct mq_ctx mq_ctx;
@@ -88,6 +89,8 @@ const char* mq_last_error(void);
                                        compiler-scheduled loop (bit-identical; the fallback for a toolchain change) */
 #define MQ_TUNE_OPTIM_TRF_CHUNK 22  /* lsmr iterations the trust-region solver launches between two reads of its done
                                        flags (default 16, 1..64; same results) */
+#define MQ_TUNE_OPTIM_TRF_FB 25     /* most frames per workgroup of the trust-region solver's kernels (default 4, 1..4;
+                                       same algorithm, the fixed reduction order follows the blocks) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

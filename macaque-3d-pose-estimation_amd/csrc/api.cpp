@@ -181,6 +181,10 @@ int mq_set_tuning(int key, int value) {
       if (value < 1 || value > 64) return fail("mq_set_tuning: lsmr chunk must be in [1, 64]", -2);
       mq::g_optim_trf_chunk = value;
       break;
+    case MQ_TUNE_OPTIM_TRF_FB:
+      if (value < 1 || value > 4) return fail("mq_set_tuning: frames per workgroup must be in [1, 4]", -2);
+      mq::g_optim_trf_fb = value;
+      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -200,6 +204,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_ATTN_KRING: return mq::g_attn_kring;
     case MQ_TUNE_OPTIM_STOP: return mq::g_optim_stop;
     case MQ_TUNE_OPTIM_TRF_CHUNK: return mq::g_optim_trf_chunk;
+    case MQ_TUNE_OPTIM_TRF_FB: return mq::g_optim_trf_fb;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }

@@ -109,6 +109,7 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
                  double* stats, hipStream_t s);
 // the scipy-faithful trust-region solver (optim_trf.hip); stats (B, 8)
 extern int g_optim_trf_chunk;
+extern int g_optim_trf_fb;
 size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL);
 int optim_points_trf(const double* cams, int C, const double* p2d, double* x, int B, int F, int J, const int* cons_host,
                      int n_strong, int n_weak, const double* ssf_host, double scale_length, double scale_length_weak,

@@ -1245,6 +1245,7 @@ void solve_trust_region_2d(const double B[3], const double g[2], double Delta, d
 }  // namespace
 
 int g_optim_trf_chunk = 16;
+int g_optim_trf_fb = TRF_FB;
 
 namespace {
 constexpr size_t TRF_UP_ARENA = 64 * 1024;
@@ -1277,16 +1278,36 @@ size_t trf_l1_lds(int FB, int MR, int J, int C) {
   return ((((size_t)FB * MR + 1) & ~(size_t)1) + (size_t)FB * J * C * 6) * sizeof(double);
 }
 constexpr size_t TRF_DYN_LDS = 128 * 1024;  // (the kernels' static LDS stays under 24 KB)
-int trf_frames_per_block(int J, int C, int NL, int n) {
+// Frames per workgroup.  `fit`: the most (<= TRF_FB and the MQ_TUNE_OPTIM_TRF_FB cap) whose rows fit in LDS.  The
+// per-iteration kernels are latency-bound chains, so fewer frames per workgroup shorten each one's chain while
+// the grid still has a CU per workgroup: the smallest count whose grid fits the device's CUs, else `fit`
+// (profiles/r05u_*: 24 frames x 4 animals 8 % faster at 1 frame than at 4; 300 x 4, which fills the CUs
+// at 4, 60 % slower at 1).  Monotonic in `fit`, so the workspace, sized at the deepest smoothing order, never
+// has fewer blocks than a call.
+static int trf_cu_count() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                             hipSuccess || cus <= 0)
+    return 256;
+  return cus;
+}
+int trf_frames_per_block(int J, int C, int NL, int n, int B, int F) {
   const int MR = (J * C * 2 + J * 3 + NL + 1) & ~1;
-  for (int fb = TRF_FB; fb > 1; --fb)
-    if (trf_jt_lds(fb, n, MR, J, C) <= TRF_DYN_LDS && trf_l1_lds(fb, MR, J, C) <= TRF_DYN_LDS) return fb;
-  return 1;
+  int fit = 1;
+  for (int fb = std::min(TRF_FB, std::max(1, g_optim_trf_fb)); fb > 1; --fb)
+    if (trf_jt_lds(fb, n, MR, J, C) <= TRF_DYN_LDS && trf_l1_lds(fb, MR, J, C) <= TRF_DYN_LDS) {
+      fit = fb;
+      break;
+    }
+  const long long cus = trf_cu_count();
+  for (int fb = 1; fb < fit; ++fb)
+    if ((long long)B * ((F + fb - 1) / fb) <= cus) return fb;
+  return fit;
 }
 
 size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL) {
   const size_t NV = (size_t)F * J * 3 + NL, MR = ((size_t)J * C * 2 + (size_t)J * 3 + NL + 1) & ~(size_t)1;
-  const int FB = trf_frames_per_block(J, C, NL, TRF_MAXN);
+  const int FB = trf_frames_per_block(J, C, NL, TRF_MAXN, B, F);
   const size_t NB = ((size_t)F + FB - 1) / FB;
   size_t n = 0;
   n += (size_t)B * F * MR * 3;           // fres ftr u
@@ -1324,7 +1345,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   D.NV = D.NX + NL;
   D.MRrep = J * C * 2;
   D.MR = (D.MRrep + J * 3 + NL + 1) & ~1;  // even: 16-B aligned rows for the LDS staging
-  D.FB = trf_frames_per_block(J, C, NL, n_deriv);
+  D.FB = trf_frames_per_block(J, C, NL, n_deriv, B, F);
   D.NB = (F + D.FB - 1) / D.FB;
   D.rp = rp;
   D.s_len = scale_length;

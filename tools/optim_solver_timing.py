@@ -1,7 +1,7 @@
 """Wall time of optim_points per solver ("trf": scipy's algorithm restated, the default; "lm"): BASELINE config 4's
 300-frame clip (4 individuals, the bench's lift inputs after Viterbi + RANSAC) and the marker-scene problems of
 tests/golden/optim_problems.npz (4 individuals per scene), median of --reps after a warm-up, with the solver stats.
-python tools/optim_solver_timing.py [--reps 3] [--solvers trf,lm] [--chunk 8]"""
+python tools/optim_solver_timing.py [--reps 3] [--solvers trf,lm] [--chunk 16] [--fb 4]"""
 import argparse
 import json
 import os
@@ -49,6 +49,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--solvers", default="trf,lm")
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--fb", type=int, default=0, help="most frames per workgroup (MQ_TUNE_OPTIM_TRF_FB)")
     ap.add_argument("--cases", default="config4,s7f24,s8f24,s9f24")
     ap.add_argument("--lib", default="", help="another build of libmq_hip.so (e.g. the -DTRF_PROFILE one in lib_prof/)")
     a = ap.parse_args()
@@ -59,6 +60,8 @@ def main():
     from mqhip.optim import optim_points_batch
     if a.chunk:
         _lib.check(_lib.Context.get(0).lib.mq_set_tuning(22, a.chunk), "chunk")
+    if a.fb:
+        _lib.check(_lib.Context.get(0).lib.mq_set_tuning(25, a.fb), "fb")
     for case in a.cases.split(","):
         g, P2, I3, cons, weak, args = config4_problem() if case == "config4" else marker_problems(case)
         for solver in a.solvers.split(","):
