@@ -43,16 +43,20 @@ constexpr int TRF_MAXJ = 32, TRF_MAXL = 64, TRF_MAXN = 3;
 constexpr int TRF_NS = 24;  // lsmr state doubles per slot
 
 // -DTRF_PROFILE builds (tools only, never the shipped library): wall-clock time per phase of the two lsmr
-// kernels, block 0 of animal 0, summed over launches and printed at the end of optim_points_trf.
+// kernels, block TRF_PROFILE_BLOCK (default 0) of animal 0, summed over launches and printed at the end of
+// optim_points_trf.
 #ifdef TRF_PROFILE
 __device__ unsigned long long g_trf_prof[2][12];
 #define TRF_PROF_BEGIN() \
   unsigned long long prof_t[12]; \
   prof_t[0] = wall_clock64()
+#ifndef TRF_PROFILE_BLOCK
+#define TRF_PROFILE_BLOCK 0
+#endif
 #define TRF_PROF(k) prof_t[k] = wall_clock64()
 #define TRF_PROF_END(kern, last)                                                       \
   do {                                                                                  \
-    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) {                       \
+    if (threadIdx.x == 0 && blockIdx.x == TRF_PROFILE_BLOCK && blockIdx.y == 0) {       \
       for (int k = 1; k <= last; ++k) atomicAdd(&g_trf_prof[kern][k], prof_t[k] - prof_t[k - 1]); \
       atomicAdd(&g_trf_prof[kern][0], 1ull);                                           \
     }                                                                                   \
@@ -66,6 +70,7 @@ __device__ unsigned long long g_trf_prof[2][12];
 struct TrfDims {
   int B, C, F, J, NL, nS, fix, n, loss;
   int NX, NV, MR, MRrep, NB, FB;
+  int NBV;  // slots of the J^T partials: NB + 1 when the length variables have a workgroup of their own, else NB
   double rp, s_len, s_len_weak;
   double c[TRF_MAXN + 1];
   double atol, btol, ctol;
@@ -84,12 +89,12 @@ struct TrfBufs {
   double* fpart;  // [B][NB][4]: sum r^2 at x, sum r^2 at the trial point, rows (host-mapped)
   double* fL;     // [B][NB][NL]: sum over the block's frames of dL * r_len at x
   double* upart;  // [2][B][NB]
-  double* vpart;  // [2][B][NB][2]: sum v^2, max |v|
+  double* vpart;  // [2][B][NBV][2]: sum v^2, max |v| (slot NB, if NBV = NB + 1: the length variables)
   double* xpart;  // [2][B][NB]
   double* Lpart;  // [B][NB][NL]
   double* npart;  // [B][NB][TRF_NPF] (host-mapped)
   double* jpart;  // [B][NB][4] (host-mapped)
-  double* gpart;  // [B][NB][2]: |g|^2, max |g| (host-mapped)
+  double* gpart;  // [B][NBV][2]: |g|^2, max |g| (host-mapped)
   double* hitn;   // [B]: lsmr's final iteration count (host-mapped)
   int* hdone;     // [B]: copy of done (host-mapped), polled by the host between chunks
   double* st;     // [2][B][TRF_NS]
@@ -459,7 +464,61 @@ __device__ __forceinline__ void length_sums(const TrfDims& D, const double* __re
   __syncthreads();
 }
 
-// v = J^T (u / beta) - beta vn for the block's parameters (and block 0's length variables).
+// The length variables, in a workgroup of their own (the last of a J^T launch, blockIdx.x == NB) when the grid
+// leaves a CU for it (D.NBV == NB + 1): v = the sum over the frames of dL * u_len (the per-block sums of the
+// m-space launch: Lpart, or fL for MODE 0 / 1) / beta, minus beta vn in MODE 2; its partials go to slot NB.
+// Done by block 0 alongside its frames, the NB x NL sums make that block, and so the launch, 1.2 us longer
+// (profiles/r05x_*); on a grid that already has more workgroups than CUs an extra one costs more than that
+// (config 4: 4 % slower, profiles/r05z_*), and block 0 keeps them.
+template <int MODE>
+__device__ __forceinline__ void jt_lengths(const TrfDims& D, const TrfBufs& Bf, int par, int b, double* red,
+                                           double* spart, double* sLs) {
+  const int t = threadIdx.x, NL = D.NL, NB = D.NB;
+  const double normb = Bf.lctl[4 * b + 1];
+  const double* up = Bf.upart + ((size_t)par * D.B + b) * NB;
+  double pu = 0.0;
+  if (MODE == 2 && t < NB) pu = up[t];
+  const size_t nb = (size_t)b * D.NV;
+  const bool lens = !D.fix && NL > 0;
+  double vnL = 0.0;
+  if (MODE == 2 && lens && t < NL) vnL = Bf.vn[nb + D.NX + t];
+  const double* lp = (MODE == 2 ? Bf.Lpart : Bf.fL) + (size_t)b * NB * NL;
+  double lv[LEN_U];
+  if (lens) length_preload(D, lp, lv);
+  if (!Bf.act[b] || (MODE > 0 && Bf.done[b])) return;
+  if (MODE == 2)
+    for (int i = t + TRF_THREADS; i < NB; i += TRF_THREADS) pu += up[i];
+  if (lens) length_sums(D, lp, lv, spart, sLs);
+  double beta = 1.0;
+  if (MODE == 1) beta = normb;
+  if (MODE == 2) {  // (the same reduction, in the same order, as every other workgroup's)
+    double d1 = 0.0, d2 = 0.0;
+    block_sum3_all(pu, d1, d2, red);
+    beta = sqrt(pu);
+  }
+  const double ib = 1.0 / beta;
+  double vsq = 0.0, vmax = 0.0;
+  if (t < NL) {
+    double v = 0.0;
+    if (lens) {
+      const double acc = sLs[t] * ib;
+      v = MODE == 2 ? vnL * -beta + acc : acc;
+      vsq = v * v;
+      vmax = fabs(v);
+    }
+    (MODE == 0 ? Bf.g : Bf.vraw)[nb + D.NX + t] = v;
+  }
+  vsq = block_sum_all(vsq, red);
+  if (MODE == 0) vmax = block_max_all(vmax, red);
+  if (t == 0) {
+    double* vp = MODE == 0 ? Bf.gpart + ((size_t)b * D.NBV + NB) * 2
+                           : Bf.vpart + (((size_t)par * D.B + b) * D.NBV + NB) * 2;
+    vp[0] = vsq;
+    vp[1] = vmax;
+  }
+}
+
+// v = J^T (u / beta) - beta vn for the block's parameters (blockIdx.x < NB; the length variables: jt_lengths).
 //   MODE 0: g = J^T f (u = fres, beta = 1, no vn); partials (sum g^2, max |g|) in gpart
 //   MODE 1: lsmr's start, v = J^T (f / normb)
 //   MODE 2: lsmr phase 2 of iteration k: v_k = J^T (u_k / beta_k) - beta_k v_{k-1}  (par = k & 1)
@@ -477,6 +536,10 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
   __shared__ double spart[TRF_THREADS];
   __shared__ double sLs[TRF_MAXL];
   extern __shared__ double lds_jt[];
+  if (blk == NB) {  // (only launched when D.NBV == NB + 1)
+    jt_lengths<MODE>(D, Bf, par, b, red, spart, sLs);
+    return;
+  }
   const int fa = max(0, f0 - n), nrow = (f0 + nf - fa) * D.MR;
   double* su = lds_jt;
   double* sj = lds_jt + (((size_t)(D.FB + D.n) * D.MR + 1) & ~(size_t)1);
@@ -488,13 +551,14 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
   double pu = 0.0;
   if (MODE == 2 && t < NB) pu = up[t];
   const size_t nb = (size_t)b * D.NV;
-  double vn0 = 0.0, vn1 = 0.0, vnL = 0.0;  // the thread's (at most two) parameters and block 0's length variable
+  double vn0 = 0.0, vn1 = 0.0, vnL = 0.0;  // the thread's (at most two) parameters and a length variable
+  const bool lblk = blk == 0 && D.NBV == NB;   // block 0 holds the length variables
   if (MODE == 2) {
     if (t < nf * J3) vn0 = Bf.vn[nb + (size_t)f0 * J3 + t];
     if (t + TRF_THREADS < nf * J3) vn1 = Bf.vn[nb + (size_t)f0 * J3 + t + TRF_THREADS];
-    if (blk == 0 && t < NL && !D.fix) vnL = Bf.vn[nb + D.NX + t];
+    if (lblk && t < NL && !D.fix) vnL = Bf.vn[nb + D.NX + t];
   }
-  const bool lens = blk == 0 && !D.fix && NL > 0;
+  const bool lens = lblk && !D.fix && NL > 0;
   const double* lp = (MODE == 2 ? Bf.Lpart : Bf.fL) + (size_t)b * NB * NL;
   double lv[LEN_U];
   if (lens) length_preload(D, lp, lv);
@@ -579,7 +643,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
     vsq += v * v;
     vmax = fmax(vmax, fabs(v));
   }
-  if (blk == 0 && t < NL) {  // the length variables: sum over frames of dL * u_len
+  if (lblk && t < NL) {  // the length variables: sum over frames of dL * u_len
     const size_t o = nb + D.NX + t;
     double v = 0.0;
     if (!D.fix) {
@@ -594,7 +658,8 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
   vsq = block_sum_all(vsq, red);
   if (MODE == 0) vmax = block_max_all(vmax, red);
   if (t == 0) {
-    double* vp = MODE == 0 ? Bf.gpart + ((size_t)b * NB + blk) * 2 : Bf.vpart + (((size_t)par * D.B + b) * NB + blk) * 2;
+    double* vp = MODE == 0 ? Bf.gpart + ((size_t)b * D.NBV + blk) * 2
+                           : Bf.vpart + (((size_t)par * D.B + b) * D.NBV + blk) * 2;
     vp[0] = vsq;
     vp[1] = vmax;
   }
@@ -717,16 +782,14 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
   const size_t nb = (size_t)b * D.NV;
   // 1. loads independent of the norms, all issued before the first wait
   const double damp = Bf.lctl[4 * b], normb = Bf.lctl[4 * b + 1], maxiter = Bf.lctl[4 * b + 2], ssf = Bf.ssf[b];
-  const double* vp = Bf.vpart + ((size_t)pp * D.B + b) * NB * 2;
+  const double* vp = Bf.vpart + ((size_t)pp * D.B + b) * D.NBV * 2;
   const double* upp = Bf.upart + ((size_t)pp * D.B + b) * NB;
   const double* xp = Bf.xpart + ((size_t)pp * D.B + b) * NB;
   double pa = 0.0, pb = 0.0, px = 0.0;
-  if (t < NB) {
-    pa = vp[2 * t];
-    if (!FIRST) {
-      pb = upp[t];
-      px = xp[t];
-    }
+  if (t < D.NBV) pa = vp[2 * t];
+  if (!FIRST && t < NB) {
+    pb = upp[t];
+    px = xp[t];
   }
   const double stv = (!FIRST && t < TRF_NS) ? Bf.st[((size_t)pp * D.B + b) * TRF_NS + t] : 0.0;
   const int nfx = min(nf + n, F - f0);
@@ -769,13 +832,12 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
   if (t < NL) sL[t] = lv;
   if (t < 2 * NL) scons[t] = cv;
   st.store();
-  for (int i = t + TRF_THREADS; i < NB; i += TRF_THREADS) {
-    pa += vp[2 * i];
-    if (!FIRST) {
+  for (int i = t + TRF_THREADS; i < D.NBV; i += TRF_THREADS) pa += vp[2 * i];
+  if (!FIRST)
+    for (int i = t + TRF_THREADS; i < NB; i += TRF_THREADS) {
       pb += upp[i];
       px += xp[i];
     }
-  }
   TRF_PROF(2);
   // 2. the norms (one combined reduction; also the barrier after the staging stores)
   block_sum3_all(pa, pb, px, red);
@@ -835,7 +897,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       for (int i = 0; i < TRF_NS; ++i) So[i] = S[i];
     }
 #ifdef TRF_PROFILE
-    if (!FIRST && blk == 0 && b == 0) atomicAdd(&g_trf_prof[1][8], wall_clock64() - prof_t[3]);  // the recurrence
+    if (!FIRST && blk == TRF_PROFILE_BLOCK && b == 0) atomicAdd(&g_trf_prof[1][8], wall_clock64() - prof_t[3]);  // the recurrence
 #endif
   }
   const double ib = 1.0 / beta;
@@ -960,7 +1022,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
   TRF_PROF(7);
   if (!FIRST) TRF_PROF_END(0, 7);
 #ifdef TRF_PROFILE
-  if (!FIRST && t == 0 && blk == 0 && b == 0) {  // the m-space split: rows from phase 3's start
+  if (!FIRST && t == 0 && blk == TRF_PROFILE_BLOCK && b == 0) {  // the m-space split: rows from phase 3's start
     atomicAdd(&g_trf_prof[0][8], prof_t[8] - prof_t[3]);
     atomicAdd(&g_trf_prof[0][9], prof_t[9] - prof_t[8]);
     atomicAdd(&g_trf_prof[0][10], prof_t[4] - prof_t[9]);
@@ -1074,7 +1136,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_nops_kernel(TrfDims D, TrfBuf
   const double* nbp = Bf.npart + (size_t)b * D.NB * TRF_NPF;
   double c0 = 0.0, c1 = 0.0, c2 = 0.0;
   if (op == OP_S1T) {
-    const double ng = sqrt(reduce_parts(Bf.gpart + (size_t)b * D.NB * 2, D.NB, 2, red));
+    const double ng = sqrt(reduce_parts(Bf.gpart + (size_t)b * D.NBV * 2, D.NBV, 2, red));
     c0 = 1.0 / ng;
     c1 = reduce_parts(nbp + 1, D.NB, TRF_NPF, red) / ng;
   } else if (op == OP_S2) {
@@ -1314,7 +1376,8 @@ size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL) {
   n += (size_t)B * F * J * C * 6;        // Jrep
   n += (size_t)B * F * NL * 4;           // lenJ
   n += (size_t)B * NV * 10;              // g vraw vn h hbar xl s1 s2 xt (+1)
-  n += (size_t)B * NB * (NL + 2 + 4 + 2 + NL);  // fL upart vpart xpart Lpart (the host-read partials are host-mapped)
+  n += (size_t)B * NB * (NL + 2 + 2 + NL) + 4 * (size_t)B * (NB + 1);  // fL upart xpart Lpart vpart (the host-read
+                                                                         // partials are host-mapped)
   n += 2 * (size_t)B * TRF_NS + (size_t)B * 8;
   n += (size_t)NL + 2 + 2 * (size_t)B + 16;  // cons, act, done, ssf
   n += ((size_t)J + 1 + 2 * (size_t)NL) / 2 + 1;  // jadj
@@ -1347,6 +1410,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   D.MR = (D.MRrep + J * 3 + NL + 1) & ~1;  // even: 16-B aligned rows for the LDS staging
   D.FB = trf_frames_per_block(J, C, NL, n_deriv, B, F);
   D.NB = (F + D.FB - 1) / D.FB;
+  D.NBV = (long long)B * (D.NB + 1) <= trf_cu_count() ? D.NB + 1 : D.NB;
   D.rp = rp;
   D.s_len = scale_length;
   D.s_len_weak = scale_length_weak;
@@ -1385,7 +1449,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   double* xt = take(NVB);
   Bf.fL = take((size_t)B * NB * NL);
   Bf.upart = take(2 * (size_t)B * NB);
-  Bf.vpart = take(2 * (size_t)B * NB * 2);
+  Bf.vpart = take(2 * (size_t)B * (NB + 1) * 2);
   Bf.xpart = take(2 * (size_t)B * NB);
   Bf.Lpart = take((size_t)B * NB * NL);
   Bf.st = take(2 * (size_t)B * TRF_NS);
@@ -1408,7 +1472,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   // arena that is recycled at each stream synchronisation (a copy still queued reads its own slot); downloads
   // land in pinned arrays read after the synchronisation that follows them.
   TrfHostStage& hs = g_trf_stage;
-  const size_t down_n = (size_t)B * NB * (4 + 2 + TRF_NPF + 4) + 2 * (size_t)B;
+  const size_t down_n = (size_t)B * NB * (4 + TRF_NPF + 4) + (size_t)B * (NB + 1) * 2 + 2 * (size_t)B;
   if (hs.up_cap < TRF_UP_ARENA) {
     if (hs.up) (void)hipHostFree(hs.up);
     hs.up = nullptr;
@@ -1428,8 +1492,8 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   }
   // the partials the host reads: written by the kernels straight into host memory (no copy, no copy kernel)
   double* hf = hs.down;                      // [B][NB][4] eval: sum r^2 at x, at the trial point, rows
-  double* hg = hf + (size_t)B * NB * 4;      // [B][NB][2] J^T f: |g|^2, max |g|
-  double* hn = hg + (size_t)B * NB * 2;      // [B][NB][TRF_NPF] n-space operations
+  double* hg = hf + (size_t)B * NB * 4;      // [B][NBV][2] J^T f: |g|^2, max |g| (NBV <= NB + 1)
+  double* hn = hg + (size_t)B * (NB + 1) * 2;  // [B][NB][TRF_NPF] n-space operations
   double* hj = hn + (size_t)B * NB * TRF_NPF;  // [B][NB][4] J a, J c products
   double* hitn = hj + (size_t)B * NB * 4;    // [B] lsmr iterations
   volatile int* hdone = reinterpret_cast<volatile int*>(hitn + B);  // [B] lsmr's done flags
@@ -1473,6 +1537,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   if (!H2D(act_d, act.data(), sizeof(int) * B)) return -3;
 
   const dim3 grid(NB, B), blk(TRF_THREADS);
+  const dim3 gridj(D.NBV, B);  // J^T launches (with the length variables' workgroup when NBV = NB + 1)
   const size_t jt_lds = trf_jt_lds(D.FB, D.n, D.MR, J, C), l1_lds = trf_l1_lds(D.FB, D.MR, J, C);
   {
     static bool attr = false;
@@ -1508,7 +1573,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     if (hipStreamBeginCapture(dc.cap, hipStreamCaptureModeThreadLocal) != hipSuccess) return -3;
     for (int i = 0; i < chunk; ++i) {
       hipLaunchKernelGGL(trf_lsmr1_kernel<false>, grid, blk, l1_lds, dc.cap, D, Bf, i & 1);
-      hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, dc.cap, D, Bf, i & 1);
+      hipLaunchKernelGGL(trf_jt_kernel<2>, gridj, blk, jt_lds, dc.cap, D, Bf, i & 1);
     }
     if (hipStreamEndCapture(dc.cap, &graph) != hipSuccess) return -3;
     const bool ok = hipGraphInstantiate(&dc.exec, graph, nullptr, nullptr, 0) == hipSuccess;
@@ -1537,7 +1602,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   std::vector<double> cost(B), gnorm2(B), ginf(B), rows(B), xnorm(B), areg(B);
   auto jac_and_grad = [&]() -> bool {
     hipLaunchKernelGGL(trf_eval_kernel, grid, blk, 0, s, D, Bf, x, Bf.fres, 1);
-    hipLaunchKernelGGL(trf_jt_kernel<0>, grid, blk, jt_lds, s, D, Bf, 0);
+    hipLaunchKernelGGL(trf_jt_kernel<0>, gridj, blk, jt_lds, s, D, Bf, 0);
     hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_XNORM);
     hipLaunchKernelGGL(trf_jv_kernel, grid, blk, 0, s, D, Bf, (const double*)Bf.g, (const double*)nullptr);
     if (!sync()) return false;
@@ -1545,9 +1610,12 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
       if (!act[b]) continue;
       cost[b] = 0.5 * sum_field(hf, 4, 0, b);
       rows[b] = sum_field(hf, 4, 2, b);
-      gnorm2[b] = sum_field(hg, 2, 0, b);
-      double m = 0.0;
-      for (int k = 0; k < NB; ++k) m = std::max(m, hg[((size_t)b * NB + k) * 2 + 1]);
+      double gs = 0.0, m = 0.0;
+      for (int k = 0; k < D.NBV; ++k) {
+        gs += hg[((size_t)b * D.NBV + k) * 2];
+        m = std::max(m, hg[((size_t)b * D.NBV + k) * 2 + 1]);
+      }
+      gnorm2[b] = gs;
       ginf[b] = m;
       xnorm[b] = std::sqrt(sum_field(hn, TRF_NPF, 0, b));
       areg[b] = 0.5 * sum_field(hj, 4, 0, b);
@@ -1610,9 +1678,9 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     if (!H2D(done_d, doneh.data(), sizeof(int) * B)) return -3;
     for (int b = 0; b < B; ++b) hdone[b] = doneh[b];  // (no kernel writes it before this iteration's lsmr)
     // lsmr(J, f, damp)
-    hipLaunchKernelGGL(trf_jt_kernel<1>, grid, blk, jt_lds, s, D, Bf, 0);
+    hipLaunchKernelGGL(trf_jt_kernel<1>, gridj, blk, jt_lds, s, D, Bf, 0);
     hipLaunchKernelGGL(trf_lsmr1_kernel<true>, grid, blk, l1_lds, s, D, Bf, 1);
-    hipLaunchKernelGGL(trf_jt_kernel<2>, grid, blk, jt_lds, s, D, Bf, 1);
+    hipLaunchKernelGGL(trf_jt_kernel<2>, gridj, blk, jt_lds, s, D, Bf, 1);
     int k = 2;  // the next iteration; every chunk starts at an even one
     double maxit = 0.0;
     for (int b = 0; b < B; ++b)
