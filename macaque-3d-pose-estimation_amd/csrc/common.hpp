@@ -3,6 +3,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
+// True the first time it is asked for the current device (one bit per device in `seen`): a kernel's function
+// attributes (the dynamic-LDS ceiling) are set once per device, also when one process drives several.
+inline bool first_on_device(std::atomic<unsigned>& seen) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 32) return true;
+  const unsigned bit = 1u << dev;
+  return (seen.fetch_or(bit) & bit) == 0;
+}
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) short short4v;
 typedef __attribute__((ext_vector_type(4))) float f32x4;

@@ -598,11 +598,9 @@ static int g_num_cus = 0;
 
 template <int EPI>
 static void launch256(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<unsigned> attr{0};
+  if (first_on_device(attr))
     (void)hipFuncSetAttribute((const void*)gemm256_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, B2_LDS);
-    attr = true;
-  }
   hipLaunchKernelGGL((gemm256_kernel<EPI>), grid, dim3(B2T), B2_LDS, stream, p, tiles_m, tiles_n);
 }
 

@@ -573,12 +573,10 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
 
 template <int EPI, int MODE, class S>
 void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
-  static bool attr = false;
-  if (!attr) {
+  static std::atomic<unsigned> attr{0};
+  if (first_on_device(attr))
     (void)hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, MODE, S::WMF, S::WNF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
-    attr = true;
-  }
   hipLaunchKernelGGL((gemm_pp_kernel<EPI, MODE, S::WMF, S::WNF>), grid, dim3(PP_T), S::LDS, stream, p, tiles_m, tiles_n);
 }
 

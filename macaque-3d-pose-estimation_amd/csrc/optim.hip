@@ -1632,8 +1632,8 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
     else hipLaunchKernelGGL(optim_factor_lds_kernel<3>, grid, dim3(256), fac_lds_b, s, D, Bf);
   };
   if (use_lds || fac_lds) {
-    static bool attr = false;
-    if (!attr) {
+    static std::atomic<unsigned> attr{0};
+    if (first_on_device(attr)) {
       const int mx = 160 * 1024;
       // (dynamic + static LDS may not exceed the CU's 160 KB, or the call fails and leaves a sticky error;
       // both kernels keep under 1 KB of static LDS)
@@ -1643,7 +1643,6 @@ int optim_points(const double* cams, int C, const double* p2d, double* x, int B,
       (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
       (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
       (void)hipFuncSetAttribute((const void*)optim_factor_lds_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, mx - 512);
-      attr = true;
     }
   }
   auto eval = [&](const double* xx, int mode, double* out) {

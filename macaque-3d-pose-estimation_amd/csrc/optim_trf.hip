@@ -1540,15 +1540,14 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   const dim3 gridj(D.NBV, B);  // J^T launches (with the length variables' workgroup when NBV = NB + 1)
   const size_t jt_lds = trf_jt_lds(D.FB, D.n, D.MR, J, C), l1_lds = trf_l1_lds(D.FB, D.MR, J, C);
   {
-    static bool attr = false;
-    if (!attr) {
+    static std::atomic<unsigned> attr{0};
+    if (first_on_device(attr)) {
       const int mx = (int)TRF_DYN_LDS;
       (void)hipFuncSetAttribute((const void*)trf_jt_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       (void)hipFuncSetAttribute((const void*)trf_jt_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       (void)hipFuncSetAttribute((const void*)trf_jt_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       (void)hipFuncSetAttribute((const void*)trf_lsmr1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       (void)hipFuncSetAttribute((const void*)trf_lsmr1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-      attr = true;
     }
   }
   if (jt_lds > TRF_DYN_LDS || l1_lds > TRF_DYN_LDS) return -2;
