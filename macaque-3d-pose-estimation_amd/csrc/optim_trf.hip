@@ -465,11 +465,11 @@ __device__ __forceinline__ void length_sums(const TrfDims& D, const double* __re
 }
 
 // The length variables, in a workgroup of their own (the last of a J^T launch, blockIdx.x == NB) when the grid
-// leaves a CU for it (D.NBV == NB + 1): v = the sum over the frames of dL * u_len (the per-block sums of the
-// m-space launch: Lpart, or fL for MODE 0 / 1) / beta, minus beta vn in MODE 2; its partials go to slot NB.
-// Done by block 0 alongside its frames, the NB x NL sums make that block, and so the launch, 1.2 us longer
-// (profiles/r05x_*); on a grid that already has more workgroups than CUs an extra one costs more than that
-// (config 4: 4 % slower, profiles/r05z_*), and block 0 keeps them.
+// (for TRF_NOMINAL_B animals) leaves a CU for it (D.NBV == NB + 1): v = the sum over the frames of dL * u_len
+// (the per-block sums of the m-space launch: Lpart, or fL for MODE 0 / 1) / beta, minus beta vn in MODE 2; its
+// partials go to slot NB.  Done by block 0 alongside its frames, the NB x NL sums make that block, and so the
+// launch, 1.2 us longer (profiles/r05x_*); on a grid that already has more workgroups than CUs an extra one
+// costs more than that (config 4: 4 % slower, profiles/r05z_*), and block 0 keeps them.
 template <int MODE>
 __device__ __forceinline__ void jt_lengths(const TrfDims& D, const TrfBufs& Bf, int par, int b, double* red,
                                            double* spart, double* sLs) {
@@ -1342,10 +1342,12 @@ size_t trf_l1_lds(int FB, int MR, int J, int C) {
 constexpr size_t TRF_DYN_LDS = 128 * 1024;  // (the kernels' static LDS stays under 24 KB)
 // Frames per workgroup.  `fit`: the most (<= TRF_FB and the MQ_TUNE_OPTIM_TRF_FB cap) whose rows fit in LDS.  The
 // per-iteration kernels are latency-bound chains, so fewer frames per workgroup shorten each one's chain while
-// the grid still has a CU per workgroup: the smallest count whose grid fits the device's CUs, else `fit`
-// (profiles/r05u_*: 24 frames x 4 animals 8 % faster at 1 frame than at 4; 300 x 4, which fills the CUs
-// at 4, 60 % slower at 1).  Monotonic in `fit`, so the workspace, sized at the deepest smoothing order, never
-// has fewer blocks than a call.
+// the grid still has a CU per workgroup: the smallest count whose grid, for TRF_NOMINAL_B animals, fits the
+// device's CUs, else `fit` (profiles/r05u_*: 24 frames x 4 animals 8 % faster at 1 frame than at 4; 300 x 4,
+// which fills the CUs at 4, 60 % slower at 1).  The choice depends on F, not on the batch, so an animal's
+// result does not depend on which animals share its call (the reductions follow the blocks).  Monotonic in
+// `fit`, so the workspace, sized at the deepest smoothing order, never has fewer blocks than a call.
+constexpr int TRF_NOMINAL_B = 4;  // the reference's four individuals
 static int trf_cu_count() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
@@ -1353,7 +1355,7 @@ static int trf_cu_count() {
     return 256;
   return cus;
 }
-int trf_frames_per_block(int J, int C, int NL, int n, int B, int F) {
+int trf_frames_per_block(int J, int C, int NL, int n, int F) {
   const int MR = (J * C * 2 + J * 3 + NL + 1) & ~1;
   int fit = 1;
   for (int fb = std::min(TRF_FB, std::max(1, g_optim_trf_fb)); fb > 1; --fb)
@@ -1363,13 +1365,13 @@ int trf_frames_per_block(int J, int C, int NL, int n, int B, int F) {
     }
   const long long cus = trf_cu_count();
   for (int fb = 1; fb < fit; ++fb)
-    if ((long long)B * ((F + fb - 1) / fb) <= cus) return fb;
+    if ((long long)TRF_NOMINAL_B * ((F + fb - 1) / fb) <= cus) return fb;
   return fit;
 }
 
 size_t optim_trf_workspace_bytes(int B, int F, int J, int C, int NL) {
   const size_t NV = (size_t)F * J * 3 + NL, MR = ((size_t)J * C * 2 + (size_t)J * 3 + NL + 1) & ~(size_t)1;
-  const int FB = trf_frames_per_block(J, C, NL, TRF_MAXN, B, F);
+  const int FB = trf_frames_per_block(J, C, NL, TRF_MAXN, F);
   const size_t NB = ((size_t)F + FB - 1) / FB;
   size_t n = 0;
   n += (size_t)B * F * MR * 3;           // fres ftr u
@@ -1408,9 +1410,9 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   D.NV = D.NX + NL;
   D.MRrep = J * C * 2;
   D.MR = (D.MRrep + J * 3 + NL + 1) & ~1;  // even: 16-B aligned rows for the LDS staging
-  D.FB = trf_frames_per_block(J, C, NL, n_deriv, B, F);
+  D.FB = trf_frames_per_block(J, C, NL, n_deriv, F);
   D.NB = (F + D.FB - 1) / D.FB;
-  D.NBV = (long long)B * (D.NB + 1) <= trf_cu_count() ? D.NB + 1 : D.NB;
+  D.NBV = (long long)TRF_NOMINAL_B * (D.NB + 1) <= trf_cu_count() ? D.NB + 1 : D.NB;  // (batch-independent too)
   D.rp = rp;
   D.s_len = scale_length;
   D.s_len_weak = scale_length_weak;

@@ -95,10 +95,14 @@ def test_optim_points_loss_and_order_variants(loss, n, solver):
 
 
 @pytest.mark.parametrize("solver", SOLVERS)
-def test_optim_batch_equals_single_and_is_deterministic(solver):
+@pytest.mark.parametrize("F", [20, 100])
+def test_optim_batch_equals_single_and_is_deterministic(solver, F):
+    """An animal's result does not depend on the animals that share its call, bit for bit (the trf solver's
+    frames per workgroup follow F, not the batch: at 100 frames a batch-sized grid would have picked 2 frames
+    per workgroup for 3 animals and 1 for one)."""
     from mqhip.geometry import CameraGroup
     from mqhip.optim import optim_points_batch
-    probs = [_problem(20, seed=s) for s in (3, 4, 5)]
+    probs = [_problem(F, seed=s) for s in (3, 4, 5)]
     cams = probs[0][0]
     g = CameraGroup.from_dicts(cams)
     P2 = np.stack([p[2] for p in probs])
