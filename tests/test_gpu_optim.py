@@ -94,6 +94,15 @@ def test_optim_points_loss_and_order_variants(loss, n, solver):
     _check_against_scipy(24, args=args, loss=loss, solver=solver)
 
 
+@pytest.mark.parametrize("F,n", [(2, 2), (3, 2), (4, 1), (5, 3)])
+def test_optim_points_trf_short_clips(F, n):
+    """Clips shorter than or barely longer than the smoothing order (no or one smoothness row per joint): the trf
+    solver against scipy at the same bounds.  (One frame fails inside the reference's own setup -- numpy's mean
+    of an empty difference -- so it is not a case.)"""
+    args = dict(ARGS, n_deriv_smooth=n)
+    _check_against_scipy(F, args=args, solver="trf")
+
+
 @pytest.mark.parametrize("solver", SOLVERS)
 @pytest.mark.parametrize("F", [20, 100])
 def test_optim_batch_equals_single_and_is_deterministic(solver, F):
