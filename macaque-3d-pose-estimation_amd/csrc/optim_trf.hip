@@ -1317,6 +1317,7 @@ struct TrfHostStage {  // per host thread: pinned staging of optim_points_trf's 
   double* down = nullptr;  // host-mapped, coherent: the partials the host reads, written there by the kernels
   double* down_dev = nullptr;
   size_t down_cap = 0;
+  bool dirty = false;  // a call is using the buffers (set at entry, cleared by a call that completes)
 };
 thread_local TrfHostStage g_trf_stage;
 constexpr int TRF_MAX_DEV = 16;
@@ -1474,6 +1475,10 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   // arena that is recycled at each stream synchronisation (a copy still queued reads its own slot); downloads
   // land in pinned arrays read after the synchronisation that follows them.
   TrfHostStage& hs = g_trf_stage;
+  // (a previous call that failed half way may have left copies from the arena, or kernels writing the host-mapped
+  // partials, in flight on its stream)
+  if (hs.dirty) (void)hipDeviceSynchronize();
+  hs.dirty = true;
   const size_t down_n = (size_t)B * NB * (4 + TRF_NPF + 4) + (size_t)B * (NB + 1) * 2 + 2 * (size_t)B;
   if (hs.up_cap < TRF_UP_ARENA) {
     if (hs.up) (void)hipHostFree(hs.up);
@@ -1809,6 +1814,7 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   }
 #endif
   if (!sync()) return -3;  // (the staging arena is the next call's)
+  hs.dirty = false;
   for (int b = 0; b < B; ++b) {
     stats[8 * b + 1] = cost[b];
     stats[8 * b + 2] = (double)(njev[b] - 1);
