@@ -501,12 +501,13 @@ def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
                     "box selection and trackers at thresholds 0)"}
 
 
-def clip_lift(kp, cams_np, device, clips=1):
+def clip_lift(kp, cams_np, device, clips=1, rank=0, world=1):
     """The step-4 lift (Viterbi 2D filter, DLT triangulation, optim_points, reprojection errors; the
     default config_tmpl.toml path) of the keypoints every rank produced in the timed region, gathered in
-    frame order: kp (F, C, A, J, 3) -> wall seconds on rank 0 (BASELINE config 3's last stage).  Each
-    rank's frames are its own synthetic sequence, so the gathered frames are lifted as `clips` clips (one
-    per rank), batched as clips x A individuals in one solve."""
+    frame order: kp (F, C, A, J, 3) -> wall seconds (BASELINE config 3's last stage).  Each rank's frames are
+    its own synthetic sequence, so the gathered frames are `clips` clips (one per rank) of A individuals; as in
+    step4_aniposefiltering.proc on a sharded run, rank r lifts the individuals i = r (mod world) of the
+    clips x A, batched in one solve (every rank holds the gathered keypoints; the caller takes the max)."""
     import numpy as np
     import torch
     from mqhip import io as mqio
@@ -515,6 +516,7 @@ def clip_lift(kp, cams_np, device, clips=1):
     Ft, C, A = kp.shape[:3]
     kp = kp.reshape((clips, Ft // clips) + kp.shape[1:])                         # (clips, F, C, A, J, 3)
     kp2d = np.ascontiguousarray(kp.transpose(0, 3, 1, 2, 4, 5).reshape((clips * A, Ft // clips) + kp.shape[2:3] + kp.shape[4:])).astype(np.float64)   # (clips*A, F, C, J, 3)
+    kp2d = np.ascontiguousarray(kp2d[rank::world])
     config = mqio.load_toml(CONFIG_TMPL)
     cg = CameraGroup.from_dicts(cams_np, device=device)
     torch.cuda.synchronize(device)
@@ -525,12 +527,13 @@ def clip_lift(kp, cams_np, device, clips=1):
     torch.cuda.synchronize(device)
     t2 = time.perf_counter()
     A2, F = kp2d.shape[:2]
-    return {"frames": int(F), "clips": int(clips), "individuals": int(A2 // clips), "ms": round((t2 - t0) * 1e3, 3),
+    return {"frames": int(F), "clips": int(clips), "individuals": int(A * clips), "individuals_per_rank": int(A2),
+            "ms": round((t2 - t0) * 1e3, 3),
             "viterbi_ms": round((t1 - t0) * 1e3, 3), "triangulate_optim_ms": round((t2 - t1) * 1e3, 3),
             "finite_3d_fraction": round(float(np.isfinite(kp3d).mean()), 4),
             "what": "step 4 (config_tmpl.toml: Viterbi filter, DLT, optim_points, reprojection errors) on the 2D "
-                    "keypoints of every frame of the timed region, gathered from all ranks (one clip per rank, "
-                    "lifted together), run on rank 0"}
+                    "keypoints of every frame of the timed region, gathered from all ranks (one clip per rank); "
+                    "the individuals split over the ranks (i = rank mod world), ms = the slowest rank"}
 
 
 class Pipeline:
@@ -809,12 +812,18 @@ def main():
         "roofline": roof,
     }
     log(f"timed region {dt:.3f} s")
-    if rank == 0 and not args.no_lift:
-        # BASELINE config 3's last stage: the clip lift of every frame the ranks just processed (rank 0)
-        cl = clip_lift(gathered.cpu().numpy(), cams_np, local, clips=world)
-        cl["value_with_lift"] = round(frames_done * N_ANIMALS / (dt + cl["ms"] * 1e-3), 3)
-        result["clip_lift"] = cl
-        log(f"clip lift of {cl['frames']} gathered frames: {cl['ms']:.1f} ms")
+    if not args.no_lift:
+        # BASELINE config 3's last stage: the clip lift of every frame the ranks just processed, its individuals
+        # split over the ranks as in run_demo's sharded step 4; the slowest rank's time
+        cl = clip_lift(gathered.cpu().numpy(), cams_np, local, clips=world, rank=rank, world=world)
+        if dist_on:
+            t = torch.tensor([cl["ms"]], device=xdev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            cl["ms"] = round(float(t.item()), 3)
+        if rank == 0:
+            cl["value_with_lift"] = round(frames_done * N_ANIMALS / (dt + cl["ms"] * 1e-3), 3)
+            result["clip_lift"] = cl
+            log(f"clip lift of {cl['frames']} gathered frames: {cl['ms']:.1f} ms")
     if extras:
         # steady state: the same step back to back for >= 3 s (the driver's utilisation sampler needs more than
         # the short timed region to see the GPU busy; the chip's clock under sustained load is what it reports)

@@ -17,8 +17,9 @@ This build runs the same chain on MI355X with the parts outside its scope replac
 
 Multi-GPU (BASELINE config 3): run one process per GPU under ``torch.distributed.run``; every rank
 calls ``proc(..., world=W, rank=r, group=g)``.  Step 1's time steps are sharded over the ranks with
-one all-gather of the 2D keypoints (RCCL over xGMI), and rank 0 runs steps 3-4 on the gathered clip
-(``step4`` couples all frames of an animal, so it is not sharded).  The files and kp3d equal the
+one all-gather of the 2D keypoints (RCCL over xGMI); rank 0 runs step 3, and step 4 runs on every rank for
+its individuals (individual a on rank a mod world -- step 4 couples the frames of an individual, not the
+individuals), whose results one object all-gather brings to rank 0.  The files and kp3d equal the
 single-process run bit for bit (tests/test_gpu_config3.py).
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29500 \\
@@ -42,9 +43,10 @@ def proc(data_name, fps, results_dir_root, device_str, config_path, raw_data_dir
     Steps 3-4 take step 1's rows in memory (the files are still written, by a background thread joined
     before returning).  On a sharded run (``world`` > 1 or ``sharded``) rank r post-processes and writes
     the cameras c = r (mod world) and assembles their kp2d slices; one all-gather of the slices gives
-    rank 0 step 3's array, and rank 0 alone writes kp2d.pickle and runs step 4 (Viterbi, DLT / RANSAC,
-    optim_points: tens of ms of GPU work for a 300-frame clip).  When step 1 had nothing to do (files
-    present) steps 3-4 read the files, as the reference does."""
+    every rank step 3's array; rank 0 writes kp2d.pickle, every rank runs step 4 (Viterbi, DLT / RANSAC,
+    optim_points: tens of ms of GPU work for a 300-frame clip) for the individuals a = r (mod world), and
+    rank 0 assembles and writes step 4's files.  When step 1 had nothing to do (files present) steps 3-4
+    read the files on rank 0, as the reference does."""
     import time
     device = int(device_str.split(':')[1]) if ':' in device_str else 0
     t0 = time.perf_counter()
@@ -66,7 +68,10 @@ def proc(data_name, fps, results_dir_root, device_str, config_path, raw_data_dir
             if s1out is not None:
                 s1out.wait()
             _barrier(group)
-        if rank != 0:
+        # step 4 over the ranks (individual a on rank a mod world, the results assembled on rank 0) when every
+        # rank holds the gathered keypoints; the file path (kp2d None) runs it on rank 0 alone
+        split = sharded_run and kp2d is not None and world > 1
+        if rank != 0 and not split:
             return None
         result_dir = os.path.join(results_dir_root, data_name)
         if kp2d is None:
@@ -74,12 +79,13 @@ def proc(data_name, fps, results_dir_root, device_str, config_path, raw_data_dir
                 s1out.wait()               # the files are the input of the file path
             kp2d = step3.proc_known_assignment(data_name, results_dir_root, config_path, n_animal=n_animal,
                                                n_kp=n_kp, track_to_animal=track_to_animal)
-        else:
+        elif rank == 0:
             from mqhip import io as mqio
             os.makedirs(result_dir, exist_ok=True)
             mqio.dump_pickle(kp2d, os.path.join(result_dir, "kp2d.pickle"))
         t3 = time.perf_counter()
-        out = step4.proc(data_name, results_dir_root, config_path, n_kp, redo=True, device=device, kp2d=kp2d)
+        out = step4.proc(data_name, results_dir_root, config_path, n_kp, redo=True, device=device, kp2d=kp2d,
+                         world=world if split else 1, rank=rank if split else 0, group=group if split else None)
         t4 = time.perf_counter()
     finally:
         if s1out is not None:

@@ -10,8 +10,12 @@ and the same numbers, but batched MI355X-first:
   (reference: a spawn pool per animal x camera, step4:145-167);
 * initial triangulation / RANSAC / reprojection errors run over all animals'
   points in one launch each (reference: per animal, per point);
-* optim_points refines all animals in one batched LM solve (reference: scipy
-  per animal).
+* optim_points refines all animals in one batched solve (reference: scipy
+  per animal);
+* on a sharded run (``world`` > 1, every rank holding the gathered kp2d) the
+  individuals are split over the ranks (individual a on rank a mod world) and
+  rank 0 assembles and writes the outputs: the same bits as one rank, since
+  every stage is independent per individual.
 
 Calibration: if the reference's ``cam_intrinsic.h5`` / ``cam_extrinsic_optim.h5``
 sit next to ``config_path`` and h5py is importable, ``calibration.toml`` is
@@ -135,12 +139,15 @@ def filter_2d(kp2d, filter_config=FILTER_CONFIG, device: int = 0):
     return np.ascontiguousarray(out.transpose(1, 3, 0, 4, 2))
 
 
-def reconstruct_3d(kp2d_f, cgroup, config, bodyparts=BODYPARTS, joint_len_median=None, verbose=False):
+def reconstruct_3d(kp2d_f, cgroup, config, bodyparts=BODYPARTS, joint_len_median=None, verbose=False,
+                   return_run=False):
     """step4:185-331 for all animals at once.  kp2d_f (F,J,A,3,C) ->
-    (kp3d (A,F,J,3), S (A,F,J), E (A,F,J), joint_len list)."""
+    (kp3d (A,F,J,3), S (A,F,J), E (A,F,J), joint_len list (one entry per refined animal, in animal order)
+    [, the refined animals when ``return_run``])."""
     tri = config['triangulation']
     n_frame, n_kp, n_animal, _, n_cam = kp2d_f.shape
     kp = np.array(kp2d_f.transpose((2, 4, 0, 1, 3)), dtype=np.float64)   # (A,C,F,J,3)
+    run = []
     pts_raw = kp[..., :2].copy()
     scores = kp[..., 2].copy()
     pts_raw[scores < tri['score_threshold']] = np.nan
@@ -208,38 +215,55 @@ def reconstruct_3d(kp2d_f, cgroup, config, bodyparts=BODYPARTS, joint_len_median
             kp3d[a] = p3[a]
         S[a] = s3[a]
         E[a] = err[a]
+    if return_run:
+        return kp3d, S, E, joint_len, run
     return kp3d, S, E, joint_len
 
 
-def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int = 0, verbose=False, kp2d=None):
+def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int = 0, verbose=False, kp2d=None,
+         world=1, rank=0, group=None):
     """step4_aniposefiltering.proc (step4:89).  ``kp2d``: step 3's (A, F, C, J, 3) array in memory (as
-    written to kp2d.pickle) instead of reading the file back."""
+    written to kp2d.pickle) instead of reading the file back.
+
+    ``world`` > 1 (every rank calls this with the same gathered ``kp2d``): rank r filters and lifts the
+    individuals a with a % world == r, one object all-gather brings their results to rank 0, which writes the
+    files and returns the data (None elsewhere).  Rank 0 writes config.toml / calibration.toml before the other
+    ranks read them (a barrier)."""
     result_dir = results_dir_root + '/' + data_name
     fixed = os.path.exists(os.path.dirname(config_path) + '/joint_len.npy')
     out_name = 'kp3d_fxdJointLen.pickle' if fixed else 'kp3d.pickle'
+    split = world > 1
+    if split and kp2d is None:
+        raise ValueError("step4.proc: a sharded run needs the gathered kp2d in memory on every rank")
     if os.path.exists(os.path.join(result_dir, out_name)) and not redo:
         print(f'Skip as exist:{data_name:s}/{out_name}')
         return
 
     # ---- configuration + calibration (step4:101-138)
-    config = mqio.load_toml(CONFIG_TMPL)
-    config['model_folder'] = os.path.abspath(os.path.dirname(result_dir))
-    mqio.dump_toml(config, result_dir + '/config.toml')
     with open(config_path, 'r') as f:
         cam_ids = [str(i) for i in yaml.safe_load(f)['camera_id']]
-    h5_in = os.path.dirname(config_path) + '/cam_intrinsic.h5'
-    if os.path.exists(h5_in):
-        write_calibration(config_path, result_dir, cam_ids)
-    elif not os.path.exists(result_dir + '/calibration.toml'):
-        raise FileNotFoundError(f'need {h5_in} (+ h5py) or {result_dir}/calibration.toml')
+    if rank == 0:
+        config = mqio.load_toml(CONFIG_TMPL)
+        config['model_folder'] = os.path.abspath(os.path.dirname(result_dir))
+        mqio.dump_toml(config, result_dir + '/config.toml')
+        h5_in = os.path.dirname(config_path) + '/cam_intrinsic.h5'
+        if os.path.exists(h5_in):
+            write_calibration(config_path, result_dir, cam_ids)
+        elif not os.path.exists(result_dir + '/calibration.toml'):
+            raise FileNotFoundError(f'need {h5_in} (+ h5py) or {result_dir}/calibration.toml')
+    if split:
+        _barrier(group)
 
     # ---- 2D filtering (step4:140-170)
     print('##### 2D filtering....', flush=True)
     if kp2d is None:
         kp2d = mqio.load_array_pickle(result_dir + '/kp2d.pickle')
     kp2d = np.asarray(kp2d, dtype=np.float64)
-    kp2d_f = filter_2d(kp2d, device=device)
-    mqio.dump_pickle(kp2d_f, result_dir + '/kp2d_f.pickle')
+    n_animal = kp2d.shape[0]
+    mine = [a for a in range(n_animal) if a % world == rank] if split else list(range(n_animal))
+    kp2d_f = filter_2d(kp2d[mine], device=device) if mine else None
+    if not split:
+        mqio.dump_pickle(kp2d_f, result_dir + '/kp2d_f.pickle')
 
     # ---- 3D reconstruction (step4:172-339)
     print('##### 3D reconstruction....', flush=True)
@@ -247,11 +271,64 @@ def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int
     if fixed:
         joint_len_median = np.median(np.load(os.path.dirname(config_path) + '/joint_len.npy'), axis=0)
     config = mqio.load_toml(result_dir + '/config.toml')
-    cgroup = CameraGroup.load(result_dir + '/calibration.toml', device=device).subset_cameras_names(cam_ids)
-    kp3d, S, E, joint_len = reconstruct_3d(kp2d_f, cgroup, config, joint_len_median=joint_len_median,
-                                           verbose=verbose)
+    part = None
+    if mine:
+        cgroup = CameraGroup.load(result_dir + '/calibration.toml', device=device).subset_cameras_names(cam_ids)
+        if split:
+            kp3d, S, E, joint_len, run = reconstruct_3d(kp2d_f, cgroup, config, joint_len_median=joint_len_median,
+                                                        verbose=verbose, return_run=True)
+            part = (mine, kp2d_f, kp3d, S, E, joint_len, [mine[i] for i in run])
+        else:
+            kp3d, S, E, joint_len = reconstruct_3d(kp2d_f, cgroup, config, joint_len_median=joint_len_median,
+                                                   verbose=verbose)
+    if split:
+        parts = _gather_objects(part, world, group)
+        if rank != 0:
+            return None
+        kp2d_f, kp3d, S, E, joint_len = _assemble(parts, n_animal)
+        if joint_len_median is not None:   # as one rank builds it: the fixed lengths, once per refined individual
+            jl_fix = np.asarray(joint_len_median, dtype=np.float64)
+            joint_len = [jl_fix for _ in joint_len]
+        mqio.dump_pickle(kp2d_f, result_dir + '/kp2d_f.pickle')
     if config['triangulation']['optim']:
         np.save(result_dir + '/joint_len.npy', np.array(joint_len))
     data = {'kp3d': kp3d, 'kp3d_score': S, 'kp3d_err': E, 'joint_len': joint_len}
     mqio.dump_pickle(data, os.path.join(result_dir, out_name))
     return data
+
+
+def _barrier(group):
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier(group=group)
+
+
+def _gather_objects(obj, world, group):
+    """Every rank's part (or None) on every rank, in rank order (torch.distributed.all_gather_object: pickled
+    numpy arrays; over RCCL the bytes travel as device tensors)."""
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj, group=group)
+    return out
+
+
+def _assemble(parts, n_animal):
+    """Rank 0: the ranks' per-individual results back in individual order -- kp2d_f (F,J,A,3,C), kp3d / S / E
+    (A,...) and joint_len (one entry per refined individual, in individual order, as one rank produces it)."""
+    first = next(p for p in parts if p is not None)
+    kf0, k0, s0, e0 = first[1], first[2], first[3], first[4]
+    kp2d_f = np.zeros(kf0.shape[:2] + (n_animal,) + kf0.shape[3:], dtype=kf0.dtype)
+    kp3d = np.zeros((n_animal,) + k0.shape[1:], dtype=k0.dtype)
+    S = np.zeros((n_animal,) + s0.shape[1:], dtype=s0.dtype)
+    E = np.zeros((n_animal,) + e0.shape[1:], dtype=e0.dtype)
+    jl = {}
+    for p in parts:
+        if p is None:
+            continue
+        mine, kf, k3, s3, e3, joint_len, run = p
+        for i, a in enumerate(mine):
+            kp2d_f[:, :, a] = kf[:, :, i]
+            kp3d[a], S[a], E[a] = k3[i], s3[i], e3[i]
+        for a, j in zip(run, joint_len):
+            jl[a] = np.array(j, dtype=np.float64)
+    return kp2d_f, kp3d, S, E, [jl[a] for a in sorted(jl)]

@@ -192,9 +192,37 @@ def test_sharded_tail_world2_equals_single_rank_files(tmp_path):
             assert a == b, (cam, name)
 
 
+def _fake_filter_2d(kp2d, filter_config=None, device=0):
+    """CPU stand-in for step 4's Viterbi filter: the (A,F,C,J,3) -> (F,J,A,3,C) layout, per individual."""
+    return np.ascontiguousarray(np.asarray(kp2d).transpose(1, 3, 0, 4, 2))
+
+
+def _fake_reconstruct_3d(kp2d_f, cgroup, config, bodyparts=None, joint_len_median=None, verbose=False,
+                         return_run=False):
+    """CPU stand-in for step 4's lift (the GPU part): a deterministic function of each individual's own 2D, with
+    `run` (the refined individuals) depending on the data, so the split / assembly is exercised as on the GPU."""
+    kp = np.asarray(kp2d_f).transpose(2, 4, 0, 1, 3)                     # (A, C, F, J, 3)
+    kp3d = kp.mean(axis=1)
+    S = kp[..., 2].min(axis=1)
+    E = kp[..., 0].std(axis=1)
+    run = [a for a in range(kp.shape[0]) if np.nansum(np.abs(kp3d[a])) > 0]
+    jl = [kp3d[a].reshape(-1)[:5].copy() for a in run]
+    return (kp3d, S, E, jl, run) if return_run else (kp3d, S, E, jl)
+
+
+class _FakeCameraGroup:
+    @staticmethod
+    def load(path, device=0):
+        return _FakeCameraGroup()
+
+    def subset_cameras_names(self, names):
+        return self
+
+
 def _demo_worker(rank, world, port, raw, res, cfg, fps, slow_rank, q):
-    """run_demo.proc on one gloo rank with the fake pose model; step 4 is replaced by a probe that returns
-    the kp2d array it would lift (the GPU part; its input is what the sharding must get right)."""
+    """run_demo.proc on one gloo rank with the fake pose model.  Step 4 runs for real -- its split of the
+    individuals over the ranks, the object all-gather and rank 0's assembly and files -- with its GPU stages
+    (Viterbi filter, lift, camera loading) replaced by deterministic per-individual CPU stand-ins."""
     import sys
     import time
     from types import SimpleNamespace
@@ -207,9 +235,12 @@ def _demo_worker(rank, world, port, raw, res, cfg, fps, slow_rank, q):
     from src.pipeline import step1_proc2d as s1
     from src.pipeline import step4_aniposefiltering as step4
     s1.inference_topdown_batch = fake_pose_batch
-    step4.proc = lambda data_name, results_dir_root, config_path, n_kp, redo=True, device=0, kp2d=None: (
-        kp2d if kp2d is not None else __import__("mqhip.io", fromlist=["load_pickle"]).load_pickle(
-            os.path.join(results_dir_root, data_name, "kp2d.pickle")))
+    step4.filter_2d = _fake_filter_2d
+    step4.reconstruct_3d = _fake_reconstruct_3d
+    step4.CameraGroup = _FakeCameraGroup
+    if rank == 0:                  # (step 4 needs a calibration.toml when there is no cam_intrinsic.h5)
+        os.makedirs(os.path.join(res, "demo"), exist_ok=True)
+        open(os.path.join(res, "demo", "calibration.toml"), "w").close()
     if rank == slow_rank:          # a slow writer: rank 0 must not read the files before it has finished
         orig = s1._write_step1_files
 
@@ -264,11 +295,27 @@ def _files(res, n_cams):
             for c in range(n_cams) for n in ("alldata.json", "frame_num.npy")}
 
 
+def _same_step4(a, b):
+    assert sorted(a) == sorted(b)
+    for k in ("kp3d", "kp3d_score", "kp3d_err"):
+        np.testing.assert_array_equal(a[k], b[k])
+    assert len(a["joint_len"]) == len(b["joint_len"])
+    for x, y in zip(a["joint_len"], b["joint_len"]):
+        np.testing.assert_array_equal(x, y)
+
+
+def _step4_files(res):
+    """Step 4's files (config.toml differs by the results path it records; kp3d.pickle is compared loaded, by
+    _same_step4: its bytes also encode which arrays share a dtype object)."""
+    return {n: open(os.path.join(res, "demo", n), "rb").read() for n in ("kp2d.pickle", "kp2d_f.pickle", "joint_len.npy")}
+
+
 def test_run_demo_world8_config3_equals_single_rank(tmp_path):
     """the whole config-3 sharded path at world 8 (gloo, CPU): a 300-step clip split by
     frame_block(300, 8) (38 / 37 steps) through pose_clip_sharded, 3 cameras so ranks 3-7 own no camera
-    (camera_shard / gather_cameras with empty parts), rank 0's kp2d.pickle and step-4 input.  Bit for bit the
-    single-rank run: rank 0's step-4 input, kp2d.pickle and every alldata.json / frame_num.npy."""
+    (camera_shard / gather_cameras with empty parts), then step 4 split by individual (2 individuals: ranks 2-7
+    own none) and assembled on rank 0.  Bit for bit the single-rank run: rank 0's step-4 data, every step-4 file,
+    kp2d.pickle and every alldata.json / frame_num.npy."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from mqhip.shard import camera_shard, frame_block
@@ -278,12 +325,12 @@ def test_run_demo_world8_config3_equals_single_rank(tmp_path):
     ref = _run_demo_ranks(1, raw, str(tmp_path / "res1"), cfg, fps)[0][1]
     got = _run_demo_ranks(8, raw, str(tmp_path / "res8"), cfg, fps)
     assert got[0][1] is not None and all(out is None for _, out, _ in got[1:])
-    np.testing.assert_array_equal(got[0][1], ref)
-    assert np.abs(ref[..., 2]).sum() > 0
+    _same_step4(got[0][1], ref)
+    assert np.nansum(np.abs(ref["kp3d"])) > 0 and len(ref["joint_len"]) == 2
     assert _files(str(tmp_path / "res1"), 3) == _files(str(tmp_path / "res8"), 3)
-    a = open(os.path.join(tmp_path, "res1", "demo", "kp2d.pickle"), "rb").read()
-    b = open(os.path.join(tmp_path, "res8", "demo", "kp2d.pickle"), "rb").read()
-    assert a == b
+    assert _step4_files(str(tmp_path / "res1")) == _step4_files(str(tmp_path / "res8"))
+    from mqhip import io as mqio
+    _same_step4(mqio.load_array_pickle(os.path.join(tmp_path, "res8", "demo", "kp3d.pickle")), ref)
     assert "after_gather_s" in got[0][2]
 
 
@@ -301,6 +348,6 @@ def test_run_demo_world2_file_path_waits_for_every_writer(tmp_path):
     (res / "demo").mkdir(parents=True)
     shutil.copytree(tmp_path / "res1" / "demo" / "1001", res / "demo" / "1001")   # one camera already done
     got = _run_demo_ranks(2, raw, str(res), cfg, fps, slow_rank=1)
-    np.testing.assert_array_equal(got[0][1], ref)
+    _same_step4(got[0][1], ref)
     assert got[1][1] is None
     assert _files(str(tmp_path / "res1"), 3) == _files(str(res), 3)
