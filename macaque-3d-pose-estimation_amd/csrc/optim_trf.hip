@@ -1603,14 +1603,30 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     for (int k = 0; k < NB; ++k) v += p[((size_t)b * NB + k) * stride + field];
     return v;
   };
-  // At an accepted x, for the animals in act, with one synchronisation: J, f, cost (mode 1), g = J^T f with its
-  // norms, |x|, and J g (the next iteration's `regularize`)
+  // At a point p (x, or a trial point), for the animals in act: J, f, cost (mode 1), g = J^T f with its norms,
+  // |p|, and J g (the next iteration's `regularize`).  Launched, then read after the next synchronisation.
   std::vector<double> cost(B), gnorm2(B), ginf(B), rows(B), xnorm(B), areg(B);
-  auto jac_and_grad = [&]() -> bool {
-    hipLaunchKernelGGL(trf_eval_kernel, grid, blk, 0, s, D, Bf, x, Bf.fres, 1);
+  auto launch_jac = [&](double* p) {
+    hipLaunchKernelGGL(trf_eval_kernel, grid, blk, 0, s, D, Bf, p, Bf.fres, 1);
     hipLaunchKernelGGL(trf_jt_kernel<0>, gridj, blk, jt_lds, s, D, Bf, 0);
-    hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_XNORM);
+    hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, p, xt, (int)OP_XNORM);
     hipLaunchKernelGGL(trf_jv_kernel, grid, blk, 0, s, D, Bf, (const double*)Bf.g, (const double*)nullptr);
+  };
+  auto read_jac = [&](int b) {
+    cost[b] = 0.5 * sum_field(hf, 4, 0, b);
+    rows[b] = sum_field(hf, 4, 2, b);
+    double gs = 0.0, m = 0.0;
+    for (int k = 0; k < D.NBV; ++k) {
+      gs += hg[((size_t)b * D.NBV + k) * 2];
+      m = std::max(m, hg[((size_t)b * D.NBV + k) * 2 + 1]);
+    }
+    gnorm2[b] = gs;
+    ginf[b] = m;
+    xnorm[b] = std::sqrt(sum_field(hn, TRF_NPF, 0, b));
+    areg[b] = 0.5 * sum_field(hj, 4, 0, b);
+  };
+  auto jac_and_grad = [&]() -> bool {
+    launch_jac(x);
     if (!sync()) return false;
     for (int b = 0; b < B; ++b) {
       if (!act[b]) continue;
@@ -1749,14 +1765,17 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
       if (!upload_act()) return -3;
       if (!H2D(Bf.coef, coef.data(), sizeof(double) * coef.size())) return -3;
       hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_STEP);
-      hipLaunchKernelGGL(trf_eval_kernel, grid, blk, 0, s, D, Bf, xt, Bf.ftr, 0);
+      // the residuals at the trial point with the Jacobian, g, |xt| and J g there, on the bet that the step is
+      // accepted (it mostly is): an accepted step then needs no further evaluation or synchronisation.  A
+      // rejected one loses nothing the next trial needs (that uses x, s1, s2 and the host's B_S, g_S).
+      launch_jac(xt);
       if (!sync()) return -3;
       for (int b = 0; b < B; ++b) {
         if (!act[b]) continue;
         nfev[b]++;
         const double sh = std::sqrt(sum_field(hn, TRF_NPF, 5, b));
         step_norm[b] = sh;
-        const double cn = 0.5 * sum_field(hf, 4, 1, b);
+        const double cn = 0.5 * sum_field(hf, 4, 0, b);
         if (!std::isfinite(cn)) {
           Delta[b] = 0.25 * sh;
           actual[b] = -1;
@@ -1782,23 +1801,18 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
         Delta[b] = Dn;
       }
     }
-    // accepted steps: x = x_new, J at x (trf.py:522-540)
+    // accepted steps: x = x_new, with J, g, |x| and J g at x as the last trial evaluated them (trf.py:522-540)
     bool anya = false;
     for (int b = 0; b < B; ++b) {
       act[b] = state[b] == RUN && actual[b] > 0;
       if (!act[b]) continue;
       anya = true;
-      cost[b] = cost_new[b];
       njev[b]++;
+      read_jac(b);  // (the partials of the animal's last trial: it stopped trying at its accepted step)
     }
     if (anya) {
       if (!upload_act()) return -3;
       hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_ACCEPT);
-      // the Jacobian of a terminating animal is not needed (scipy evaluates it, njev counts it)
-      for (int b = 0; b < B; ++b)
-        if (act[b] && status[b] != 0) act[b] = 0;
-      if (!upload_act()) return -3;
-      if (!jac_and_grad()) return -3;
     }
   }
 #ifdef TRF_PROFILE
