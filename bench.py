@@ -788,7 +788,9 @@ def main():
                 "kernel": "%s (FFN fc1, M=%d N=%d K=%d)" % (
                     "gemm_pp_kernel<EPI_GELU_BF16>" if lib.mq_get_tuning(12) == 1 else "gemm256_kernel<EPI_GELU_BF16>",
                     2 * n * cfg.tokens, cfg.ffn, cfg.embed_dims),
-                "flops_per_launch": fl.value, "avg_launch_ms": round(avg_ms.value, 5), "launches": cnt.value}
+                "flops_per_launch": fl.value, "avg_launch_ms": round(avg_ms.value, 5), "launches": cnt.value,
+                "launches_timed": "fc1 of layers 7, 15, 23, 31 in every timed step (HIP event pairs on the forward's "
+                                  "stream; each pair idles the GPU ~4 us on either side of its launch)"}
 
     frames_done = world * args.steps * FPS
     value = frames_done * N_ANIMALS / dt
