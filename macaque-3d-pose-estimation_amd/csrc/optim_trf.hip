@@ -1568,8 +1568,11 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= TRF_MAX_DEV) return -3;
   TrfDevCache& dc = g_trf_dev[dev];
   if (!dc.cap && hipStreamCreateWithFlags(&dc.cap, hipStreamNonBlocking) != hipSuccess) return -3;
+  // (the polling events order nothing but the host's read of the done flags, which a stale read only delays by a
+  // chunk: no system-scope cache fence at each chunk boundary)
   for (auto& e : dc.ev)
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return -3;
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+      return -3;
   hipEvent_t* done_ev = dc.ev;
   if (!dc.exec || dc.chunk != chunk || dc.jt_lds != jt_lds || dc.l1_lds != l1_lds ||
       std::memcmp(&dc.D, &D, sizeof(D)) != 0 || std::memcmp(&dc.Bf, &Bf, sizeof(Bf)) != 0) {
