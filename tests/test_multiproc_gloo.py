@@ -219,7 +219,7 @@ class _FakeCameraGroup:
         return self
 
 
-def _demo_worker(rank, world, port, raw, res, cfg, fps, slow_rank, q):
+def _demo_worker(rank, world, port, raw, res, cfg, fps, slow_rank, q, n_animal=2):
     """run_demo.proc on one gloo rank with the fake pose model.  Step 4 runs for real -- its split of the
     individuals over the ranks, the object all-gather and rank 0's assembly and files -- with its GPU stages
     (Viterbi filter, lift, camera loading) replaced by deterministic per-individual CPU stand-ins."""
@@ -254,7 +254,7 @@ def _demo_worker(rank, world, port, raw, res, cfg, fps, slow_rank, q):
     try:
         stub = SimpleNamespace(cfg=SimpleNamespace(n_joints=17))
         tm = {}
-        out = run_demo.proc("demo", fps, res, "cuda:0", cfg, raw, 17, n_animal=2, pose_model=stub, id_model=None,
+        out = run_demo.proc("demo", fps, res, "cuda:0", cfg, raw, 17, n_animal=n_animal, pose_model=stub, id_model=None,
                             world=world, rank=rank, timings=tm)
         q.put((rank, out, sorted(tm)))
     finally:
@@ -263,11 +263,11 @@ def _demo_worker(rank, world, port, raw, res, cfg, fps, slow_rank, q):
             dist.destroy_process_group()
 
 
-def _run_demo_ranks(world, raw, res, cfg, fps, slow_rank=-1):
+def _run_demo_ranks(world, raw, res, cfg, fps, slow_rank=-1, n_animal=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_demo_worker, args=(r, world, port, raw, res, cfg, fps, slow_rank, q))
+    procs = [ctx.Process(target=_demo_worker, args=(r, world, port, raw, res, cfg, fps, slow_rank, q, n_animal))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -351,3 +351,18 @@ def test_run_demo_world2_file_path_waits_for_every_writer(tmp_path):
     _same_step4(got[0][1], ref)
     assert got[1][1] is None
     assert _files(str(tmp_path / "res1"), 3) == _files(str(res), 3)
+
+
+def test_run_demo_world3_uneven_step4_split(tmp_path):
+    """Step 4 split unevenly: 4 individuals over 3 ranks (individuals 0 and 3 on rank 0), two of them without a
+    track (nothing to lift, so outside the refined set whose joint lengths are listed): rank 0's assembled data
+    and step-4 files equal the single-rank run's."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    raw, cfg, fps, _ = _demo_inputs(tmp_path, 3, 23)
+    ref = _run_demo_ranks(1, raw, str(tmp_path / "res1"), cfg, fps, n_animal=4)[0][1]
+    got = _run_demo_ranks(3, raw, str(tmp_path / "res3"), cfg, fps, n_animal=4)
+    assert got[0][1] is not None and got[1][1] is None and got[2][1] is None
+    _same_step4(got[0][1], ref)
+    assert ref["kp3d"].shape[0] == 4 and len(ref["joint_len"]) == 2
+    assert _step4_files(str(tmp_path / "res1")) == _step4_files(str(tmp_path / "res3"))
