@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cmath>
 #include <cstring>
+#include <initializer_list>
 #include <limits>
 #include <vector>
 
@@ -1456,13 +1457,16 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
   Bf.xpart = take(2 * (size_t)B * NB);
   Bf.Lpart = take((size_t)B * NB * NL);
   Bf.st = take(2 * (size_t)B * TRF_NS);
-  Bf.lctl = take(4 * (size_t)B);
-  Bf.coef = take(4 * (size_t)B);
+  // the host-written inputs, one contiguous run in upload order, so that each group of them the driver sends
+  // together (call setup; lsmr setup: lctl, done, act; a trial: act, coef) is one copy
   int* cons_d = reinterpret_cast<int*>(take(((size_t)NL * 2 + 1) / 2 + 1));
   int* jadj_d = reinterpret_cast<int*>(take(((size_t)J + 1 + 2 * (size_t)NL) / 2 + 1));
-  int* act_d = reinterpret_cast<int*>(take(((size_t)B + 1) / 2 + 1));
-  int* done_d = reinterpret_cast<int*>(take(((size_t)B + 1) / 2 + 1));
   double* ssf_d = take(B);
+  Bf.lctl = take(4 * (size_t)B);
+  int* done_d = reinterpret_cast<int*>(take(((size_t)B + 1) / 2 + 1));
+  int* act_d = reinterpret_cast<int*>(take(((size_t)B + 1) / 2 + 1));
+  Bf.coef = take(4 * (size_t)B);
+  char* const ctl_end = reinterpret_cast<char*>(w);
   Bf.cams = cams;
   Bf.p2d = p2d;
   Bf.cons = cons_d;
@@ -1526,7 +1530,23 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     hs.up_off += (bytes + 255) & ~(size_t)255;
     return hipMemcpyAsync(d, st, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
   };
-  if (NL && !H2D(cons_d, cons_host, sizeof(int) * 2 * NL)) return -3;
+  // several host arrays into the device run [d0, d1) with one copy (the bytes between them are padding)
+  struct Seg {
+    void* d;
+    const void* h;
+    size_t bytes;
+  };
+  auto H2Drun = [&](void* d0, void* d1, std::initializer_list<Seg> segs) {
+    const size_t bytes = (size_t)(static_cast<char*>(d1) - static_cast<char*>(d0));
+    if (bytes > TRF_UP_ARENA) return false;
+    if (hs.up_off + bytes > hs.up_cap && !sync()) return false;
+    char* st = hs.up + hs.up_off;
+    std::memset(st, 0, bytes);
+    for (const Seg& g : segs)
+      if (g.bytes) std::memcpy(st + (static_cast<char*>(g.d) - static_cast<char*>(d0)), g.h, g.bytes);
+    hs.up_off += (bytes + 255) & ~(size_t)255;
+    return hipMemcpyAsync(d0, st, bytes, hipMemcpyHostToDevice, s) == hipSuccess;
+  };
   // J^T's constraint terms per joint (trf_jt_kernel): the constraints with the joint as their first end (+) or,
   // failing that, their second end (-), in ascending order of l
   std::vector<int> jadj(J + 1 + 2 * NL, 0);
@@ -1538,10 +1558,12 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
     }
     jadj[j + 1] = e;
   }
-  if (!H2D(jadj_d, jadj.data(), sizeof(int) * jadj.size())) return -3;
-  if (!H2D(ssf_d, ssf_host, sizeof(double) * B)) return -3;
   std::vector<int> act(B, 1), doneh(B, 1);
-  if (!H2D(act_d, act.data(), sizeof(int) * B)) return -3;
+  // (lctl, done and coef are sent before their first reads; zeros until then)
+  if (!H2Drun(cons_d, ctl_end,
+              {{cons_d, cons_host, sizeof(int) * 2 * NL}, {jadj_d, jadj.data(), sizeof(int) * jadj.size()},
+               {ssf_d, ssf_host, sizeof(double) * B}, {act_d, act.data(), sizeof(int) * B}}))
+    return -3;
 
   const dim3 grid(NB, B), blk(TRF_THREADS);
   const dim3 gridj(D.NBV, B);  // J^T launches (with the length variables' workgroup when NBV = NB + 1)
@@ -1674,7 +1696,6 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
       any = true;
     }
     if (!any) break;
-    if (!upload_act()) return -3;
     // regularize: the 1-D quadratic along -g inside the trust region (trf.py:480-484; J g from jac_and_grad)
     for (int b = 0; b < B; ++b) {
       ctl[4 * b] = ctl[4 * b + 1] = ctl[4 * b + 2] = ctl[4 * b + 3] = 0.0;
@@ -1699,8 +1720,10 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
       ctl[4 * b + 1] = std::sqrt(2.0 * cost[b]);  // norm(f)
       ctl[4 * b + 2] = std::min(rows[b], (double)nparam);
     }
-    if (!H2D(Bf.lctl, ctl.data(), sizeof(double) * ctl.size())) return -3;
-    if (!H2D(done_d, doneh.data(), sizeof(int) * B)) return -3;
+    if (!H2Drun(Bf.lctl, act_d + B,
+                {{Bf.lctl, ctl.data(), sizeof(double) * ctl.size()}, {done_d, doneh.data(), sizeof(int) * B},
+                 {act_d, act.data(), sizeof(int) * B}}))
+      return -3;
     for (int b = 0; b < B; ++b) hdone[b] = doneh[b];  // (no kernel writes it before this iteration's lsmr)
     // lsmr(J, f, damp)
     hipLaunchKernelGGL(trf_jt_kernel<1>, gridj, blk, jt_lds, s, D, Bf, 0);
@@ -1765,8 +1788,9 @@ int optim_points_trf(const double* cams, int C, const double* p2d, double* x, in
         pred[b] = -(0.5 * q + (p[0] * gS[2 * b] + p[1] * gS[2 * b + 1]));
       }
       if (!anyt) break;
-      if (!upload_act()) return -3;
-      if (!H2D(Bf.coef, coef.data(), sizeof(double) * coef.size())) return -3;
+      if (!H2Drun(act_d, Bf.coef + coef.size(),
+                  {{act_d, act.data(), sizeof(int) * B}, {Bf.coef, coef.data(), sizeof(double) * coef.size()}}))
+        return -3;
       hipLaunchKernelGGL(trf_nops_kernel, grid, blk, 0, s, D, Bf, x, xt, (int)OP_STEP);
       // the residuals at the trial point with the Jacobian, g, |xt| and J g there, on the bet that the step is
       // accepted (it mostly is): an accepted step then needs no further evaluation or synchronisation.  A
