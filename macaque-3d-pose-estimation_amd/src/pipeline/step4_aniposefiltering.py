@@ -228,7 +228,8 @@ def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int
     ``world`` > 1 (every rank calls this with the same gathered ``kp2d``): rank r filters and lifts the
     individuals a with a % world == r, one object all-gather brings their results to rank 0, which writes the
     files and returns the data (None elsewhere).  Rank 0 writes config.toml / calibration.toml before the other
-    ranks read them (a barrier)."""
+    ranks read them.  An exception on any rank is raised on every rank (each waiting point exchanges the ranks'
+    errors), so a failure ends the run instead of leaving the others waiting."""
     result_dir = results_dir_root + '/' + data_name
     fixed = os.path.exists(os.path.dirname(config_path) + '/joint_len.npy')
     out_name = 'kp3d_fxdJointLen.pickle' if fixed else 'kp3d.pickle'
@@ -242,7 +243,8 @@ def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int
     # ---- configuration + calibration (step4:101-138)
     with open(config_path, 'r') as f:
         cam_ids = [str(i) for i in yaml.safe_load(f)['camera_id']]
-    if rank == 0:
+
+    def setup():
         config = mqio.load_toml(CONFIG_TMPL)
         config['model_folder'] = os.path.abspath(os.path.dirname(result_dir))
         mqio.dump_toml(config, result_dir + '/config.toml')
@@ -251,8 +253,11 @@ def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int
             write_calibration(config_path, result_dir, cam_ids)
         elif not os.path.exists(result_dir + '/calibration.toml'):
             raise FileNotFoundError(f'need {h5_in} (+ h5py) or {result_dir}/calibration.toml')
-    if split:
-        _barrier(group)
+    if not split:
+        setup()
+    else:
+        own = _attempt(setup, rank) if rank == 0 else None
+        _raise_if_any(_gather_objects(own, world, group), own)
 
     # ---- 2D filtering (step4:140-170)
     print('##### 2D filtering....', flush=True)
@@ -261,30 +266,36 @@ def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int
     kp2d = np.asarray(kp2d, dtype=np.float64)
     n_animal = kp2d.shape[0]
     mine = [a for a in range(n_animal) if a % world == rank] if split else list(range(n_animal))
-    kp2d_f = filter_2d(kp2d[mine], device=device) if mine else None
-    if not split:
-        mqio.dump_pickle(kp2d_f, result_dir + '/kp2d_f.pickle')
-
-    # ---- 3D reconstruction (step4:172-339)
-    print('##### 3D reconstruction....', flush=True)
     joint_len_median = None
     if fixed:
         joint_len_median = np.median(np.load(os.path.dirname(config_path) + '/joint_len.npy'), axis=0)
-    config = mqio.load_toml(result_dir + '/config.toml')
-    part = None
-    if mine:
+
+    def lift():
+        kp2d_f = filter_2d(kp2d[mine], device=device) if mine else None
+        if not split:
+            mqio.dump_pickle(kp2d_f, result_dir + '/kp2d_f.pickle')
+        # ---- 3D reconstruction (step4:172-339)
+        print('##### 3D reconstruction....', flush=True)
+        config = mqio.load_toml(result_dir + '/config.toml')
+        if not mine:
+            return config, None
         cgroup = CameraGroup.load(result_dir + '/calibration.toml', device=device).subset_cameras_names(cam_ids)
-        if split:
-            kp3d, S, E, joint_len, run = reconstruct_3d(kp2d_f, cgroup, config, joint_len_median=joint_len_median,
-                                                        verbose=verbose, return_run=True)
-            part = (mine, kp2d_f, kp3d, S, E, joint_len, [mine[i] for i in run])
-        else:
-            kp3d, S, E, joint_len = reconstruct_3d(kp2d_f, cgroup, config, joint_len_median=joint_len_median,
-                                                   verbose=verbose)
-    if split:
-        parts = _gather_objects(part, world, group)
+        if not split:
+            return config, (kp2d_f,) + tuple(reconstruct_3d(kp2d_f, cgroup, config, joint_len_median=joint_len_median,
+                                                            verbose=verbose))
+        kp3d, S, E, joint_len, run = reconstruct_3d(kp2d_f, cgroup, config, joint_len_median=joint_len_median,
+                                                    verbose=verbose, return_run=True)
+        return config, (mine, kp2d_f, kp3d, S, E, joint_len, [mine[i] for i in run])
+
+    if not split:
+        config, (kp2d_f, kp3d, S, E, joint_len) = lift()
+    else:
+        out = _attempt(lift, rank)
+        parts = _gather_objects(out if isinstance(out, _Failure) else out[1], world, group)
+        _raise_if_any(parts, out)
         if rank != 0:
             return None
+        config = out[0]
         kp2d_f, kp3d, S, E, joint_len = _assemble(parts, n_animal)
         if joint_len_median is not None:   # as one rank builds it: the fixed lengths, once per refined individual
             jl_fix = np.asarray(joint_len_median, dtype=np.float64)
@@ -297,10 +308,33 @@ def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int
     return data
 
 
-def _barrier(group):
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized():
-        dist.barrier(group=group)
+class _Failure:
+    """A rank's exception, as sent to the other ranks (the original object stays on its own rank)."""
+
+    def __init__(self, rank, exc):
+        self.rank, self.text = rank, f'{type(exc).__name__}: {exc}'
+        self.exc = exc
+
+    def __getstate__(self):
+        return {'rank': self.rank, 'text': self.text, 'exc': None}
+
+
+def _attempt(fn, rank):
+    """fn() or the _Failure it raised (sent to every rank before anyone raises)."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 -- re-raised by _raise_if_any on every rank
+        return _Failure(rank, e)
+
+
+def _raise_if_any(parts, own):
+    """After the exchange: this rank's own exception as it was raised, else one naming every failed rank."""
+    if isinstance(own, _Failure):
+        raise own.exc
+    bad = [p for p in parts if isinstance(p, _Failure)]
+    if not bad:
+        return
+    raise RuntimeError('step4.proc failed on rank(s) ' + '; '.join(f'{p.rank}: {p.text}' for p in bad))
 
 
 def _gather_objects(obj, world, group):

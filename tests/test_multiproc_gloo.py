@@ -366,3 +366,59 @@ def test_run_demo_world3_uneven_step4_split(tmp_path):
     _same_step4(got[0][1], ref)
     assert ref["kp3d"].shape[0] == 4 and len(ref["joint_len"]) == 2
     assert _step4_files(str(tmp_path / "res1")) == _step4_files(str(tmp_path / "res3"))
+
+
+def _step4_fail_worker(rank, world, port, res, cfg, stage, q):
+    """step4.proc at world `world` over gloo with the CPU stand-ins, failing on purpose: "setup" -- rank 0 finds no
+    calibration; "lift" -- rank 1's lift raises.  Reports what each rank raised."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.join(os.path.dirname(here), "macaque-3d-pose-estimation_amd")]
+    import torch.distributed as dist
+    from src.pipeline import step4_aniposefiltering as step4
+    step4.filter_2d = _fake_filter_2d
+    step4.CameraGroup = _FakeCameraGroup
+
+    def lift(*a, **k):
+        if rank == 1:
+            raise ValueError("lift failed on purpose")
+        return _fake_reconstruct_3d(*a, **k)
+    step4.reconstruct_3d = lift
+    if rank == 0 and stage == "lift":
+        os.makedirs(os.path.join(res, "demo"), exist_ok=True)
+        open(os.path.join(res, "demo", "calibration.toml"), "w").close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kp2d = np.random.default_rng(3).random((3, 6, 2, 17, 3))
+        step4.proc("demo", res, cfg, 17, kp2d=kp2d, world=world, rank=rank)
+        q.put((rank, "ok", ""))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, type(e).__name__, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stage", ["setup", "lift"])
+def test_step4_split_failure_raises_on_every_rank(tmp_path, stage):
+    """A sharded step 4 whose setup (rank 0: no calibration) or lift (rank 1) fails raises on every rank instead of
+    leaving the others waiting in the exchange: the failing rank its own exception, the others a RuntimeError
+    naming it."""
+    import yaml
+    cfg = tmp_path / "config.yaml"
+    cfg.write_text(yaml.safe_dump({"camera_id": [1000, 1001]}))
+    res = str(tmp_path / "res")
+    os.makedirs(os.path.join(res, "demo"), exist_ok=True)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_step4_fail_worker, args=(r, 2, port, res, str(cfg), stage, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (kind, msg)) for r, kind, msg in [q.get(timeout=120) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+    bad = 0 if stage == "setup" else 1
+    assert got[bad][0] == ("FileNotFoundError" if stage == "setup" else "ValueError")
+    other = 1 - bad
+    assert got[other][0] == "RuntimeError" and f"rank(s) {bad}:" in got[other][1], got
