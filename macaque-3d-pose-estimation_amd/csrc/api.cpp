@@ -185,6 +185,9 @@ int mq_set_tuning(int key, int value) {
       if (value < 1 || value > 4) return fail("mq_set_tuning: frames per workgroup must be in [1, 4]", -2);
       mq::g_optim_trf_fb = value;
       break;
+    case MQ_TUNE_GEMM_BLASLT:
+      mq::g_gemm_blaslt = value != 0;
+      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -205,8 +208,14 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_OPTIM_STOP: return mq::g_optim_stop;
     case MQ_TUNE_OPTIM_TRF_CHUNK: return mq::g_optim_trf_chunk;
     case MQ_TUNE_OPTIM_TRF_FB: return mq::g_optim_trf_fb;
+    case MQ_TUNE_GEMM_BLASLT: return mq::g_gemm_blaslt;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
+}
+
+int mq_gemm_plans(int index, int* info, float* ms) {
+  if (!info || !ms) return fail("mq_gemm_plans: null argument");
+  return mq::gemm_blaslt_report(index, info, ms);
 }
 
 const char* mq_last_error(void) { return g_err.c_str(); }
@@ -529,6 +538,13 @@ static int ensure_workspace(mq_vitpose* m, int F) {
   return 0;
 }
 
+// a plain bias GEMM of the forward (proj, fc2, deconv 1): the hipBLASLt kernel when its tuning chose one (the
+// hand kernel's bits, faster; blaslt.hip), else the hand kernel
+static int gemm_plain(const mq::GemmArgs& g, hipStream_t s) {
+  const int r = mq::gemm_blaslt(g, mq::EPI_BF16, s);
+  return r == 1 ? mq::gemm_bf16(g, mq::EPI_BF16, s) : r;
+}
+
 static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, float* heatmaps, hipStream_t s) {
   const int F = flip ? 2 * n : n;
   const int T = m->T, D = m->D, FF = m->FF, dc = m->dc;
@@ -566,7 +582,7 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
       K_TRY(mq::layernorm_f32_bf16(m->X, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
     } else {
       g = mq::GemmArgs{m->O, ly.wproj, P1, ly.bproj, nullptr, rows, D, D, D, D, D, 0};
-      K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+      K_TRY(gemm_plain(g, s));
       K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, nullptr, false, ly.ln2_g, ly.ln2_b, m->Hn, rows, D, 1e-6f, s));
     }
     g = mq::GemmArgs{m->Hn, ly.wfc1, m->G, ly.bfc1, nullptr, rows, FF, D, D, D, FF, 0};
@@ -590,7 +606,10 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
     K_TRY(mq::gemm_bf16(g, mq::EPI_GELU_BF16, s));
     if (timed) HIP_TRY(hipEventRecord(e1, s));
     g = mq::GemmArgs{m->G, ly.wfc2, rf32 ? (void*)m->X : (void*)P2, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0};
-    K_TRY(mq::gemm_bf16(g, rf32 ? mq::EPI_RESID_F32 : mq::EPI_BF16, s));
+    if (rf32)
+      K_TRY(mq::gemm_bf16(g, mq::EPI_RESID_F32, s));
+    else
+      K_TRY(gemm_plain(g, s));
   }
   if (m->L > 0 && !rf32)
     K_TRY(mq::add_layernorm_f32_bf16(m->X, P1, P2, false, m->lnf_g, m->lnf_b, m->Hn, rows, D, 1e-6f, s));
@@ -599,7 +618,7 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
   // head: deconv1 (GEMM + col2im + BN + ReLU)
   unsigned short* cols1 = m->G;
   g = mq::GemmArgs{m->Hn, m->w_dc1, cols1, nullptr, nullptr, rows, 16 * dc, D, D, D, 16 * dc, 0};
-  K_TRY(mq::gemm_bf16(g, mq::EPI_BF16, s));
+  K_TRY(gemm_plain(g, s));
   K_TRY(mq::deconv_col2im_bn_relu(cols1, m->bn1_scale, m->bn1_shift, m->Y1, F, m->gh, m->gw, dc, s));
   const int rows2 = F * 4 * T;
   if (m->dc2_subpixel) {
@@ -620,6 +639,19 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
   K_TRY(mq::gemm_bf16(g, mq::EPI_NCHW_F32, s));
   if (flip) K_TRY(mq::flip_average(m->hm_all, heatmaps, n, m->J, 4 * m->gh, 4 * m->gw, m->flip_idx, s));
   return 0;
+}
+
+// the routing plans of the forward's plain GEMMs, made before a capture (a capture never tunes; blaslt.hip)
+static void prepare_forward_gemms(mq_vitpose* m, int F, hipStream_t s) {
+  if (m->L <= 0 || g_vit_resid_f32) return;
+  const int rows = F * m->T, D = m->D, FF = m->FF, dc = m->dc;
+  const Layer& ly = m->layers[0];
+  (void)mq::gemm_blaslt_prepare(mq::GemmArgs{m->O, ly.wproj, m->QKV, ly.bproj, nullptr, rows, D, D, D, D, D, 0},
+                                mq::EPI_BF16, s);
+  (void)mq::gemm_blaslt_prepare(mq::GemmArgs{m->G, ly.wfc2, m->QKV, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0},
+                                mq::EPI_BF16, s);
+  (void)mq::gemm_blaslt_prepare(
+      mq::GemmArgs{m->Hn, m->w_dc1, m->G, nullptr, nullptr, rows, 16 * dc, D, D, D, 16 * dc, 0}, mq::EPI_BF16, s);
 }
 
 int mq_vitpose_forward(mq_vitpose* m, const float* crops, int n, int flip_test, float* heatmaps, void* stream) {
@@ -644,6 +676,7 @@ int mq_vitpose_forward(mq_vitpose* m, const float* crops, int n, int flip_test, 
       (void)hipGraphExecDestroy(m->gexec);
       m->gexec = nullptr;
     }
+    prepare_forward_gemms(m, F, s);
     HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     rc = launch_forward(m, crops, n, flip_test, heatmaps, cs);
     hipGraph_t graph = nullptr;

@@ -1,7 +1,7 @@
 // A/B of the ViT-H layer GEMMs: the hand-written kernels (mq_gemm_bf16) vs hipBLASLt with the
 // epilogues the library offers (bias; bias + GELU; f32 C accumulate with beta = 1), one process.
 // Build: hipcc -O2 --offload-arch=gfx950 tools/blaslt_probe.cpp -Iinclude -Lmacaque-3d-pose-estimation_amd/lib
-//        -lmq_hip -lhipblaslt -o tools/blaslt_probe   (tools/gpu_blaslt.sh)
+//        -lmq_hip -lhipblaslt -o tools/blaslt_probe   (built on the CPU, run on the GPU box)
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
@@ -43,8 +43,11 @@ static float bf2f(unsigned short h) {
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? std::atoi(argv[1]) : 20;
-  const Shape shapes[] = {{"qkv", 12288, 3840, 1280, 0}, {"proj", 12288, 1280, 1280, 2}, {"fc1", 12288, 5120, 1280, 1},
-                          {"fc2", 12288, 1280, 5120, 2}, {"dc1", 12288, 4096, 1280, 0}};
+  // (round 4 on, proj and fc2 write bf16 branch outputs with the bias: epilogue 0; the f32 residual forms stay as
+  // "proj_f32" / "fc2_f32")
+  const Shape shapes[] = {{"qkv", 12288, 3840, 1280, 0},     {"proj", 12288, 1280, 1280, 0}, {"fc1", 12288, 5120, 1280, 1},
+                          {"fc2", 12288, 1280, 5120, 0},     {"dc1", 12288, 4096, 1280, 0},
+                          {"proj_f32", 12288, 1280, 1280, 2}, {"fc2_f32", 12288, 1280, 5120, 2}};
   mq_ctx* ctx = nullptr;
   CK(mq_create(0, &ctx));
   hipStream_t st;

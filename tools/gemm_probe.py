@@ -13,7 +13,8 @@ sys.path.insert(0, os.path.join(ROOT, "macaque-3d-pose-estimation_amd"))
 COLD = False
 SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
     "qkv": (12288, 3840, 1280, 0),
-    "proj": (12288, 1280, 1280, 2),
+    "proj": (12288, 1280, 1280, 2),  # (until round 4: the f32 residual epilogue)
+    "proj_bf16": (12288, 1280, 1280, 0),  # round 4 on: bf16 branch output
     "fc1": (12288, 5120, 1280, 1),
     "fc2": (12288, 1280, 5120, 2),
     "dc1": (12288, 4096, 1280, 0),
