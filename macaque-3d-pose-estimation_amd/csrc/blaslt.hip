@@ -5,7 +5,8 @@
 // run on a random A with the call's W and bias; a candidate is kept only if its whole output equals the hand
 // kernel's bit for bit (which rules out split-K sums: the K sum must run in one accumulator in ascending order,
 // as in the hand kernels), and the fastest kept one is used if it beats the hand kernel by 2 %.  Every call gets
-// the device's workspace (256 MiB, allocated once), as the library's own probes run them.  Otherwise, or
+// a workspace (256 MiB per host thread and device, allocated outside capture), as the library's probes run them:
+// per thread, so that two threads' streams never share one.  Otherwise, or
 // before tuning (a call inside stream capture never tunes), the caller runs the hand kernel: either route gives
 // the same bits, so where the tuning lands never changes a result.  MQ_TUNE_GEMM_BLASLT = 0 turns the route off.
 #include <hip/hip_runtime.h>
@@ -16,6 +17,7 @@
 #include <memory>
 #include <mutex>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 #include "common.hpp"
@@ -71,8 +73,11 @@ struct Plan {
 std::mutex g_mu;                                      // plans, handles, and a plan's descriptor while it launches
 std::map<Key, std::unique_ptr<Plan>> g_plans;
 hipblasLtHandle_t g_handle[16] = {};
-void* g_ws[16] = {};
+thread_local void* t_ws[16] = {};
 constexpr size_t WS_BYTES = (size_t)256 << 20;
+
+// this thread's workspace on dev (null inside a capture that would have to allocate it)
+void* workspace(int dev, hipStream_t s);
 
 // a plain GEMM the library can compute: bf16 out with bias or nothing, no fused side input, no implicit
 // convolution, no head-major store, sizes where 256 x 256 tiles fill the device
@@ -120,12 +125,9 @@ void destroy(Plan& p) {
 // valid result too.  Nonzero: a HIP / library failure (the call falls back to the hand kernel).
 int tune(const GemmArgs& p, int dev, Plan& plan, hipStream_t s) {
   if (!g_handle[dev] && hipblasLtCreate(&g_handle[dev]) != HIPBLAS_STATUS_SUCCESS) return -1;
-  if (!g_ws[dev] && hipMalloc(&g_ws[dev], WS_BYTES) != hipSuccess) {
-    g_ws[dev] = nullptr;
-    return -1;
-  }
+  void* ws = workspace(dev, s);
+  if (!ws) return -1;
   hipblasLtHandle_t lt = g_handle[dev];
-  void* ws = g_ws[dev];
   // C^T[N, M] = W[N, K] * A[M, K]^T in hipBLASLt's column-major view: m = N, n = M, op(W) = T, op(A) = N
   const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
   const hipblasLtEpilogue_t ep = p.bias ? HIPBLASLT_EPILOGUE_BIAS : HIPBLASLT_EPILOGUE_DEFAULT;
@@ -183,8 +185,7 @@ int tune(const GemmArgs& p, int dev, Plan& plan, hipStream_t s) {
   }
   const float alpha = 1.f, beta = 0.f;
   std::vector<int> diff(CMP_BLOCKS);
-  float best = -1.f;
-  int best_i = -1;
+  std::vector<std::pair<float, int>> kept;  // (one timed run, candidate) of the bit-identical ones
   for (int h = 0; h < nres; ++h) {
     if (heur[h].state != HIPBLAS_STATUS_SUCCESS || heur[h].workspaceSize > WS_BYTES) continue;
     auto run_lt = [&]() {
@@ -200,14 +201,14 @@ int tune(const GemmArgs& p, int dev, Plan& plan, hipStream_t s) {
     if (std::any_of(diff.begin(), diff.end(), [](int d) { return d != 0; })) continue;
     ++plan.identical;
     (void)run_lt();
-    const float ms = time_ms(run_lt, s, 5);
-    if (ms > 0.f && (best < 0.f || ms < best)) {
-      best = ms;
-      best_i = h;
-    }
+    const float ms = time_ms(run_lt, s, 4);  // best of 4 (a single timed run misranks the candidates)
+    if (ms > 0.f) kept.emplace_back(ms, h);
   }
+  std::sort(kept.begin(), kept.end());
+  const float best = kept.empty() ? -1.f : kept[0].first;
+  const int best_i = kept.empty() ? -1 : kept[0].second;
   (void)run_hand();
-  plan.ms_hand = time_ms(run_hand, s, 5);
+  plan.ms_hand = time_ms(run_hand, s, 4);
   plan.ms_lt = best;
   if (best_i >= 0 && plan.ms_hand > 0.f && best < 0.98f * plan.ms_hand) {
     plan.algo = heur[best_i].algo;
@@ -215,6 +216,11 @@ int tune(const GemmArgs& p, int dev, Plan& plan, hipStream_t s) {
   }
   release();
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+void* workspace(int dev, hipStream_t s) {
+  if (!t_ws[dev] && !capturing(s) && hipMalloc(&t_ws[dev], WS_BYTES) != hipSuccess) t_ws[dev] = nullptr;
+  return t_ws[dev];
 }
 
 }  // namespace
@@ -238,12 +244,14 @@ int gemm_blaslt(const GemmArgs& p, int epi, hipStream_t s) {
   }
   Plan& plan = *it->second;
   if (!plan.use_lt) return 1;
+  void* ws = workspace(dev, s);
+  if (!ws) return 1;
   if (p.bias && hipblasLtMatmulDescSetAttribute(plan.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &p.bias,
                                                 sizeof(p.bias)) != HIPBLAS_STATUS_SUCCESS)
     return -5;
   const float alpha = 1.f, beta = 0.f;
   return hipblasLtMatmul(g_handle[dev], plan.desc, &alpha, p.W, plan.la, p.A, plan.lb, &beta, p.C, plan.lc, p.C,
-                         plan.lc, &plan.algo, g_ws[dev], WS_BYTES, s) == HIPBLAS_STATUS_SUCCESS
+                         plan.lc, &plan.algo, ws, WS_BYTES, s) == HIPBLAS_STATUS_SUCCESS
              ? 0
              : -5;
 }
