@@ -185,7 +185,7 @@ int tune(const GemmArgs& p, int dev, Plan& plan, hipStream_t s) {
   }
   const float alpha = 1.f, beta = 0.f;
   std::vector<int> diff(CMP_BLOCKS);
-  std::vector<std::pair<float, int>> kept;  // (one timed run, candidate) of the bit-identical ones
+  std::vector<std::pair<float, int>> kept;  // (best of 4 runs in ms, candidate) of the bit-identical ones
   for (int h = 0; h < nres; ++h) {
     if (heur[h].state != HIPBLAS_STATUS_SUCCESS || heur[h].workspaceSize > WS_BYTES) continue;
     auto run_lt = [&]() {
@@ -223,27 +223,32 @@ void* workspace(int dev, hipStream_t s) {
   return t_ws[dev];
 }
 
+// p's plan on dev, tuned now if there is none (g_mu held); null inside a capture that would have to tune.  A
+// failed tuning is recorded as a hand-kernel plan.
+Plan* find_or_tune(const GemmArgs& p, int dev, hipStream_t s) {
+  const Key key{dev, p.M, p.N, p.K, p.lda, p.ldw, p.ldc, p.bias ? 1 : 0};
+  auto it = g_plans.find(key);
+  if (it != g_plans.end()) return it->second.get();
+  if (capturing(s)) return nullptr;
+  auto plan = std::make_unique<Plan>();
+  if (tune(p, dev, *plan, s)) {
+    destroy(*plan);
+    (void)hipGetLastError();
+  }
+  return g_plans.emplace(key, std::move(plan)).first->second.get();
+}
+
+bool current_device(int& dev) { return hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 16; }
+
 }  // namespace
 
 int gemm_blaslt(const GemmArgs& p, int epi, hipStream_t s) {
-  if (!eligible(p, epi)) return 1;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 1;
-  const Key key{dev, p.M, p.N, p.K, p.lda, p.ldw, p.ldc, p.bias ? 1 : 0};
+  if (!eligible(p, epi) || !current_device(dev)) return 1;
   std::lock_guard<std::mutex> lock(g_mu);
-  auto it = g_plans.find(key);
-  if (it == g_plans.end()) {
-    if (capturing(s)) return 1;
-    auto plan = std::make_unique<Plan>();
-    if (tune(p, dev, *plan, s)) {
-      destroy(*plan);
-      (void)hipGetLastError();
-      plan->use_lt = false;
-    }
-    it = g_plans.emplace(key, std::move(plan)).first;
-  }
-  Plan& plan = *it->second;
-  if (!plan.use_lt) return 1;
+  Plan* found = find_or_tune(p, dev, s);
+  if (!found || !found->use_lt) return 1;
+  Plan& plan = *found;
   void* ws = workspace(dev, s);
   if (!ws) return 1;
   if (p.bias && hipblasLtMatmulDescSetAttribute(plan.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &p.bias,
@@ -257,20 +262,13 @@ int gemm_blaslt(const GemmArgs& p, int epi, hipStream_t s) {
 }
 
 int gemm_blaslt_prepare(const GemmArgs& p, int epi, hipStream_t s) {
-  // the plan only (tuning writes private buffers, not p.C): before a graph capture that will launch p
-  if (!eligible(p, epi) || capturing(s)) return 0;
+  // the plan only (tuning writes private buffers, not p.C) and this thread's workspace: before a graph capture
+  // that will launch p
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 0;
-  const Key key{dev, p.M, p.N, p.K, p.lda, p.ldw, p.ldc, p.bias ? 1 : 0};
+  if (!eligible(p, epi) || !current_device(dev) || capturing(s)) return 0;
   std::lock_guard<std::mutex> lock(g_mu);
-  if (g_plans.count(key)) return 0;
-  auto plan = std::make_unique<Plan>();
-  if (tune(p, dev, *plan, s)) {
-    destroy(*plan);
-    (void)hipGetLastError();
-    plan->use_lt = false;
-  }
-  g_plans.emplace(key, std::move(plan));
+  (void)find_or_tune(p, dev, s);
+  (void)workspace(dev, s);
   return 0;
 }
 
