@@ -156,3 +156,14 @@ def test_context_ignores_tuning_environment():
     import inspect
     from mqhip import _lib
     assert "apply_tuning_env" not in inspect.getsource(_lib.Context)
+
+
+def test_gemm_plans_empty_without_a_forward(lib):
+    """mq_gemm_plans reads the process's GEMM routing decisions (none before a ViT forward); no HIP call."""
+    import ctypes as C
+    import numpy as np
+    info = np.zeros(6, np.int32)
+    ms = np.zeros(2, np.float32)
+    assert lib.mq_gemm_plans(0, C.c_void_p(info.ctypes.data), C.c_void_p(ms.ctypes.data)) == -1
+    assert lib.mq_gemm_plans(-1, C.c_void_p(info.ctypes.data), C.c_void_p(ms.ctypes.data)) == -1
+    assert lib.mq_gemm_plans(0, None, None) < 0 and b"null argument" in lib.mq_last_error()
