@@ -812,9 +812,6 @@ def main():
         "end_to_end_model_tflops": round(model_tflops, 2),
         "end_to_end_mfma_frac": round(model_tflops / (world * PEAK_BF16_TFLOPS), 4),
         "roofline": roof,
-        # the plain bias GEMMs (proj, fc2, deconv 1) run on a hipBLASLt kernel only where one gives the hand kernel's
-        # bits faster (MQ_TUNE_GEMM_BLASLT, tuned at the first warm-up step); the decision per shape
-        "gemm_routes": _lib.gemm_plans(),
     }
     log(f"timed region {dt:.3f} s")
     if not args.no_lift:

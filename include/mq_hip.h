@@ -53,8 +53,10 @@ extern "C" {
  *   7 -- mq_optim_points takes a solver (0: scipy's trust-region-reflective + lsmr, restated -- the default and
  *        the parity mode; 1: the Levenberg-Marquardt + PCG solver of ABI 1-6) and writes 8 stats per animal;
  *        tuning keys MQ_TUNE_OPTIM_TRF_CHUNK (22), MQ_TUNE_VIT_RESID_F32 (23), MQ_TUNE_ATTN_KRING (24) and
- *        MQ_TUNE_OPTIM_TRF_FB (25) added; tuning key MQ_TUNE_GEMM_BLASLT (26) and mq_gemm_plans added. */
-#define MQ_ABI_VERSION 7
+ *        MQ_TUNE_OPTIM_TRF_FB (25) added; tuning key MQ_TUNE_GEMM_BLASLT (26) and mq_gemm_plans added.
+ *   8 -- the hipBLASLt route is gone: every GEMM of the library is a hand-written kernel.  MQ_TUNE_GEMM_BLASLT (26)
+ *        now returns -2 like any unknown key, and mq_gemm_plans was removed. */
+#define MQ_ABI_VERSION 8
 
 typedef struct mq_ctx mq_ctx;
 typedef struct mq_vitpose mq_vitpose;
@@ -91,18 +93,9 @@ const char* mq_last_error(void);
                                        flags (default 16, 1..64; same results) */
 #define MQ_TUNE_OPTIM_TRF_FB 25     /* most frames per workgroup of the trust-region solver's kernels (default 4, 1..4;
                                        same algorithm, the fixed reduction order follows the blocks) */
-#define MQ_TUNE_GEMM_BLASLT 26      /* 1 (default): the ViT's plain bias GEMMs (proj, fc2, deconv 1) may run on a hipBLASLt
-                                       kernel, chosen per shape at the first eager call among the library's no-workspace
-                                       candidates whose output equals the hand kernel's bit for bit, when it is faster;
-                                       0: the hand kernels only (same results) */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);
-/* The GEMM routing decisions made so far in this process (MQ_TUNE_GEMM_BLASLT), one per shape: for index 0, 1, ...
- * info[6] = {M, N, K, 1 if the hipBLASLt kernel runs, library candidates, candidates bit-identical to the hand
- * kernel} and ms[2] = {hand kernel, fastest identical candidate (or -1)}.  Returns 0, or -1 past the last. */
-int mq_gemm_plans(int index, int* info, float* ms);
-
 /* Bind a context to HIP device `device`. */
 int mq_create(int device, mq_ctx** out);
 int mq_destroy(mq_ctx* ctx);
@@ -243,7 +236,7 @@ int mq_conv3x3_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int w
  * (n_img, h, w, ch), ch % 64 == 0, cout % 256 == 0; w_packed = mq_deconv_subpixel_pack of the torch weight
  * [ch][cout][4][4]; shift4 = the BatchNorm shift repeated for the 4 classes (4 * cout floats, may be null).
  * Replaces the head's second deconvolution + col2im (ViTPose HeatmapHead deconv_layers.3/.4/.5,
- * model/pose/ViTPose_huge_macaque_256x192.py head). */
+ * model/pose/td-hm_ViTPose-huge_8xb64-210e_coco-256x192_sn_macaque.py:85-108). */
 int mq_deconv_subpixel_pack(mq_ctx* ctx, const float* w, const float* scale, uint16_t* w_packed, int ch, int cout,
                             void* stream);
 int mq_deconv_subpixel_bf16(mq_ctx* ctx, const uint16_t* x, int n_img, int height, int width, int ch,

@@ -185,9 +185,6 @@ int mq_set_tuning(int key, int value) {
       if (value < 1 || value > 4) return fail("mq_set_tuning: frames per workgroup must be in [1, 4]", -2);
       mq::g_optim_trf_fb = value;
       break;
-    case MQ_TUNE_GEMM_BLASLT:
-      mq::g_gemm_blaslt = value != 0;
-      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -208,14 +205,8 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_OPTIM_STOP: return mq::g_optim_stop;
     case MQ_TUNE_OPTIM_TRF_CHUNK: return mq::g_optim_trf_chunk;
     case MQ_TUNE_OPTIM_TRF_FB: return mq::g_optim_trf_fb;
-    case MQ_TUNE_GEMM_BLASLT: return mq::g_gemm_blaslt;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
-}
-
-int mq_gemm_plans(int index, int* info, float* ms) {
-  if (!info || !ms) return fail("mq_gemm_plans: null argument");
-  return mq::gemm_blaslt_report(index, info, ms);
 }
 
 const char* mq_last_error(void) { return g_err.c_str(); }
@@ -538,12 +529,8 @@ static int ensure_workspace(mq_vitpose* m, int F) {
   return 0;
 }
 
-// a plain bias GEMM of the forward (proj, fc2, deconv 1): the hipBLASLt kernel when its tuning chose one (the
-// hand kernel's bits, faster; blaslt.hip), else the hand kernel
-static int gemm_plain(const mq::GemmArgs& g, hipStream_t s) {
-  const int r = mq::gemm_blaslt(g, mq::EPI_BF16, s);
-  return r == 1 ? mq::gemm_bf16(g, mq::EPI_BF16, s) : r;
-}
+// a plain bias GEMM of the forward (proj, fc2, deconv 1): the hand-written kernels only (gemm_pp.hip)
+static int gemm_plain(const mq::GemmArgs& g, hipStream_t s) { return mq::gemm_bf16(g, mq::EPI_BF16, s); }
 
 static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, float* heatmaps, hipStream_t s) {
   const int F = flip ? 2 * n : n;
@@ -641,19 +628,6 @@ static int launch_forward(mq_vitpose* m, const float* crops, int n, int flip, fl
   return 0;
 }
 
-// the routing plans of the forward's plain GEMMs, made before a capture (a capture never tunes; blaslt.hip)
-static void prepare_forward_gemms(mq_vitpose* m, int F, hipStream_t s) {
-  if (m->L <= 0 || g_vit_resid_f32) return;
-  const int rows = F * m->T, D = m->D, FF = m->FF, dc = m->dc;
-  const Layer& ly = m->layers[0];
-  (void)mq::gemm_blaslt_prepare(mq::GemmArgs{m->O, ly.wproj, m->QKV, ly.bproj, nullptr, rows, D, D, D, D, D, 0},
-                                mq::EPI_BF16, s);
-  (void)mq::gemm_blaslt_prepare(mq::GemmArgs{m->G, ly.wfc2, m->QKV, ly.bfc2, nullptr, rows, D, FF, FF, FF, D, 0},
-                                mq::EPI_BF16, s);
-  (void)mq::gemm_blaslt_prepare(
-      mq::GemmArgs{m->Hn, m->w_dc1, m->G, nullptr, nullptr, rows, 16 * dc, D, D, D, 16 * dc, 0}, mq::EPI_BF16, s);
-}
-
 int mq_vitpose_forward(mq_vitpose* m, const float* crops, int n, int flip_test, float* heatmaps, void* stream) {
   if (!m || !crops || !heatmaps) return fail("mq_vitpose_forward: null argument");
   if (!m->finalized) return fail("mq_vitpose_forward: model not finalized", -2);
@@ -676,7 +650,6 @@ int mq_vitpose_forward(mq_vitpose* m, const float* crops, int n, int flip_test, 
       (void)hipGraphExecDestroy(m->gexec);
       m->gexec = nullptr;
     }
-    prepare_forward_gemms(m, F, s);
     HIP_TRY(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     rc = launch_forward(m, crops, n, flip_test, heatmaps, cs);
     hipGraph_t graph = nullptr;

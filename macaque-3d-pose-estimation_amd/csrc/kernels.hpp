@@ -65,12 +65,6 @@ bool gemm_pingpong_fits(const GemmArgs& p, int epi, int num_cus);
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 int gemm_pingpong_deconv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
-// hipBLASLt for plain bf16 bias GEMMs where, tuned once per shape, it gives the hand kernel's bits faster
-// (blaslt.hip): 0 launched, 1 not taken (run gemm_bf16), < 0 error.  _prepare tunes ahead of a graph capture.
-extern int g_gemm_blaslt;  // MQ_TUNE_GEMM_BLASLT
-int gemm_blaslt(const GemmArgs& p, int epi, hipStream_t stream);
-int gemm_blaslt_prepare(const GemmArgs& p, int epi, hipStream_t stream);
-int gemm_blaslt_report(int index, int* info, float* ms);
 
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,

@@ -13,10 +13,10 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libmq_hip.so"))
-ABI_VERSION = 7  # include/mq_hip.h MQ_ABI_VERSION
+ABI_VERSION = 8  # include/mq_hip.h MQ_ABI_VERSION
 
 EXPORTED = [
-    "mq_abi_version", "mq_last_error", "mq_set_tuning", "mq_get_tuning", "mq_gemm_plans", "mq_create", "mq_destroy",
+    "mq_abi_version", "mq_last_error", "mq_set_tuning", "mq_get_tuning", "mq_create", "mq_destroy",
     "mq_vitpose_create", "mq_vitpose_destroy", "mq_vitpose_set_param", "mq_vitpose_finalize",
     "mq_vitpose_set_graph", "mq_vitpose_timing", "mq_vitpose_timing_result", "mq_crop_udp", "mq_vitpose_forward", "mq_decode_udp", "mq_topdown",
     "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_camera_undistort", "mq_camera_project", "mq_triangulate_dlt", "mq_reproj_error",
@@ -46,7 +46,6 @@ _SIGS = {
     "mq_last_error": (C.c_char_p, []),
     "mq_set_tuning": (i32, [i32, i32]),
     "mq_get_tuning": (i32, [i32]),
-    "mq_gemm_plans": (i32, [i32, vp, vp]),
     "mq_create": (i32, [i32, C.POINTER(vp)]),
     "mq_destroy": (i32, [vp]),
     "mq_vitpose_create": (i32, [vp, i32, i32, i32, i32, i32, C.POINTER(vp)]),
@@ -183,17 +182,3 @@ class Context:
                 _lib.mq_destroy(self.handle)
         except Exception:
             pass
-
-
-def gemm_plans():
-    """The GEMM routing decisions of this process (mq_gemm_plans, MQ_TUNE_GEMM_BLASLT): one dict per shape."""
-    import numpy as np
-    lib = load()
-    out = []
-    info = np.zeros(6, np.int32)
-    ms = np.zeros(2, np.float32)
-    while lib.mq_gemm_plans(len(out), info.ctypes.data, ms.ctypes.data) == 0:
-        out.append({"M": int(info[0]), "N": int(info[1]), "K": int(info[2]), "hipblaslt": bool(info[3]),
-                    "candidates": int(info[4]), "bit_identical": int(info[5]), "hand_ms": round(float(ms[0]), 4),
-                    "hipblaslt_ms": round(float(ms[1]), 4)})
-    return out

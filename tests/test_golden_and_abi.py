@@ -114,7 +114,7 @@ def test_library_exports_every_header_symbol(lib):
     for s in syms:
         assert hasattr(lib, s), f"libmq_hip.so does not export {s}"
     assert sorted(_lib.EXPORTED) == syms
-    assert lib.mq_abi_version() == 7
+    assert lib.mq_abi_version() == 8
 
 
 def test_library_is_gfx950_code_object(lib):
@@ -135,12 +135,11 @@ def test_tuning_knobs_only_select_equivalent_variants(lib):
     """mq_set_tuning accepts only routing knobs whose settings are tested equal (GEMM routing,
     attention version, PCG iterations); the timing-ablation keys of earlier builds (which produced
     wrong results on purpose) are rejected.  No HIP call is made, so this runs without a GPU."""
-    for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 17, 27, 99):
+    for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 17, 26, 27, 99):
         assert lib.mq_set_tuning(key, 1) == -2, key
         assert lib.mq_get_tuning(key) == -2, key
     for key, default, other in ((2, 0, 1), (12, 1, 0), (18, 1, 0), (19, 1, 0), (20, 1, 0), (4, 40, 10),
-                                (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1), (22, 16, 1), (23, 0, 1), (24, 1, 0), (25, 4, 2),
-                                (26, 1, 0)):
+                                (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1), (22, 16, 1), (23, 0, 1), (24, 1, 0), (25, 4, 2)):
         assert lib.mq_get_tuning(key) == default
         assert lib.mq_set_tuning(key, other) == 0
         assert lib.mq_get_tuning(key) == other
@@ -156,14 +155,3 @@ def test_context_ignores_tuning_environment():
     import inspect
     from mqhip import _lib
     assert "apply_tuning_env" not in inspect.getsource(_lib.Context)
-
-
-def test_gemm_plans_empty_without_a_forward(lib):
-    """mq_gemm_plans reads the process's GEMM routing decisions (none before a ViT forward); no HIP call."""
-    import ctypes as C
-    import numpy as np
-    info = np.zeros(6, np.int32)
-    ms = np.zeros(2, np.float32)
-    assert lib.mq_gemm_plans(0, C.c_void_p(info.ctypes.data), C.c_void_p(ms.ctypes.data)) == -1
-    assert lib.mq_gemm_plans(-1, C.c_void_p(info.ctypes.data), C.c_void_p(ms.ctypes.data)) == -1
-    assert lib.mq_gemm_plans(0, None, None) < 0 and b"null argument" in lib.mq_last_error()
