@@ -58,10 +58,26 @@ SOLVER_COST_RATIO = 1.0001     # the GPU solver (trf, scipy's algorithm) on the 
 KP3D_OPTIM_MM_MEDIAN = 1.0     # ... and its distance to scipy's answer on those identical inputs (median / p99)
 KP3D_OPTIM_MM_P99 = 5.0
 # every 3D point (not only all-clear ones): the views whose bf16 heatmap ranks two near-equal peaks the other way
-# (unclear joints) move single points by tens of mm; stated after measurement (DLT p99 16-65 mm,
-# median 0.006 mm over the four scenes)
+# (unclear joints) move single points by tens of mm; stated after measurement, per scene where a scene needs more
+# than the default (median 0.006 mm over the scenes).  p99 measured, DLT / final kp3d: config 2 22.8 /
+# 22.8, the bench's 8-frame slice 24.5 / -, 24 frames seed 7 21.1 / 4.6, seed 8 16.0 / 23.7, seed 9 65.0 / 39.2
 KP3D_EVERY_MM_MEDIAN = 1.0
-KP3D_EVERY_MM_P99 = 100.0
+KP3D_EVERY_MM_P99 = 35.0
+KP3D_EVERY_MM_P99_SCENE = {(24, 9): (75.0, 45.0)}   # (n_frames, seed): (DLT, final kp3d)
+# the chains' optimised joints on all-clear points, p99, as an absolute bound next to the scipy-relative one below;
+# measured 7.88 (24 frames, seed 7), 10.45 (the bench's 8-frame slice), 22.20 (seed 8), 40.60 (seed 9)
+KP3D_OPTIM_E2E_MM_P99 = 12.0
+KP3D_OPTIM_E2E_MM_P99_SCENE = {(24, 8): 26.0, (24, 9): 45.0}
+
+
+def every_point_p99_bounds(n_frames, seed=7):
+    """(DLT, final kp3d) every-point p99 bounds (mm) of a scene."""
+    return KP3D_EVERY_MM_P99_SCENE.get((n_frames, seed), (KP3D_EVERY_MM_P99, KP3D_EVERY_MM_P99))
+
+
+def optim_e2e_p99_bound(n_frames, seed=7):
+    """Absolute bound (mm) on the chains' optimised joints, all-clear points, p99."""
+    return KP3D_OPTIM_E2E_MM_P99_SCENE.get((n_frames, seed), KP3D_OPTIM_E2E_MM_P99)
 # chain to chain after optim_points, against scipy's own sensitivity to the same 2D differences (scipy run on
 # the HIP chain's 2D vs scipy on the oracle chain's): the restated solver adds at most this much
 E2E_OVER_SCIPY_SENSITIVITY_MM = 1.0
