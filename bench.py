@@ -335,9 +335,14 @@ def lift_cpu(cams_np):
             pts = kt[:, :, a, :2, c].copy()
             scs = kt[:, :, a, 2, c].copy()
             pts[scs < fc["score_threshold"]] = np.nan
-            with ctx.Pool(n_proc) as pool:
+            # closed and joined, not terminated (a `with` block SIGTERMs the workers, which profilers log as aborts)
+            pool = ctx.Pool(n_proc)
+            try:
                 res = list(pool.imap_unordered(_viterbi_joint, [(j, pts[:, j, None], scs[:, j, None], fc["n_back"],
                                                                  fc["offset_threshold"]) for j in range(J)]))
+            finally:
+                pool.close()
+                pool.join()
             pf = np.full((F, J, 2), np.nan)
             sf = np.empty((F, J))
             for j, p, sc in res:
@@ -510,13 +515,16 @@ def config5_gpu(device, pose_model, frames, cams_dev, steps=5):
                     "box selection and trackers at thresholds 0)"}
 
 
-def clip_lift(kp, cams_np, device, clips=1, rank=0, world=1):
+def clip_lift(kp, cams_np, device, clips=1, rank=0, world=1, config=None, camera_group=None, return_kp3d=False):
     """The step-4 lift (Viterbi 2D filter, DLT triangulation, optim_points, reprojection errors; the
     default config_tmpl.toml path) of the keypoints every rank produced in the timed region, gathered in
     frame order: kp (F, C, A, J, 3) -> wall seconds (BASELINE config 3's last stage).  Each rank's frames are
     its own synthetic sequence, so the gathered frames are `clips` clips (one per rank) of A individuals; as in
     step4_aniposefiltering.proc on a sharded run, rank r lifts the individuals i = r (mod world) of the
-    clips x A, batched in one solve (every rank holds the gathered keypoints; the caller takes the max)."""
+    clips x A, batched in one solve (every rank holds the gathered keypoints; the caller takes the max).
+    config / camera_group / return_kp3d: the step-4 config (default config_tmpl.toml), the camera group (default
+    the HIP CameraGroup on `device`) and the rank's kp3d in the result -- for the CPU test of the exchange and
+    split (tests/test_multiproc_gloo.py, with oracle stand-ins)."""
     import numpy as np
     import torch
     from mqhip import io as mqio
@@ -526,17 +534,21 @@ def clip_lift(kp, cams_np, device, clips=1, rank=0, world=1):
     kp = kp.reshape((clips, Ft // clips) + kp.shape[1:])                         # (clips, F, C, A, J, 3)
     kp2d = np.ascontiguousarray(kp.transpose(0, 3, 1, 2, 4, 5).reshape((clips * A, Ft // clips) + kp.shape[2:3] + kp.shape[4:])).astype(np.float64)   # (clips*A, F, C, J, 3)
     kp2d = np.ascontiguousarray(kp2d[rank::world])
-    config = mqio.load_toml(CONFIG_TMPL)
-    cg = CameraGroup.from_dicts(cams_np, device=device)
-    torch.cuda.synchronize(device)
+    config = mqio.load_toml(CONFIG_TMPL) if config is None else config
+    cg = CameraGroup.from_dicts(cams_np, device=device) if camera_group is None else camera_group
+    on_gpu = device is not None and torch.cuda.is_available()
+    if on_gpu:
+        torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     kf = filter_2d(kp2d, device=device)
     t1 = time.perf_counter()
     kp3d, _, _, _ = reconstruct_3d(kf, cg, config)
-    torch.cuda.synchronize(device)
+    if on_gpu:
+        torch.cuda.synchronize(device)
     t2 = time.perf_counter()
     A2, F = kp2d.shape[:2]
-    return {"frames": int(F), "clips": int(clips), "individuals": int(A * clips), "individuals_per_rank": int(A2),
+    extra = {"kp3d": kp3d} if return_kp3d else {}
+    return {**extra, "frames": int(F), "clips": int(clips), "individuals": int(A * clips), "individuals_per_rank": int(A2),
             "ms": round((t2 - t0) * 1e3, 3),
             "viterbi_ms": round((t1 - t0) * 1e3, 3), "triangulate_optim_ms": round((t2 - t1) * 1e3, 3),
             "finite_3d_fraction": round(float(np.isfinite(kp3d).mean()), 4),
@@ -758,6 +770,9 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, log_slot=i)
+    # (this rank's compute ends here: one host synchronisation, so the exchange below is timed on its own)
+    torch.cuda.synchronize(dev)
+    t_steps = time.perf_counter()
     # the one exchange step: every rank's per-view 2D keypoints, in frame order (mqhip.shard)
     per_frame = kp_log.view(args.steps, FPS, N_VIEWS, N_ANIMALS, cfg.n_joints, 3).flatten(0, 1)
     if dist_on:
@@ -765,16 +780,24 @@ def main():
     else:
         gathered = per_frame
     torch.cuda.synchronize(dev)
+    t_gather = time.perf_counter()
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     if timing:
         _lib.check(lib.mq_vitpose_timing(model.handle, 0), "timing")
+    # per rank: the timed steps (crop -> ViT -> decode -> DLT) and the keypoint all-gather alone, so a multi-GPU run
+    # separates compute from exchange
+    rank_times = [[(t_steps - t0) * 1e3, (t_gather - t_steps) * 1e3]]
     if dist_on:
         t = torch.tensor([dt], device=xdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        mine = torch.tensor(rank_times[0], device=xdev, dtype=torch.float64)
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        rank_times = [p.tolist() for p in parts]
 
     roof = None
     if timing:
@@ -821,6 +844,10 @@ def main():
         "end_to_end_model_tflops": round(model_tflops, 2),
         "end_to_end_mfma_frac": round(model_tflops / (world * PEAK_BF16_TFLOPS), 4),
         "roofline": roof,
+        "ranks": [{"rank": r, "steps_ms": round(a, 3), "ms_per_step": round(a / args.steps, 3),
+                   "gather_ms": round(b, 3)} for r, (a, b) in enumerate(rank_times)],
+        "gather_ms_max": round(max(b for _, b in rank_times), 3),
+        "gather_bytes_per_rank": int(args.steps * FPS * N_VIEWS * N_ANIMALS * cfg.n_joints * 3 * 4),
     }
     log(f"timed region {dt:.3f} s")
     if not args.no_lift:

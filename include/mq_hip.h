@@ -93,6 +93,9 @@ const char* mq_last_error(void);
                                        flags (default 16, 1..64; same results) */
 #define MQ_TUNE_OPTIM_TRF_FB 25     /* most frames per workgroup of the trust-region solver's kernels (default 4, 1..4;
                                        same algorithm, the fixed reduction order follows the blocks) */
+#define MQ_TUNE_GEMM_W4 27          /* 1: the ViT's bf16-output GEMMs (qkv, proj, fc1, fc2, deconv 1) on the one-wave-per-SIMD
+                                       256x256 kernel (128 x 128 per wave, gemm_w4.hip); 0: the ping-pong kernel.  Same
+                                       accumulation order, the same bits */
 int mq_set_tuning(int key, int value);
 /* Current value of a tuning knob (negative on an unknown key). */
 int mq_get_tuning(int key);

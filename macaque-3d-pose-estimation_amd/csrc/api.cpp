@@ -185,6 +185,10 @@ int mq_set_tuning(int key, int value) {
       if (value < 1 || value > 4) return fail("mq_set_tuning: frames per workgroup must be in [1, 4]", -2);
       mq::g_optim_trf_fb = value;
       break;
+    case MQ_TUNE_GEMM_W4:
+      if (value < 0 || value > 2) return fail("mq_set_tuning: GEMM_W4 must be 0, 1 or 2", -2);
+      mq::g_gemm_w4 = value;
+      break;
     default:
       return fail("mq_set_tuning: unknown key", -2);
   }
@@ -205,6 +209,7 @@ int mq_get_tuning(int key) {
     case MQ_TUNE_OPTIM_STOP: return mq::g_optim_stop;
     case MQ_TUNE_OPTIM_TRF_CHUNK: return mq::g_optim_trf_chunk;
     case MQ_TUNE_OPTIM_TRF_FB: return mq::g_optim_trf_fb;
+    case MQ_TUNE_GEMM_W4: return mq::g_gemm_w4;
     default: return fail("mq_get_tuning: unknown key", -2);
   }
 }

@@ -611,6 +611,7 @@ static int gemm256(const GemmArgs& p, int epi, hipStream_t stream) {
     if (hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || !g_num_cus)
       g_num_cus = 256;
   }
+  if (gemm_w4_fits(p, epi)) return gemm_w4(p, epi, g_num_cus, stream);
   if (gemm_pingpong_fits(p, epi, g_num_cus)) return gemm_pingpong(p, epi, g_num_cus, stream);
   const int tiles_m = (p.M + B2M - 1) / B2M, tiles_n = (p.N + B2N - 1) / B2N;
   const int tiles = tiles_m * tiles_n;

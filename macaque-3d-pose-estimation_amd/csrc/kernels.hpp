@@ -65,6 +65,10 @@ bool gemm_pingpong_fits(const GemmArgs& p, int epi, int num_cus);
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 int gemm_pingpong_conv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 int gemm_pingpong_deconv(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
+// one-wave-per-SIMD 256x256 kernel, 128 x 128 per wave (gemm_w4.hip): bf16 epilogues, K % 32 == 0
+extern int g_gemm_w4;  // MQ_TUNE_GEMM_W4
+bool gemm_w4_fits(const GemmArgs& p, int epi);
+int gemm_w4(const GemmArgs& p, int epi, int num_cus, hipStream_t stream);
 
 // ViT ops (vit_ops.hip)
 int layernorm_f32_bf16(const float* x, const float* gamma, const float* beta, unsigned short* y, int rows, int dim,

@@ -135,11 +135,12 @@ def test_tuning_knobs_only_select_equivalent_variants(lib):
     """mq_set_tuning accepts only routing knobs whose settings are tested equal (GEMM routing,
     attention version, PCG iterations); the timing-ablation keys of earlier builds (which produced
     wrong results on purpose) are rejected.  No HIP call is made, so this runs without a GPU."""
-    for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 17, 26, 27, 99):
+    for key in (1, 3, 5, 6, 7, 8, 9, 10, 11, 13, 14, 15, 16, 17, 26, 28, 99):
         assert lib.mq_set_tuning(key, 1) == -2, key
         assert lib.mq_get_tuning(key) == -2, key
     for key, default, other in ((2, 0, 1), (12, 1, 0), (18, 1, 0), (19, 1, 0), (20, 1, 0), (4, 40, 10),
-                                (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1), (22, 16, 1), (23, 0, 1), (24, 1, 0), (25, 4, 2)):
+                                (21, OPTIM_STOP_DEFAULT, 0 if OPTIM_STOP_DEFAULT else 1), (22, 16, 1), (23, 0, 1), (24, 1, 0), (25, 4, 2),
+                                (27, 0, 1)):
         assert lib.mq_get_tuning(key) == default
         assert lib.mq_set_tuning(key, other) == 0
         assert lib.mq_get_tuning(key) == other

@@ -422,3 +422,84 @@ def test_step4_split_failure_raises_on_every_rank(tmp_path, stage):
     assert got[bad][0] == ("FileNotFoundError" if stage == "setup" else "ValueError")
     other = 1 - bad
     assert got[other][0] == "RuntimeError" and f"rank(s) {bad}:" in got[other][1], got
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# bench.py's N > 1 exchange: every rank's per-view 2D keypoints of its own frames -> the keypoint
+# all-gather (mqhip.shard.gather_keypoints, as in bench.main) -> bench.clip_lift with the individuals split over the
+# ranks.  The exchange logic runs for real over gloo; the lift's GPU stages are oracle stand-ins (oracle/viterbi.py's
+# batched Viterbi for step 4's filter_2d, oracle/geometry.py's CameraGroupOracle DLT and reprojection error inside
+# step 4's own reconstruct_3d, optim_points off).  The GPU-side checks of the same path stay in tests/test_gpu_*.
+
+def _bench_rank_frames(rank, n_frames, cams):
+    """A rank's (n_frames, C, A, J, 3) f32 keypoint log, laid out as bench.main's kp_log per frame."""
+    from mqhip import synth
+    kp = synth.make_kp2d(cams, synth.make_skeletons(4, n_frames, seed=2 + rank), seed=3 + rank)   # (A, F, C, J, 3)
+    return np.ascontiguousarray(kp.transpose(1, 2, 0, 3, 4)).astype(np.float32)
+
+
+def _bench_lift_setup():
+    import bench
+    from mqhip import io as mqio
+    from oracle.viterbi import step4_filter_batched
+    from src.pipeline import step4_aniposefiltering as step4
+    step4.filter_2d = lambda kp2d, filter_config=None, device=0: step4_filter_batched(kp2d)
+    cfg = mqio.load_toml(step4.CONFIG_TMPL)
+    cfg["triangulation"]["optim"] = False
+    cfg["triangulation"]["ransac"] = False
+    return bench, cfg
+
+
+def _bench_exchange_worker(rank, world, port, n_frames, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [root, os.path.join(root, "macaque-3d-pose-estimation_amd")]
+    import torch.distributed as dist
+    from mqhip import synth
+    from mqhip.shard import gather_keypoints
+    from oracle.geometry import CameraGroupOracle
+    bench, cfg = _bench_lift_setup()
+    cams = synth.make_cameras(8)
+    per_frame = torch.from_numpy(_bench_rank_frames(rank, n_frames, cams))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        gathered = gather_keypoints(per_frame, world * n_frames, world)
+        cl = bench.clip_lift(gathered.numpy(), cams, None, clips=world, rank=rank, world=world, config=cfg,
+                             camera_group=CameraGroupOracle(cams), return_kp3d=True)
+        q.put((rank, gathered.numpy(), cl["kp3d"], cl["individuals_per_rank"], cl["individuals"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_exchange_world4_equals_single_rank():
+    """World 4, 3 frames per rank (12 gathered frames = 4 clips x 4 individuals): every rank holds the same
+    gathered keypoints, in rank-then-frame order, equal to the concatenation of the ranks' own logs; rank r lifts
+    the individuals r, r + 4, ... of the 16 and its 3D joints equal the single-rank lift's rows bit for bit."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "macaque-3d-pose-estimation_amd")]
+    from mqhip import synth
+    from oracle.geometry import CameraGroupOracle
+    world, n_frames = 4, 3
+    cams = synth.make_cameras(8)
+    full = np.concatenate([_bench_rank_frames(r, n_frames, cams) for r in range(world)])
+    bench, cfg = _bench_lift_setup()
+    ref = bench.clip_lift(full, cams, None, clips=world, rank=0, world=1, config=cfg,
+                          camera_group=CameraGroupOracle(cams), return_kp3d=True)["kp3d"]
+    assert ref.shape == (world * 4, n_frames, 17, 3) and np.isfinite(ref).mean() > 0.5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_exchange_worker, args=(r, world, port, n_frames, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, gathered, kp3d, per_rank, total in got:
+        np.testing.assert_array_equal(gathered, full)
+        assert per_rank == 4 and total == 16
+        np.testing.assert_array_equal(kp3d, ref[r::world])

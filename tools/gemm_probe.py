@@ -18,6 +18,7 @@ SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
     "fc1": (12288, 5120, 1280, 1),
     "fc2": (12288, 1280, 5120, 2),
     "dc1": (12288, 4096, 1280, 0),
+    "fc2_bf16": (12288, 1280, 5120, 0),  # round 4 on: bf16 branch output
     "dc2": (49152, 4096, 256, 0),
     "f32": (12288, 1280, 5120, 4),   # fc2 shape, plain f32 epilogue
     "fc1_f32": (12288, 5120, 1280, 4),
@@ -31,7 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--shape", default="all")
-    ap.add_argument("--variants", default="pp,il,torch", help="GEMM routes to A/B in this process: pp, il, small, torch")
+    ap.add_argument("--variants", default="pp,il,torch", help="GEMM routes to A/B in this process: pp, il, small, w4 (LDS-DMA), w4v (VGPR-staged), torch")
     ap.add_argument("--cold", action="store_true",
                     help="evict L2/Infinity Cache (384 MB write) before every launch; time each launch alone")
     args = ap.parse_args()
@@ -53,11 +54,13 @@ def main():
             # routing knobs (include/mq_hip.h): pp = ping-pong (default), il = interleaved K-step, small = 128x128
             _lib.check(ctx.lib.mq_set_tuning(12, 0 if var == "il" else 1), "tuning")
             _lib.check(ctx.lib.mq_set_tuning(2, 1 if var == "small" else 0), "tuning")
+            _lib.check(ctx.lib.mq_set_tuning(27, {"w4": 1, "w4v": 2}.get(var, 0)), "tuning")
             for name in names:
                 res[f"{name}/{var}/r{rnd}"] = bench_one(ctx, _lib, torch, name, args.iters)
                 print(f"{name} v={var} r={rnd}", res[f"{name}/{var}/r{rnd}"], flush=True)
     _lib.check(ctx.lib.mq_set_tuning(12, 1), "tuning")
     _lib.check(ctx.lib.mq_set_tuning(2, 0), "tuning")
+    _lib.check(ctx.lib.mq_set_tuning(27, 0), "tuning")
     print(json.dumps(res))
 
 
