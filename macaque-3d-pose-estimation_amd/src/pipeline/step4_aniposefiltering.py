@@ -236,14 +236,36 @@ def proc(data_name, results_dir_root, config_path, n_kp, redo=False, device: int
     split = world > 1
     if split and kp2d is None:
         raise ValueError("step4.proc: a sharded run needs the gathered kp2d in memory on every rank")
-    if os.path.exists(os.path.join(result_dir, out_name)) and not redo:
-        print(f'Skip as exist:{data_name:s}/{out_name}')
-        return
+    if split:
+        # the ranks' objects (failures, per-individual results) travel over a gloo group: a rank whose device has
+        # faulted can still report, and nothing waits on a collective over a dead device
+        group = _object_group(group)
+
+    def skip():
+        return os.path.exists(os.path.join(result_dir, out_name)) and not redo
+
+    def read_cam_ids():
+        with open(config_path, 'r') as f:
+            return [str(i) for i in yaml.safe_load(f)['camera_id']]
+
+    if not split:
+        if skip():
+            print(f'Skip as exist:{data_name:s}/{out_name}')
+            return
+        cam_ids = read_cam_ids()
+    else:
+        # every rank reads the camera ids and rank 0 decides the skip, inside the first exchange: a rank that fails
+        # here (a missing or malformed config.yaml) ends the run on every rank, and all ranks follow rank 0's skip
+        own = _attempt(lambda: (read_cam_ids(), skip() if rank == 0 else None), rank)
+        parts = _gather_objects(own if isinstance(own, _Failure) else (None if rank else own[1]), world, group)
+        _raise_if_any(parts, own)
+        cam_ids = own[0]
+        if parts[0]:
+            if rank == 0:
+                print(f'Skip as exist:{data_name:s}/{out_name}')
+            return None
 
     # ---- configuration + calibration (step4:101-138)
-    with open(config_path, 'r') as f:
-        cam_ids = [str(i) for i in yaml.safe_load(f)['camera_id']]
-
     def setup():
         config = mqio.load_toml(CONFIG_TMPL)
         config['model_folder'] = os.path.abspath(os.path.dirname(result_dir))
@@ -337,9 +359,26 @@ def _raise_if_any(parts, own):
     raise RuntimeError('step4.proc failed on rank(s) ' + '; '.join(f'{p.rank}: {p.text}' for p in bad))
 
 
+_OBJECT_GROUPS = {}
+
+
+def _object_group(group):
+    """The group step 4's object exchanges use: the caller's group when it has one, the default group when that is
+    gloo already, else a gloo group over every rank (created once, collectively, at the first sharded call)."""
+    import datetime
+    import torch.distributed as dist
+    if group is not None or dist.get_backend() == 'gloo':
+        return group
+    key = dist.get_world_size()
+    if key not in _OBJECT_GROUPS:
+        timeout = datetime.timedelta(seconds=float(os.environ.get('MQ_DIST_TIMEOUT_S', '7200')))
+        _OBJECT_GROUPS[key] = dist.new_group(backend='gloo', timeout=timeout)
+    return _OBJECT_GROUPS[key]
+
+
 def _gather_objects(obj, world, group):
-    """Every rank's part (or None) on every rank, in rank order (torch.distributed.all_gather_object: pickled
-    numpy arrays; over RCCL the bytes travel as device tensors)."""
+    """Every rank's part (or None) on every rank, in rank order (torch.distributed.all_gather_object over the gloo
+    object group: pickled numpy arrays through host memory)."""
     import torch.distributed as dist
     out = [None] * world
     dist.all_gather_object(out, obj, group=group)

@@ -370,7 +370,8 @@ def test_run_demo_world3_uneven_step4_split(tmp_path):
 
 def _step4_fail_worker(rank, world, port, res, cfg, stage, q):
     """step4.proc at world `world` over gloo with the CPU stand-ins, failing on purpose: "setup" -- rank 0 finds no
-    calibration; "lift" -- rank 1's lift raises.  Reports what each rank raised."""
+    calibration; "lift" -- rank 1's lift raises; "config" -- rank 1 cannot read config.yaml (before the
+    first exchange).  Reports what each rank raised."""
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [here, os.path.join(os.path.dirname(here), "macaque-3d-pose-estimation_amd")]
@@ -387,6 +388,8 @@ def _step4_fail_worker(rank, world, port, res, cfg, stage, q):
     if rank == 0 and stage == "lift":
         os.makedirs(os.path.join(res, "demo"), exist_ok=True)
         open(os.path.join(res, "demo", "calibration.toml"), "w").close()
+    if stage == "config" and rank == 1:   # this rank's view of config.yaml is missing
+        cfg = cfg + ".missing"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -399,7 +402,7 @@ def _step4_fail_worker(rank, world, port, res, cfg, stage, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("stage", ["setup", "lift"])
+@pytest.mark.parametrize("stage", ["setup", "lift", "config"])
 def test_step4_split_failure_raises_on_every_rank(tmp_path, stage):
     """A sharded step 4 whose setup (rank 0: no calibration) or lift (rank 1) fails raises on every rank instead of
     leaving the others waiting in the exchange: the failing rank its own exception, the others a RuntimeError
@@ -419,7 +422,7 @@ def test_step4_split_failure_raises_on_every_rank(tmp_path, stage):
     for p in procs:
         p.join(timeout=60)
     bad = 0 if stage == "setup" else 1
-    assert got[bad][0] == ("FileNotFoundError" if stage == "setup" else "ValueError")
+    assert got[bad][0] == {"setup": "FileNotFoundError", "lift": "ValueError", "config": "FileNotFoundError"}[stage]
     other = 1 - bad
     assert got[other][0] == "RuntimeError" and f"rank(s) {bad}:" in got[other][1], got
 
