@@ -1289,6 +1289,27 @@ void solve_trust_region_2d(const double B[3], const double g[2], double Delta, d
   const double co[5] = {-b + d, 2 * (a - c + f), 6 * b, 2 * (-a + c + f), -b - d};
   std::vector<double> ts;
   poly_real_roots(co, 4, ts);
+  if (ts.empty()) {
+    // No sign change (numpy's companion eigenvalues would all be complex here, and scipy's argmin over an empty
+    // set raises): the quartic's touching points -- critical points where it is zero to rounding -- are the
+    // boundary candidates; failing those, the Cauchy point -Delta g / |g|.
+    const double dco[4] = {4 * co[0], 3 * co[1], 2 * co[2], co[3]};
+    std::vector<double> crit;
+    poly_real_roots(dco, 3, crit);
+    double scale = 0.0;
+    for (double v : co) scale = std::max(scale, std::fabs(v));
+    for (double tt : crit) {
+      double mag = 0.0;  // |c_i t^(4-i)| summed: the rounding scale of the polynomial's value at t
+      for (int i = 0; i <= 4; ++i) mag += std::fabs(co[i]) * std::pow(std::fabs(tt), 4 - i);
+      if (std::fabs(poly_eval(co, 4, tt)) <= 64 * 2.220446049250313e-16 * (mag > 0 ? mag : scale)) ts.push_back(tt);
+    }
+    if (ts.empty()) {
+      const double gn = std::sqrt(g[0] * g[0] + g[1] * g[1]);
+      p[0] = gn > 0 ? -Delta * g[0] / gn : 0.0;
+      p[1] = gn > 0 ? -Delta * g[1] / gn : -Delta;
+      return;
+    }
+  }
   double best = std::numeric_limits<double>::infinity();
   p[0] = 0.0;
   p[1] = -Delta;
@@ -1345,18 +1366,17 @@ constexpr size_t TRF_DYN_LDS = 128 * 1024;  // (the kernels' static LDS stays un
 // Frames per workgroup.  `fit`: the most (<= TRF_FB and the MQ_TUNE_OPTIM_TRF_FB cap) whose rows fit in LDS.  The
 // per-iteration kernels are latency-bound chains, so fewer frames per workgroup shorten each one's chain while
 // the grid still has a CU per workgroup: the smallest count whose grid, for TRF_NOMINAL_B animals, fits the
-// device's CUs, else `fit` (profiles/r05u_*: 24 frames x 4 animals 8 % faster at 1 frame than at 4; 300 x 4,
+// nominal CUs (TRF_NOMINAL_CUS below), else `fit` (profiles/r05u_*: 24 frames x 4 animals 8 % faster at 1 frame than at 4; 300 x 4,
 // which fills the CUs at 4, 60 % slower at 1).  The choice depends on F, not on the batch, so an animal's
 // result does not depend on which animals share its call (the reductions follow the blocks).  Monotonic in
 // `fit`, so the workspace, sized at the deepest smoothing order, never has fewer blocks than a call.
 constexpr int TRF_NOMINAL_B = 4;  // the reference's four individuals
-static int trf_cu_count() {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                             hipSuccess || cus <= 0)
-    return 256;
-  return cus;
-}
+// The block decomposition (frames per workgroup, the length variables' own workgroup) is sized for a nominal
+// MI355X (256 CUs), not for the device at hand: the reductions follow the blocks, so an optim_points result
+// depends, bit for bit, only on the problem and MQ_TUNE_OPTIM_TRF_FB -- the same on every device and every rank
+// of a sharded step 4.  On a device with fewer CUs the same blocks simply take more rounds.
+constexpr long long TRF_NOMINAL_CUS = 256;
+static int trf_cu_count() { return (int)TRF_NOMINAL_CUS; }
 int trf_frames_per_block(int J, int C, int NL, int n, int F) {
   const int MR = (J * C * 2 + J * 3 + NL + 1) & ~1;
   int fit = 1;
