@@ -476,7 +476,24 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   using NAc = std::integral_constant<int, NA>;
   using NBc = std::integral_constant<int, NB>;
   // barrier that opens an MFMA segment: the segment's fragment reads are complete
+#ifdef PP_STAMP
+  // diagnostic build only (tools/gemm_stamp.py; never the shipped library): s_memtime before and after every barrier of
+  // K-steps 4-7 of block 0, lane 0 of waves 0 and 4 (one wave of each group, the same SIMD), into p.aux
+  int stamp_n = 0, stamp_g = 0;
+  auto stamp = [&]() {
+    if (blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == 4) && stamp_g >= 4 && stamp_g < 8 && p.aux)
+      reinterpret_cast<unsigned long long*>(const_cast<float*>(p.aux))[(wave >> 2) * 64 + stamp_n] =
+          __builtin_amdgcn_s_memtime();
+    ++stamp_n;
+  };
+  auto bar = [&]() {  // arrival, then release
+    stamp();
+    pp_barrier();
+    stamp();
+  };
+#else
   auto bar = [&]() { pp_barrier(); };
+#endif
   auto open_mfma = [&]() {
     bar();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -495,6 +512,10 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
       (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) ? S::STORES_BF16 : S::STORES_F32;
   bool stores_pending = false;
   for (int g = 0; g < total; ++g) {
+#ifdef PP_STAMP
+    stamp_g = g;
+    if (g == 4) stamp_n = 0;
+#endif
     const int slot = g & 1;
     const char* As = smem + slot * PP_STAGE;
     const char* Ws = As + S::OPA;

@@ -50,6 +50,13 @@ def main():
         out["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
     if "SQ_VALU_MFMA_BUSY_CYCLES" in avg and "GRBM_GUI_ACTIVE" in avg:
         out["mfma_busy_per_gui_cycle"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, avg["GRBM_GUI_ACTIVE"])
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back): the share of the chip's
+        # 1,024 SIMD-cycles in which a matrix pipe was busy
+        out["mfma_busy_fraction"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / max(1.0, avg["GRBM_GUI_ACTIVE"] / 8 * 1024)
+    if "SQ_WAVE_CYCLES" in avg:
+        wc = max(1.0, avg["SQ_WAVE_CYCLES"])
+        out["wave_cycle_split"] = {k: avg[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+                                   if k in avg}
     if dur:
         out["avg_duration_ns_under_pmc"] = sum(dur) / len(dur)
     print(json.dumps(out, indent=1))
