@@ -40,7 +40,9 @@ namespace {
 
 constexpr int TRF_THREADS = 256;
 constexpr int TRF_FB = 4;  // frames per workgroup (at most; fewer when a block's rows would not fit in LDS)
+// (5 measured slower on config 4: 23.1 vs 20.9 ms for 240 instead of 300 workgroups; profiles/r06k_*)
 constexpr int TRF_MAXJ = 32, TRF_MAXL = 64, TRF_MAXN = 3;
+static_assert(TRF_FB * TRF_MAXJ * 3 <= 2 * TRF_THREADS, "a block's parameters: at most two per thread");
 constexpr int TRF_NS = 24;  // lsmr state doubles per slot
 
 // -DTRF_PROFILE builds (tools only, never the shipped library): wall-clock time per phase of the two lsmr
@@ -275,6 +277,14 @@ struct Stager {
 // TrfDims made the compiler copy it to scratch: a memory round trip per use)
 __device__ __forceinline__ double dcoef(const TrfDims& D, int m) {
   return m == 0 ? D.c[0] : (m == 1 ? D.c[1] : (m == 2 ? D.c[2] : D.c[3]));
+}
+
+// frame of flat row i in a block of rows `per` wide (i < TRF_FB * per): comparisons, no integer division
+__device__ __forceinline__ int trf_frame_of(int i, int per) {
+  int fl = 0;
+#pragma unroll
+  for (int k = 1; k < TRF_FB; ++k) fl += i >= k * per;
+  return fl;
 }
 
 // lsmr state slot
@@ -604,7 +614,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_jt_kernel(TrfDims D, TrfBufs 
 #pragma unroll
     for (int k = 0; k < 3; ++k) {  // (NT <= 3 TRF_THREADS for 4 frames x 17 joints x 8 cameras; more loop)
       for (int i = k * TRF_THREADS + t; i < NT; i += 3 * TRF_THREADS) {
-        const int fl = (i >= JC) + (i >= 2 * JC) + (i >= 3 * JC), jc = i - fl * JC;
+        const int fl = trf_frame_of(i, JC), jc = i - fl * JC;
         const int j = (int)(((float)jc + 0.5f) * iC), c = jc - j * C;
         const trf_d2* jr2 = reinterpret_cast<const trf_d2*>(sj + (size_t)i * 6);
         const trf_d2 ju = *reinterpret_cast<const trf_d2*>(su + (size_t)(f0 + fl - fa) * D.MR + 2 * jc);
@@ -915,7 +925,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const int i0 = base + k * MW, i = i0 < NR ? i0 : 0;
-        const int fl = (i >= nrep) + (i >= 2 * nrep) + (i >= 3 * nrep), r = i - fl * nrep;
+        const int fl = trf_frame_of(i, nrep), r = i - fl * nrep;
         const int j = (int)(((float)r + 0.5f) * iC);
         const trf_d2* jr2 = reinterpret_cast<const trf_d2*>(sj + (size_t)i * 6);
         a0[k] = jr2[0];
@@ -931,7 +941,7 @@ __global__ void __launch_bounds__(TRF_THREADS) trf_lsmr1_kernel(TrfDims D, TrfBu
       for (int k = 0; k < 3; ++k) {
         const int i = base + k * MW;
         if (i < NR) {
-          const int fl = (i >= nrep) + (i >= 2 * nrep) + (i >= 3 * nrep), r = i - fl * nrep;
+          const int fl = trf_frame_of(i, nrep), r = i - fl * nrep;
           const double ju = a0[k].x * v0[k] + a0[k].y * v1[k] + a1[k].x * v2[k];
           const double jv = a1[k].y * v0[k] + a2[k].x * v1[k] + a2[k].y * v2[k];
           const double un0 = (um[k].x * ib) * -alpha + ju, un1 = (um[k].y * ib) * -alpha + jv;
