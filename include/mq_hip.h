@@ -55,7 +55,8 @@ extern "C" {
  *        tuning keys MQ_TUNE_OPTIM_TRF_CHUNK (22), MQ_TUNE_VIT_RESID_F32 (23), MQ_TUNE_ATTN_KRING (24) and
  *        MQ_TUNE_OPTIM_TRF_FB (25) added; tuning key MQ_TUNE_GEMM_BLASLT (26) and mq_gemm_plans added.
  *   8 -- the hipBLASLt route is gone: every GEMM of the library is a hand-written kernel.  MQ_TUNE_GEMM_BLASLT (26)
- *        now returns -2 like any unknown key, and mq_gemm_plans was removed. */
+ *        now returns -2 like any unknown key, and mq_gemm_plans was removed.  MQ_TUNE_GEMM_W4 (27) and the host-only
+ *        mq_trust_region_2d added. */
 #define MQ_ABI_VERSION 8
 
 typedef struct mq_ctx mq_ctx;
@@ -419,6 +420,14 @@ int mq_optim_prepare(const double* p3ds, int B, int F, int J, const int32_t* con
  * -2 if cap is too small.  Replaces the interpreter-bound json.dumps of step 1's writer. */
 int mq_alldata_json(int n_frames, const int32_t* nrows, const int64_t* tid, const double* box, const double* kp,
                     int J, const int64_t* assigned, const double* score, char* out, int64_t cap, int64_t* len);
+
+/* The 2-D trust-region subproblem of scipy's trf (scipy 1.15.3 optimize/_lsq/common.py solve_trust_region_2d, called
+ * by trf_no_bounds for each trial step of optim_points' least_squares, cameras.py:1166-1180) on the HOST (no HIP
+ * call): minimise 0.5 p^T B p + g^T p subject to |p| <= Delta, B = [B[0] B[1]; B[1] B[2]] (host arrays).  The
+ * Newton point when B is positive definite and the point lies inside; else the best boundary point among the real
+ * roots of scipy's quartic (found by bracketing and bisection instead of np.roots); when the quartic has no sign
+ * change, its touching points, then the Cauchy point -Delta g / |g| (scipy raises there).  Writes p[2]. */
+int mq_trust_region_2d(const double* B, const double* g, double Delta, double* p);
 
 /* CameraGroup.optim_points (cameras.py:1116-1190) and optim_points_jointlenfix (:1192-1415) for
  * B animals at once.  Replaces scipy least_squares (cameras.py:1166-1180: trf, 2-point sparse Jacobian,

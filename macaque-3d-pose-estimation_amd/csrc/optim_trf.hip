@@ -1338,6 +1338,21 @@ void solve_trust_region_2d(const double B[3], const double g[2], double Delta, d
 
 }  // namespace
 
+}  // namespace mq
+
+extern int mq_fail_host(const std::string& msg, int code);
+
+// The 2-D trust-region subproblem on the host (no HIP call): what optim_points' driver solves each trial step,
+// exposed so the CPU tests compare it with the numpy restatement (oracle/trf.py, scipy 1.15.3 common.py).
+extern "C" int mq_trust_region_2d(const double* B, const double* g, double Delta, double* p) {
+  if (!B || !g || !p) return mq_fail_host("mq_trust_region_2d: null argument", -1);
+  if (!(Delta > 0) || !std::isfinite(Delta)) return mq_fail_host("mq_trust_region_2d: Delta must be finite and > 0", -2);
+  mq::solve_trust_region_2d(B, g, Delta, p);
+  return 0;
+}
+
+namespace mq {
+
 int g_optim_trf_chunk = 16;
 int g_optim_trf_fb = TRF_FB;
 

@@ -22,7 +22,7 @@ EXPORTED = [
     "mq_gemm_bf16", "mq_omnidir_undistort", "mq_omnidir_project", "mq_camera_undistort", "mq_camera_project", "mq_triangulate_dlt", "mq_reproj_error",
     "mq_triangulate_ransac", "mq_triangulate_pinv", "mq_geometry_affinity", "mq_match_svt", "mq_viterbi_filter",
     "mq_det_resize_patch", "mq_layernorm", "mq_add_layernorm", "mq_window_attention", "mq_patch_merge_gather", "mq_upsample_add",
-    "mq_im2col3x3", "mq_conv3x3_bf16", "mq_gemm_resid_relu_bf16", "mq_id_conv_bf16", "mq_deconv_subpixel_pack", "mq_deconv_subpixel_bf16", "mq_f32_to_bf16", "mq_subsample2", "mq_nms", "mq_rpn_proposals", "mq_roi_align", "mq_rcnn_post", "mq_det_topk_boxes", "mq_optim_prepare", "mq_optim_points", "mq_attention_bf16", "mq_alldata_json",
+    "mq_im2col3x3", "mq_conv3x3_bf16", "mq_gemm_resid_relu_bf16", "mq_id_conv_bf16", "mq_deconv_subpixel_pack", "mq_deconv_subpixel_bf16", "mq_f32_to_bf16", "mq_subsample2", "mq_nms", "mq_rpn_proposals", "mq_roi_align", "mq_rcnn_post", "mq_det_topk_boxes", "mq_optim_prepare", "mq_trust_region_2d", "mq_optim_points", "mq_attention_bf16", "mq_alldata_json",
     "mq_id_crop_resize", "mq_id_preprocess", "mq_id_im2col", "mq_id_maxpool", "mq_id_relu_bf16", "mq_id_head",
 ]
 
@@ -96,6 +96,7 @@ _SIGS = {
     "mq_rcnn_post": (i32, [vp, vp, vp, vp, i32, i32, f32, f32, f32, f32, f32, f32, i32, vp, vp, vp, vp]),
     "mq_det_topk_boxes": (i32, [vp, vp, vp, vp, i32, i32, i32, f32, f64, f64, f64, vp, vp, vp, vp, vp]),
     "mq_optim_prepare": (i32, [vp, i32, i32, i32, vp, i32, i32, f64, vp, vp]),
+    "mq_trust_region_2d": (i32, [vp, vp, f64, vp]),
     "mq_viterbi_filter": (i32, [vp, vp, i32, i32, i32, i32, f64, i32, f64, vp, vp]),
     "mq_attention_bf16": (i32, [vp, vp, vp, i32, i32, i32, i32, vp]),
     "mq_optim_points": (i32, [vp, vp, i32, vp, vp, i32, i32, i32, vp, i32, i32, vp, f64, f64, f64, i32, i32, i32,
