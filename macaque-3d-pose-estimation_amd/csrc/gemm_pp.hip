@@ -64,7 +64,7 @@ struct PPShape {
   // bias slice per wave: 16 WNF = 64 floats, one dword LDS-DMA (256 B)
   static_assert(WNF == 4, "the epilogue's bias read, paired stores and bias DMA are written for 4 fragments");
   static constexpr int BIAS_SLOT = 256;
-  static constexpr int LDS = PP_BIAS + 8 * BIAS_SLOT;
+  static constexpr int LDS = PP_BIAS + 16 * BIAS_SLOT;  // two bias slots per wave (tile parity)
   // DMA groups (8 rows x 128 B = one 1-KiB wave instruction) in first-read order: P0 A, P0 W, P1 W, P2 A
   static constexpr int GA0 = BM / 16;         // P0 A groups (M half 0 of both wave groups)
   static constexpr int GW0 = 4 * 2 * NA;      // P0 W groups (N part A of the 4 wave columns)
@@ -91,6 +91,21 @@ __device__ __forceinline__ int pp_swz(int row) { return (row >> 1) & 7; }
 __device__ __forceinline__ bf16x8 pp_frag(const char* op, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(op + row * 128 + ((chunk ^ pp_swz(row)) << 4));
 }
+
+// -DPP_DIAG=<bits> diagnostic builds (tools/gemm_diag.py; never the shipped library, results are garbage): take
+// parts of the kernel out to see what they cost.  1: no counted vmcnt waits in the K-loop; 2: no LDS-DMA at all (nor
+// its waits); 4: no barriers (and no stagger: the wave groups run free); 8: the fragment reads of the first K-step
+// only (later K-steps reuse the registers); 16: no epilogue; 32: the bf16 epilogues without their stores; 64: the bf16
+// epilogues store every tile into C's first 256 x 256 block; 128: both wave groups run their epilogues in the same
+// barrier interval (group 0 defers its own past the next K-step's phase-0 DMA issue; rejected, r06r); 256: the bf16
+// epilogues store each wave's 16 KiB lane-linearly into a fixed region of its own.
+#ifndef PP_DIAG
+#define PP_DIAG 0
+#endif
+#define PP_LOOP_WAIT(n)                                   \
+  do {                                                    \
+    if constexpr (!(PP_DIAG & 3)) pp_wait_vm<n>(); \
+  } while (0)
 
 template <int N_IN_FLIGHT>
 __device__ __forceinline__ void pp_wait_vm() {
@@ -246,8 +261,17 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
         // even lanes: [own tile j | neighbour's tile j]; odd: [neighbour's j+1 | own j+1]
         const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
         const int n = nb + (jp + (odd ? 1 : 0)) * 16 + nbase;
+#if PP_DIAG & 32  // the epilogue's arithmetic without its stores
+        asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
+#elif PP_DIAG & 256  // each wave stores its 16 x 1 KiB into a fixed region of its own, lane-linear (whole lines)
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + ((size_t)(blockIdx.x * 8 + (threadIdx.x >> 6)) * 16 + i * 2 + (jp >> 1)) * 512 +
+                                  lane * 8) = o;
+#elif PP_DIAG & 64  // every tile stores into the first 256 x 256 of C (L2-resident lines)
+        *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)(m & 255) * p.ldc + (n & 255)) = o;
+#else
         if (full || (m < p.M && n < p.N))
           *reinterpret_cast<uint4*>(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n) : crow_p + n) = o;
+#endif
       }
     }
     return;
@@ -409,6 +433,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     sdst[i] = (gw[i] ? S::OPA : 0) + grow[i] * 128;
   }
   auto issue = [&](int i, int slot) {
+    if constexpr ((PP_DIAG & 2) != 0) return;
     char* dst = smem + slot * PP_STAGE + sdst[i];
     if (CONV && !gw[i]) {
       // K-step iss_k = tap * (C / 64) + c64: the tap's shifted pixel, channels 64 c64 .. + 63; a pixel
@@ -447,10 +472,13 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   // compute cursor: tile index, K-step in it, its origin, this wave's bias DMA offset (one column per lane)
   int ct = 0, kt = 0, cm0 = 0, cn0 = 0;
   pp_tile_coords<S>(lo + xb, tiles_m, tiles_n, cm0, cn0);
-  char* bias_lds = smem + PP_BIAS + wave * S::BIAS_SLOT;
+  constexpr bool CO = (PP_DIAG & 128) != 0;
+  auto bias_slot = [&](int t) { return smem + PP_BIAS + ((CO ? (t & 1) * 8 : 0) + wave) * S::BIAS_SLOT; };
+  char* bias_lds = bias_slot(0);
   auto bias_offset = [&](int n0) -> unsigned { return (unsigned)((n0 + wcol + lane) * 4); };
   unsigned bias_off = bias_offset(cn0);
   auto issue_bias = [&]() {
+    if constexpr ((PP_DIAG & 2) != 0) return;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0);
   };
 
@@ -478,10 +506,14 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   // barrier that opens an MFMA segment: the segment's fragment reads are complete
 #ifdef PP_STAMP
   // diagnostic build only (tools/gemm_stamp.py; never the shipped library): s_memtime before and after every barrier of
-  // K-steps 4-7 of block 0, lane 0 of waves 0 and 4 (one wave of each group, the same SIMD), into p.aux
+  // K-steps PP_STAMP_G0..+3 (default 4-7) of block 0, lane 0 of waves 0 and 4 (one wave of each group, the same SIMD), into p.aux
+#ifndef PP_STAMP_G0
+#define PP_STAMP_G0 4  // first stamped K-step (of the block's walk; 18: across fc1's first tile boundary)
+#endif
   int stamp_n = 0, stamp_g = 0;
   auto stamp = [&]() {
-    if (blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == 4) && stamp_g >= 4 && stamp_g < 8 && p.aux)
+    if (blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == 4) && stamp_g >= PP_STAMP_G0 && stamp_g < PP_STAMP_G0 + 4 &&
+        p.aux && stamp_n < 64)
       reinterpret_cast<unsigned long long*>(const_cast<float*>(p.aux))[(wave >> 2) * 64 + stamp_n] =
           __builtin_amdgcn_s_memtime();
     ++stamp_n;
@@ -492,7 +524,9 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     stamp();
   };
 #else
-  auto bar = [&]() { pp_barrier(); };
+  auto bar = [&]() {
+    if constexpr (!(PP_DIAG & 4)) pp_barrier();
+  };
 #endif
   auto open_mfma = [&]() {
     bar();
@@ -505,44 +539,62 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   advance();
   pp_wait_vm<S::N3>();
   pp_barrier();
-  if (wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
+  if (!(PP_DIAG & 4) && wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
 
   // >= this many epilogue stores of a full tile are younger than the DMA the next two waits retire
   constexpr int EPI_OPS =
       (EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16) ? S::STORES_BF16 : S::STORES_F32;
   bool stores_pending = false;
+  auto epilogue = [&](const char* bl, int m0, int n0) {
+    if constexpr (!(PP_DIAG & 16))
+      pp_epilogue<EPI, S, MODE == PP_DECONV>(p, acc, reinterpret_cast<const float*>(bl), m0, n0, wm, wn, lane);
+  };
+  auto tile_full = [&](int m0, int n0) { return !(PP_DIAG & 48) && (m0 + S::BM <= p.M) && (n0 + S::BN <= p.N); };
+  bool epi_pending = false;  // group 0: the previous tile's epilogue waits for the next K-step's phase-0 DMA issue
+  int pm0 = 0, pn0 = 0;
   for (int g = 0; g < total; ++g) {
 #ifdef PP_STAMP
     stamp_g = g;
-    if (g == 4) stamp_n = 0;
+    if (g == PP_STAMP_G0) stamp_n = 0;
 #endif
     const int slot = g & 1;
     const char* As = smem + slot * PP_STAGE;
     const char* Ws = As + S::OPA;
     // ---- phase 0: quadrant (M half 0, N part A)
+    auto reads0 = [&]() {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < 2 && (!(PP_DIAG & 8) || g == 0); ++kk) {
 #pragma unroll
-      for (int j = 0; j < NA; ++j)
-        b0[j][kk] = pp_frag(Ws, wcol + j * 16 + frow, kk * 4 + fk);
+        for (int j = 0; j < NA; ++j)
+          b0[j][kk] = pp_frag(Ws, wcol + j * 16 + frow, kk * 4 + fk);
 #pragma unroll
-      for (int i = 0; i < QM; ++i)
-        a[i][kk] = pp_frag(As, arow + i * 16 + frow, kk * 4 + fk);
-    }
+        for (int i = 0; i < QM; ++i)
+          a[i][kk] = pp_frag(As, arow + i * 16 + frow, kk * 4 + fk);
+      }
+    };
+    const bool defer = CO && epi_pending;
+    if (!defer) reads0();
 #pragma unroll
     for (int i = 0; i < S::C0; ++i) issue(i, slot ^ 1);
     issue_bias();
     // retires the DMAs of the previous K-step's phase 2 (younger: its phase 3, this phase + bias)
     if (stores_pending)
-      pp_wait_vm<S::N0 + EPI_OPS>();
+      PP_LOOP_WAIT(S::N0 + EPI_OPS);
     else
-      pp_wait_vm<S::N0>();
+      PP_LOOP_WAIT(S::N0);
+    if (defer) {  // group 0, first K-step of a tile: the previous tile's epilogue beside group 1's
+      bar();
+      epilogue(bias_slot(ct - 1), pm0, pn0);
+      stores_pending = tile_full(pm0, pn0);
+      epi_pending = false;
+      reads0();
+    }
     open_mfma();
     mfma_quadrant(0, b0, 0, NAc{});
     bar();
     // ---- phase 1: quadrant (M half 0, N part B)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < 2 && (!(PP_DIAG & 8) || g == 0); ++kk)
 #pragma unroll
       for (int j = 0; j < NB; ++j)
         b1[j][kk] = pp_frag(Ws, wcol + 16 * NA + j * 16 + frow, kk * 4 + fk);
@@ -550,16 +602,16 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     for (int i = S::C0; i < S::C0 + S::C1; ++i) issue(i, slot ^ 1);
     // retires the previous K-step's phase-3 DMAs (younger: phase 0 + bias, this phase)
     if (stores_pending)
-      pp_wait_vm<S::N1 + EPI_OPS>();
+      PP_LOOP_WAIT(S::N1 + EPI_OPS);
     else
-      pp_wait_vm<S::N1>();
+      PP_LOOP_WAIT(S::N1);
     stores_pending = false;
     open_mfma();
     mfma_quadrant(0, b1, NA, NBc{});
     bar();
     // ---- phase 2: quadrant (M half 1, N part A)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < 2 && (!(PP_DIAG & 8) || g == 0); ++kk)
 #pragma unroll
       for (int i = 0; i < QM; ++i)
         a[i][kk] = pp_frag(As, arow + 16 * QM + i * 16 + frow, kk * 4 + fk);
@@ -572,23 +624,41 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
 #pragma unroll
     for (int i = S::C0 + S::C1 + S::C2; i < 8; ++i) issue(i, slot ^ 1);
     advance();
-    pp_wait_vm<S::N3>();  // phases 0-1 of this K-step (P0 of stage g+1) and the bias
+    PP_LOOP_WAIT(S::N3);  // phases 0-1 of this K-step (P0 of stage g+1) and the bias
     open_mfma();
     mfma_quadrant(1, b1, NA, NBc{});
     bar();
     if (++kt == nk) {
-      pp_epilogue<EPI, S, MODE == PP_DECONV>(p, acc, reinterpret_cast<const float*>(bias_lds), cm0, cn0, wm, wn,
-                                             lane);
-      stores_pending = (cm0 + S::BM <= p.M) && (cn0 + S::BN <= p.N);
+      if (CO && wm == 0) {
+        pm0 = cm0;
+        pn0 = cn0;
+        epi_pending = true;
+      } else {
+        epilogue(bias_lds, cm0, cn0);
+        stores_pending = tile_full(cm0, cn0);
+        if (CO) bar();  // group 0 passes it after its next phase-0 DMA issue, then runs its own epilogue
+      }
       kt = 0;
       ++ct;
       if (ct < my_tiles) {
         pp_tile_coords<S>(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
         bias_off = bias_offset(cn0);
       }
+      bias_lds = bias_slot(ct);
     }
   }
-  if (wm == 0) pp_barrier();  // balance the stagger
+  if (CO && epi_pending) {  // group 0's last tile
+    bar();
+    epilogue(bias_slot(ct - 1), pm0, pn0);
+  }
+  if constexpr ((PP_DIAG & 16) != 0) {  // keep the accumulators live (a store the host never asks for)
+    if (p.M < 0)
+#pragma unroll
+      for (int i = 0; i < WMF; ++i)
+#pragma unroll
+        for (int j = 0; j < WNF; ++j) reinterpret_cast<f32x4*>(p.C)[(i * WNF + j) * 512 + threadIdx.x] = acc[i][j];
+  }
+  if (!(PP_DIAG & 4) && wm == 0) pp_barrier();  // balance the stagger
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 

@@ -1,0 +1,75 @@
+"""A/B of PP_DIAG diagnostic builds of libmq_hip.so (csrc/gemm_pp.hip: one part of the ping-pong mainloop taken
+out; results are garbage, only the time means something) against the shipped library, in one process.
+
+Build: make -C macaque-3d-pose-estimation_amd/csrc OUT=../lib_diag<n> EXTRA=-DPP_DIAG=<n>
+Run:   python tools/gemm_diag.py [--shape fc1,qkv] [--diag 2,10,26]   (PP_DIAG bits: csrc/gemm_pp.hip)
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from gemm_probe import SHAPES  # noqa: E402
+
+PKG = os.path.join(ROOT, "macaque-3d-pose-estimation_amd")
+BITS = {1: "no counted vmcnt waits", 2: "no LDS-DMA", 4: "no barriers", 8: "fragment reads once", 16: "no epilogue", 32: "epilogue without stores", 64: "epilogue stores L2-resident", 128: "both groups' epilogues in one interval",
+        256: "epilogue stores lane-linear per wave"}
+
+
+def what(d):
+    return "shipped" if d == 0 else ", ".join(v for b, v in BITS.items() if d & b)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="fc1,qkv,fc2_bf16")
+    ap.add_argument("--diag", default="16,32,64")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    vp, i32 = C.c_void_p, C.c_int
+    libs = {}
+    for d in [0] + [int(x) for x in args.diag.split(",")]:
+        path = os.path.join(PKG, "lib" if d == 0 else f"lib_diag{d}", "libmq_hip.so")
+        lib = C.CDLL(path)
+        lib.mq_create.argtypes = [i32, C.POINTER(vp)]
+        lib.mq_gemm_bf16.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]
+        ctx = vp()
+        assert lib.mq_create(0, C.byref(ctx)) == 0, path
+        libs[d] = (lib, ctx)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    res = {}
+    for name in args.shape.split(","):
+        M, N, K, epi = SHAPES[name]
+        A = (torch.rand((M, K), device="cuda") * 2 - 1).to(torch.bfloat16)
+        W = ((torch.rand((N, K), device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+        bias = torch.zeros((N,), device="cuda")
+        Cm = torch.zeros((M, N), device="cuda", dtype=torch.bfloat16 if epi in (0, 1) else torch.float32)
+        for rnd in range(args.rounds):
+            for d, (lib, ctx) in libs.items():
+                def run():
+                    assert lib.mq_gemm_bf16(ctx, C.c_void_p(A.data_ptr()), C.c_void_p(W.data_ptr()),
+                                            C.c_void_p(Cm.data_ptr()), C.c_void_p(bias.data_ptr()), None, M, N, K, K, K,
+                                            N, 0, epi, s) == 0
+                for _ in range(3):
+                    run()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    run()
+                e1.record()
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) / args.iters * 1e3
+                res.setdefault((name, d), []).append(us)
+        for d in libs:
+            v = sorted(res[(name, d)])
+            print(f"{name} diag {d} ({what(d)}): median {v[len(v) // 2]:.1f} us  all {[round(x, 1) for x in res[(name, d)]]}",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -25,6 +25,11 @@ SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
     "fc1_bf16": (12288, 5120, 1280, 0),
     "n5120_k5120": (12288, 5120, 5120, 0),
     "m8192": (8192, 5120, 1280, 0),
+    # one tile per CU on 240 / 120 CUs (the epilogue's store cost against the number of CUs storing at once)
+    "fc1_m3072": (3072, 5120, 1280, 1),
+    "fc1_m1536": (1536, 5120, 1280, 1),
+    "bf16_m3072": (3072, 5120, 1280, 0),
+    "bf16_m1536": (1536, 5120, 1280, 0),
 }
 
 
