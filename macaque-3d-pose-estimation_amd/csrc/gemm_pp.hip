@@ -98,7 +98,8 @@ __device__ __forceinline__ bf16x8 pp_frag(const char* op, int row, int chunk) {
 // only (later K-steps reuse the registers); 16: no epilogue; 32: the bf16 epilogues without their stores; 64: the bf16
 // epilogues store every tile into C's first 256 x 256 block; 128: both wave groups run their epilogues in the same
 // barrier interval (group 0 defers its own past the next K-step's phase-0 DMA issue; rejected, r06r); 256: the bf16
-// epilogues store each wave's 16 KiB lane-linearly into a fixed region of its own.
+// epilogues store each wave's 16 KiB lane-linearly into a fixed region of its own; 512: the bf16 epilogues run all
+// their arithmetic first, then issue their 16 stores back to back.
 #ifndef PP_DIAG
 #define PP_DIAG 0
 #endif
@@ -242,6 +243,9 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
     // 16-byte store per lane per pair; an odd last fragment stores its 4 columns (8 B) per lane
     const bool odd = (lane >> 4) & 1;
     const int nbase = nn - (odd ? 4 : 0);
+#if PP_DIAG & 512  // all arithmetic first, then the 16 stores back to back
+    uint4 ov[WMF][WNF / 2];
+#endif
 #pragma unroll
     for (int i = 0; i < WMF; ++i) {
       const int m = mb + i * 16 + mm;
@@ -268,12 +272,29 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, f32x4 (&acc)[S::W
                                   lane * 8) = o;
 #elif PP_DIAG & 64  // every tile stores into the first 256 x 256 of C (L2-resident lines)
         *reinterpret_cast<uint4*>((bf16_t*)p.C + (size_t)(m & 255) * p.ldc + (n & 255)) = o;
+#elif PP_DIAG & 512
+        (void)crow_p;
+        ov[i][jp >> 1] = o;
 #else
         if (full || (m < p.M && n < p.N))
           *reinterpret_cast<uint4*>(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n) : crow_p + n) = o;
 #endif
       }
     }
+#if PP_DIAG & 512
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < WMF; ++i) {
+      const int m = mb + i * 16 + mm;
+      bf16_t* crow_p = (bf16_t*)p.C + crow(m < p.M ? m : 0) * p.ldc - dc_col;
+#pragma unroll
+      for (int jp = 0; jp + 1 < WNF; jp += 2) {
+        const int n = nb + (jp + (odd ? 1 : 0)) * 16 + nbase;
+        if (full || (m < p.M && n < p.N))
+          *reinterpret_cast<uint4*>(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n) : crow_p + n) = ov[i][jp >> 1];
+      }
+    }
+#endif
     return;
   }
   if constexpr (EPI == EPI_RESID_F32) {
