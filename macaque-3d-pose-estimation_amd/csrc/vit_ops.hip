@@ -242,6 +242,12 @@ __device__ __forceinline__ float bfly32_max_raw(float x) {
   return max3_raw(__uint_as_float(p[0]), __uint_as_float(p[1]), __uint_as_float(p[1]));
 }
 
+// -DATT_DIAG=<bits> diagnostic builds (tools/gemm_diag.py --attention; never the shipped library, results are
+// garbage): 1 no K / V / Q loads; 2 no exponentials (the argument itself); 4 no P V^T MFMAs; 8 no stores; 16 no
+// Q K^T MFMAs.  Values a removed part would have produced are laundered through an empty asm so the rest stays.
+#ifndef ATT_DIAG
+#define ATT_DIAG 0
+#endif
 template <int DH, int TT = 0>
 __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t* __restrict__ qkv,
                                                                      bf16_t* __restrict__ out, int T_rt, int D,
@@ -270,7 +276,7 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
   const int l16 = lane & 15, g = lane >> 4;
   const int ntb = T / 16;
 
-  const int nk_ins = (T * KCH + 63) / 64, nv_ins = (T * L::VCH + 63) / 64;
+  const int nk_ins = (ATT_DIAG & 1) ? 0 : (T * KCH + 63) / 64, nv_ins = (ATT_DIAG & 1) ? 0 : (T * L::VCH + 63) / 64;
   for (int ins = wave; ins < nk_ins; ins += ATT_WAVES) {
     const int q = ins * 64 + lane;
     int t = q / KCH, ch = q - (q / KCH) * KCH;
@@ -295,6 +301,8 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
     for (int ks = 0; ks < NKS; ++ks) {
       if (HALF && ks == NKS - 1 && g >= 2)
         qf[u][ks] = bf16x8{};
+      else if constexpr ((ATT_DIAG & 1) != 0)
+        asm volatile("" : "=v"(qf[u][ks]));
       else
         qf[u][ks] = *reinterpret_cast<const bf16x8*>(qrow + ks * 32 + 8 * g);
     }
@@ -334,7 +342,10 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
         // reads issued after fragment t: min(t + KD, NF) - (t + 1)
         att_wait_lgkm_n(NF - 1 - t < KD - 1 ? NF - 1 - t : KD - 1);
         __builtin_amdgcn_sched_barrier(0);
-        S[u][t % NTB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[t % KR], qf[u][t / NTB], S[u][t % NTB], 0, 0, 0);
+        if constexpr (!(ATT_DIAG & 16))
+          S[u][t % NTB] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[t % KR], qf[u][t / NTB], S[u][t % NTB], 0, 0, 0);
+        else
+          asm volatile("" : "+v"(S[u][t % NTB]) : "v"(ring[t % KR]), "v"(qf[u][t / NTB]));
         __builtin_amdgcn_sched_barrier(0);
         if (t + KD < NF) ring[(t + KD) % KR] = att_read_kfrag(kbase[(t + KD) / NTB], (t + KD) % NTB);
       }
@@ -384,7 +395,11 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const f32x2 arg = __builtin_elementwise_fma((f32x2){S[u][tb][2 * h], S[u][tb][2 * h + 1]}, sc2, mb2);
+#if ATT_DIAG & 2
+          const f32x2 pv = arg;
+#else
           const f32x2 pv = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+#endif
           S[u][tb][2 * h] = pv.x;
           S[u][tb][2 * h + 1] = pv.y;
           l2[h] += pv;
@@ -433,7 +448,10 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
         }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt)
-          O[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb[dt], P[u][kst], O[u][dt], 0, 0, 0);
+          if constexpr (!(ATT_DIAG & 4))
+            O[u][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vb[dt], P[u][kst], O[u][dt], 0, 0, 0);
+          else
+            asm volatile("" : "+v"(O[u][dt]) : "v"(vb[dt]), "v"(P[u][kst]));
       }
     }
   };
@@ -459,13 +477,19 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
       const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
       const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
       const uint4 o = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-      *reinterpret_cast<uint4*>(orow + (dp + (odd ? 1 : 0)) * 16 + 4 * (g - (odd ? 1 : 0))) = o;
+      if constexpr ((ATT_DIAG & 8) != 0)
+        asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
+      else
+        *reinterpret_cast<uint4*>(orow + (dp + (odd ? 1 : 0)) * 16 + 4 * (g - (odd ? 1 : 0))) = o;
     }
     if constexpr (NDT & 1) {
       constexpr int dt = NDT - 1;
       const uint2 o = make_uint2(pack_bf16x2(O[u][dt][0] * inv, O[u][dt][1] * inv),
                                  pack_bf16x2(O[u][dt][2] * inv, O[u][dt][3] * inv));
-      *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * g) = o;
+      if constexpr ((ATT_DIAG & 8) != 0)
+        asm volatile("" ::"v"(o.x), "v"(o.y));
+      else
+        *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * g) = o;
     }
   };
   qk(0);

@@ -29,20 +29,27 @@ def main():
     ap.add_argument("--diag", default="16,32,64")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--attention", action="store_true",
+                    help="time mq_attention_bf16 (ViT-H, 64 images) from lib_attdiag<n> builds (-DATT_DIAG=<n>, vit_ops.hip)")
     args = ap.parse_args()
     import torch
     vp, i32 = C.c_void_p, C.c_int
     libs = {}
     for d in [0] + [int(x) for x in args.diag.split(",")]:
-        path = os.path.join(PKG, "lib" if d == 0 else f"lib_diag{d}", "libmq_hip.so")
+        sub = "lib" if d == 0 else (f"lib_attdiag{d}" if args.attention else f"lib_diag{d}")
+        path = os.path.join(PKG, sub, "libmq_hip.so")
         lib = C.CDLL(path)
         lib.mq_create.argtypes = [i32, C.POINTER(vp)]
         lib.mq_gemm_bf16.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]
+        lib.mq_attention_bf16.argtypes = [vp, vp, vp, i32, i32, i32, i32, vp]
         ctx = vp()
         assert lib.mq_create(0, C.byref(ctx)) == 0, path
         libs[d] = (lib, ctx)
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     res = {}
+    if args.attention:
+        attention(args, torch, libs, s)
+        return
     for name in args.shape.split(","):
         M, N, K, epi = SHAPES[name]
         A = (torch.rand((M, K), device="cuda") * 2 - 1).to(torch.bfloat16)
@@ -70,6 +77,37 @@ def main():
             v = sorted(res[(name, d)])
             print(f"{name} diag {d} ({what(d)}): median {v[len(v) // 2]:.1f} us  all {[round(x, 1) for x in res[(name, d)]]}",
                   flush=True)
+
+
+ATT_BITS = {1: "no K/V/Q loads", 2: "no exponentials", 4: "no PV MFMAs", 8: "no stores", 16: "no QK MFMAs"}
+
+
+def attention(args, torch, libs, s):
+    n, T, D, H = 64, 192, 1280, 16
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0)
+    qkv = torch.randn((n * T, 3 * D), generator=g, device="cuda").to(torch.bfloat16)
+    out = torch.empty((n * T, D), device="cuda", dtype=torch.bfloat16)
+    res = {}
+    for rnd in range(args.rounds):
+        for d, (lib, ctx) in libs.items():
+            def run():
+                assert lib.mq_attention_bf16(ctx, C.c_void_p(qkv.data_ptr()), C.c_void_p(out.data_ptr()), n, T, D, H,
+                                             s) == 0
+            for _ in range(3):
+                run()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            res.setdefault(d, []).append(e0.elapsed_time(e1) / args.iters * 1e3)
+    for d, v in res.items():
+        w = "shipped" if d == 0 else ", ".join(t for b, t in ATT_BITS.items() if d & b)
+        print(f"attention diag {d} ({w}): median {sorted(v)[len(v) // 2]:.1f} us  all {[round(x, 1) for x in v]}",
+              flush=True)
 
 
 if __name__ == "__main__":
