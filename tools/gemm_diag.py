@@ -15,7 +15,7 @@ from gemm_probe import SHAPES  # noqa: E402
 
 PKG = os.path.join(ROOT, "macaque-3d-pose-estimation_amd")
 BITS = {1: "no counted vmcnt waits", 2: "no LDS-DMA", 4: "no barriers", 8: "fragment reads once", 16: "no epilogue", 32: "epilogue without stores", 64: "epilogue stores L2-resident", 128: "both groups' epilogues in one interval",
-        256: "epilogue stores lane-linear per wave",
+        256: "epilogue stores lane-linear per wave", 1024: "deferred-store kernel",
         512: "epilogue arithmetic first, then the stores"}
 
 
@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--diag", default="16,32,64")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--check", action="store_true",
+                    help="also compare each build's output with the shipped library's, bit for bit (for diag builds that "
+                         "keep the results, e.g. 1024)")
     ap.add_argument("--attention", action="store_true",
                     help="time mq_attention_bf16 (ViT-H, 64 images) from lib_attdiag<n> builds (-DATT_DIAG=<n>, vit_ops.hip)")
     args = ap.parse_args()
@@ -73,6 +76,19 @@ def main():
                 torch.cuda.synchronize()
                 us = e0.elapsed_time(e1) / args.iters * 1e3
                 res.setdefault((name, d), []).append(us)
+        if args.check:
+            outs = {}
+            for d, (lib, ctx) in libs.items():
+                Cm.fill_(7.0)
+                assert lib.mq_gemm_bf16(ctx, C.c_void_p(A.data_ptr()), C.c_void_p(W.data_ptr()), C.c_void_p(Cm.data_ptr()),
+                                        C.c_void_p(bias.data_ptr()), None, M, N, K, K, K, N, 0, epi, s) == 0
+                torch.cuda.synchronize()
+                outs[d] = Cm.clone()
+            for d in libs:
+                if d:
+                    same = bool(torch.equal(outs[0].view(torch.int16) if outs[0].dtype == torch.bfloat16 else outs[0],
+                                            outs[d].view(torch.int16) if outs[d].dtype == torch.bfloat16 else outs[d]))
+                    print(f"{name} diag {d}: bit-identical to shipped = {same}", flush=True)
         for d in libs:
             v = sorted(res[(name, d)])
             print(f"{name} diag {d} ({what(d)}): median {v[len(v) // 2]:.1f} us  all {[round(x, 1) for x in res[(name, d)]]}",

@@ -30,6 +30,10 @@ SHAPES = {  # name: (M, N, K, epilogue)  for 64 forwards x 192 tokens, ViT-H
     "fc1_m1536": (1536, 5120, 1280, 1),
     "bf16_m3072": (3072, 5120, 1280, 0),
     "bf16_m1536": (1536, 5120, 1280, 0),
+    # ragged tiles (partial M and N tiles, one and several K-steps)
+    "odd_gelu": (700, 520, 320, 1),
+    "odd_bf16": (1000, 264, 2048, 0),
+    "odd_k64": (300, 264, 64, 6),
 }
 
 
