@@ -46,11 +46,7 @@
 
 namespace mq {
 
-#ifndef PP_DIAG
-#define PP_DIAG 0  // diagnostic builds only (the bits are listed below pp_wait_vm)
-#endif
 int g_gemm_pingpong = 1;
-int g_gemm_pp_defer = (PP_DIAG & 1024) ? 1 : 0;  // plain bf16-epilogue GEMMs on gemm_ppd_kernel (stores deferred)
 
 constexpr int PP_BK = 64, PP_T = 512;
 constexpr int PP_STAGE = 64 * 1024;   // one BK slice of the A and W tiles (both shapes: (BM + BN) x 128 B)
@@ -687,290 +683,6 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-// bias + activation + bf16 of two neighbouring fragments (j, j + 1) of one fragment row, paired by
-// v_permlane16_swap into one 16-B row chunk per lane: pp_epilogue's arithmetic, in its order
-template <int EPI>
-__device__ __forceinline__ uint4 pp_pack_pair(const f32x4& x0, const f32x4& x1, const f32x4& c0, const f32x4& c1) {
-  unsigned pk[2][2];
-  auto one = [&](const f32x4& x, const f32x4& c, unsigned* o) {
-    float v[4] = {x[0] + c[0], x[1] + c[1], x[2] + c[2], x[3] + c[3]};
-    if constexpr (EPI == EPI_GELU_BF16) {
-      const f32x2 g0 = gelu_sig2((f32x2){v[0], v[1]}), g1 = gelu_sig2((f32x2){v[2], v[3]});
-      v[0] = g0.x;
-      v[1] = g0.y;
-      v[2] = g1.x;
-      v[3] = g1.y;
-    }
-    if constexpr (EPI == EPI_RELU_BF16) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    o[0] = pack_bf16x2(v[0], v[1]);
-    o[1] = pack_bf16x2(v[2], v[3]);
-  };
-  one(x0, c0, pk[0]);
-  one(x1, c1, pk[1]);
-  const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
-  const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-  return make_uint4(s0[0], s1[0], s0[1], s1[1]);
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// Deferred-store ping-pong (plain GEMMs with a bf16 epilogue: qkv, proj, fc1, fc2, deconv 1).  The same K-steps,
-// phases, DMA plan and accumulation order as gemm_pp_kernel, so the same bits; what moves is the epilogue's 16
-// global stores per wave.  At a tile's end each wave only packs its outputs (bias, activation, bf16, the
-// permlane pairing) into 64 registers; the stores go out during the next tile's first K-step, four after each
-// phase's LDS-DMA issue, while the other wave group runs its MFMAs.  That K-step's MFMAs start from zero (an
-// inline-constant C operand) instead of the accumulators, so these are dead once packed and the packed values
-// take their place: the first K-step is peeled off the tile's K loop.  The counted waits add the stores younger
-// than the DMA they retire (all 16 of a full tile; none, the conservative count, when a partial tile may skip
-// some).
-template <int EPI, int WMF_, int WNF_>
-__global__ __launch_bounds__(PP_T, 2) void gemm_ppd_kernel(GemmArgs p, int tiles_m, int tiles_n) {
-  using S = PPShape<WMF_, WNF_>;
-  static_assert(EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16, "bf16 epilogues only");
-  constexpr int WMF = S::WMF, WNF = S::WNF, QM = S::QM, NA = S::NA, NB = S::NB;
-  static_assert(NA == 2 && NB == 2 && QM == 4, "a quadrant's stores are 4 rows x one fragment pair");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int frow = lane & 15;
-  const int fk = lane >> 4;
-  const int arow = wm * (S::BM / 2);
-  const int wcol = wn * 16 * WNF;
-
-  const int nt = tiles_m * tiles_n;
-  const int G = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int nbx = (G - xcd + 7) >> 3;
-  const int xb = bid >> 3;
-  const int q = nt >> 3, r = nt & 7;
-  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int len = q + (xcd < r ? 1 : 0);
-  const int my_tiles = xb < len ? (len - xb + nbx - 1) / nbx : 0;
-  const int nk = p.K / PP_BK;
-  if (my_tiles == 0) return;
-
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)((size_t)p.M * p.lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsW =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, p.bias ? p.N * 4 : 0, 0x00020000);
-  int grow[8];
-  bool gw[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) grow[i] = pp_group_row<S>(pp_slot_group<S>(wave, i), gw[i]);
-  int iss_t = 0, iss_k = 0;
-  unsigned voff[8];
-  auto set_tile_ptrs = [&](int ti) {
-    int m0, n0;
-    pp_tile_coords<S>(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = grow[i] + (lane >> 3);
-      const int chunk = (lane & 7) ^ pp_swz(row);
-      voff[i] = gw[i] ? (unsigned)(((size_t)min(n0 + row, p.N - 1) * p.ldw + chunk * 8) * 2)
-                      : (unsigned)(((size_t)min(m0 + row, p.M - 1) * p.lda + chunk * 8) * 2);
-    }
-  };
-  set_tile_ptrs(0);
-  __amdgpu_buffer_rsrc_t srs[8];
-  int sdst[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    srs[i] = gw[i] ? rsW : rsA;
-    sdst[i] = (gw[i] ? S::OPA : 0) + grow[i] * 128;
-  }
-  auto issue = [&](int i, int slot) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(srs[i], MQ_LDS_LOCAL(smem + slot * PP_STAGE + sdst[i]), 16, voff[i],
-                                             iss_k * PP_BK * 2, 0, 0);
-  };
-  auto advance = [&]() {
-    if (iss_k + 1 < nk) {
-      ++iss_k;
-    } else if (iss_t + 1 < my_tiles) {
-      ++iss_t;
-      iss_k = 0;
-      set_tile_ptrs(iss_t);
-    }
-  };
-  int cm0 = 0, cn0 = 0;
-  pp_tile_coords<S>(lo + xb, tiles_m, tiles_n, cm0, cn0);
-  char* bias_lds = smem + PP_BIAS + wave * S::BIAS_SLOT;
-  auto bias_offset = [&](int n0) -> unsigned { return (unsigned)((n0 + wcol + lane) * 4); };
-  unsigned bias_off = bias_offset(cn0);
-  auto issue_bias = [&]() { __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_lds), 4, bias_off, 0, 0, 0); };
-
-  f32x4 acc[WMF][WNF];
-  bf16x8 a[QM][2], b0[NA][2], b1[NB][2];
-  uint4 outp[WMF][WNF / 2];  // the previous tile's packed outputs: [fragment row][fragment pair]
-  int pm0 = 0, pn0 = 0;
-  auto bar = [&]() { pp_barrier(); };
-  auto open_mfma = [&]() {
-    bar();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  // one quadrant's 16 MFMAs; ZERO: the tile's first K-step (C operand 0 for the first 32-deep step)
-  auto mfma_quadrant = [&](int qm, auto& bb, int jbase, auto zero) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < QM; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x4& c = acc[qm * QM + i][jbase + j];
-          if (decltype(zero)::value && kk == 0)
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][kk], a[i][kk], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          else
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][kk], a[i][kk], c, 0, 0, 0);
-        }
-    __builtin_amdgcn_s_setprio(0);
-  };
-  const int mm = lane & 15;
-  const int nn = 4 * (lane >> 4);
-  const bool odd = (lane >> 4) & 1;
-  const int nbase = nn - (odd ? 4 : 0);
-  // the tile's outputs into outp (the accumulators are dead afterwards)
-  auto pack = [&]() {
-    f32x4 bv[WNF];
-    const unsigned addr = (unsigned)(uintptr_t)MQ_LDS_LOCAL(bias_lds + nn);
-    asm volatile(
-        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
-        "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
-        : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
-        : "v"(addr)
-        : "memory");
-#pragma unroll
-    for (int i = 0; i < WMF; ++i)
-#pragma unroll
-      for (int jp = 0; jp < WNF; jp += 2) outp[i][jp >> 1] = pp_pack_pair<EPI>(acc[i][jp], acc[i][jp + 1], bv[jp], bv[jp + 1]);
-  };
-  // the previous tile's stores of quadrant qd (4 fragment rows x one fragment pair)
-  auto store_q = [&](int qd) {
-    const int qm = qd >> 1, qn = qd & 1;
-    const int mb = pm0 + wm * (S::BM / 2), nb = pn0 + wn * 16 * WNF;
-    const bool full = (pm0 + S::BM <= p.M) && (pn0 + S::BN <= p.N);
-#pragma unroll
-    for (int ii = 0; ii < QM; ++ii) {
-      const int i = qm * QM + ii;
-      const int m = mb + i * 16 + mm;
-      const int n = nb + (2 * qn + (odd ? 1 : 0)) * 16 + nbase;
-      if (full || (m < p.M && n < p.N))
-        *reinterpret_cast<uint4*>(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n)
-                                                                 : (bf16_t*)p.C + (size_t)m * p.ldc + n) = outp[i][qn];
-    }
-  };
-  // one K-step of the 4-phase plan (gemm_pp_kernel's table); FIRST: the tile's first, with the previous tile's
-  // stores (do_st) after each phase's DMA issue.  st_prev / st_cur: the previous / this K-step issued all 16 stores
-  // (a full tile), counted by the waits; otherwise the waits count none, which only waits longer.
-  auto kstep = [&](int g, auto first, bool do_st, bool st_prev, bool st_cur) {
-    constexpr bool F = decltype(first)::value;
-    const int slot = g & 1;
-    const char* As = smem + slot * PP_STAGE;
-    const char* Ws = As + S::OPA;
-    using ZT = std::integral_constant<bool, F>;
-    // ---- phase 0
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int j = 0; j < NA; ++j) b0[j][kk] = pp_frag(Ws, wcol + j * 16 + frow, kk * 4 + fk);
-#pragma unroll
-      for (int i = 0; i < QM; ++i) a[i][kk] = pp_frag(As, arow + i * 16 + frow, kk * 4 + fk);
-    }
-#pragma unroll
-    for (int i = 0; i < S::C0; ++i) issue(i, slot ^ 1);
-    issue_bias();
-    if (F && do_st) store_q(0);
-    {  // retires the previous K-step's phase-2 DMA; younger: its phase 3 (+ q2, q3 stores), this phase (+ q0)
-      const int ex = (st_prev ? 8 : 0) + (st_cur ? 4 : 0);
-      if (ex == 0) pp_wait_vm<S::N0>();
-      else if (ex == 4) pp_wait_vm<S::N0 + 4>();
-      else if (ex == 8) pp_wait_vm<S::N0 + 8>();
-      else pp_wait_vm<S::N0 + 12>();
-    }
-    open_mfma();
-    mfma_quadrant(0, b0, 0, ZT{});
-    bar();
-    // ---- phase 1
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < NB; ++j) b1[j][kk] = pp_frag(Ws, wcol + 16 * NA + j * 16 + frow, kk * 4 + fk);
-#pragma unroll
-    for (int i = S::C0; i < S::C0 + S::C1; ++i) issue(i, slot ^ 1);
-    if (F && do_st) store_q(1);
-    {  // retires the previous K-step's phase-3 DMA; younger: its q3 stores, this phase 0 (+ q0) and 1 (+ q1)
-      const int ex = (st_prev ? 4 : 0) + (st_cur ? 8 : 0);
-      if (ex == 0) pp_wait_vm<S::N1>();
-      else if (ex == 4) pp_wait_vm<S::N1 + 4>();
-      else if (ex == 8) pp_wait_vm<S::N1 + 8>();
-      else pp_wait_vm<S::N1 + 12>();
-    }
-    open_mfma();
-    mfma_quadrant(0, b1, NA, ZT{});
-    bar();
-    // ---- phase 2
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < QM; ++i) a[i][kk] = pp_frag(As, arow + 16 * QM + i * 16 + frow, kk * 4 + fk);
-#pragma unroll
-    for (int i = S::C0 + S::C1; i < S::C0 + S::C1 + S::C2; ++i) issue(i, slot ^ 1);
-    if (F && do_st) store_q(2);
-    open_mfma();
-    mfma_quadrant(1, b0, 0, ZT{});
-    bar();
-    // ---- phase 3
-#pragma unroll
-    for (int i = S::C0 + S::C1 + S::C2; i < 8; ++i) issue(i, slot ^ 1);
-    if (F && do_st) store_q(3);
-    advance();
-    if (st_cur)  // phases 0-1 of this K-step and the bias; younger: q1-q3 stores and phases 2-3
-      pp_wait_vm<S::N3 + 12>();
-    else
-      pp_wait_vm<S::N3>();
-    open_mfma();
-    mfma_quadrant(1, b1, NA, ZT{});
-    bar();
-  };
-
-  // prologue: stage 0 into buffer 0, P0 landed, then the stagger (as gemm_pp_kernel)
-#pragma unroll
-  for (int i = 0; i < 8; ++i) issue(i, 0);
-  advance();
-  pp_wait_vm<S::N3>();
-  pp_barrier();
-  if (wm == 1) pp_barrier();
-  int g = 0;
-  bool have_prev = false, prev_full = false, st_prev = false;
-  for (int ti = 0; ti < my_tiles; ++ti) {
-    const bool st_cur = have_prev && prev_full;
-    kstep(g++, std::true_type{}, have_prev, st_prev, st_cur);
-    st_prev = st_cur;
-    for (int k = 1; k < nk; ++k) {
-      kstep(g++, std::false_type{}, false, st_prev, false);
-      st_prev = false;
-    }
-    pack();
-    pm0 = cm0;
-    pn0 = cn0;
-    have_prev = true;
-    prev_full = (cm0 + S::BM <= p.M) && (cn0 + S::BN <= p.N);
-    if (ti + 1 < my_tiles) {
-      pp_tile_coords<S>(lo + xb + (ti + 1) * nbx, tiles_m, tiles_n, cm0, cn0);
-      bias_off = bias_offset(cn0);
-    }
-  }
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd) store_q(qd);  // the last tile's
-  if (wm == 0) pp_barrier();  // balance the stagger
-  pp_wait_vm<0>();
-}
-
 template <int EPI, int MODE, class S>
 void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static std::atomic<unsigned> attr{0};
@@ -987,28 +699,11 @@ int tiles_of(const GemmArgs& p, int& tm, int& tn) {
   return tm * tn;
 }
 
-template <int EPI, class S>
-void launch_ppd(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
-  static std::atomic<unsigned> attr{0};
-  if (first_on_device(attr))
-    (void)hipFuncSetAttribute((const void*)gemm_ppd_kernel<EPI, S::WMF, S::WNF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
-  hipLaunchKernelGGL((gemm_ppd_kernel<EPI, S::WMF, S::WNF>), grid, dim3(PP_T), S::LDS, stream, p, tiles_m, tiles_n);
-}
-
 template <class S>
 int launch_shape(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
   int tiles_m, tiles_n;
   const int tiles = tiles_of<S>(p, tiles_m, tiles_n);
   dim3 grid(tiles < num_cus ? tiles : num_cus);
-  if (g_gemm_pp_defer) {
-    switch (epi) {
-      case EPI_BF16: launch_ppd<EPI_BF16, S>(grid, stream, p, tiles_m, tiles_n); return hipGetLastError() == hipSuccess ? 0 : -4;
-      case EPI_GELU_BF16: launch_ppd<EPI_GELU_BF16, S>(grid, stream, p, tiles_m, tiles_n); return hipGetLastError() == hipSuccess ? 0 : -4;
-      case EPI_RELU_BF16: launch_ppd<EPI_RELU_BF16, S>(grid, stream, p, tiles_m, tiles_n); return hipGetLastError() == hipSuccess ? 0 : -4;
-      default: break;
-    }
-  }
   switch (epi) {
     case EPI_BF16: launch_pp<EPI_BF16, PP_GEMM, S>(grid, stream, p, tiles_m, tiles_n); break;
     case EPI_GELU_BF16: launch_pp<EPI_GELU_BF16, PP_GEMM, S>(grid, stream, p, tiles_m, tiles_n); break;
