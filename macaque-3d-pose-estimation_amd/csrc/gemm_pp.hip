@@ -99,7 +99,8 @@ __device__ __forceinline__ bf16x8 pp_frag(const char* op, int row, int chunk) {
 // epilogues store every tile into C's first 256 x 256 block; 128: both wave groups run their epilogues in the same
 // barrier interval (group 0 defers its own past the next K-step's phase-0 DMA issue; rejected, r06r); 256: the bf16
 // epilogues store each wave's 16 KiB lane-linearly into a fixed region of its own; 512: the bf16 epilogues run all
-// their arithmetic first, then issue their 16 stores back to back.
+// their arithmetic first, then issue their 16 stores back to back; 4096: wave group 1 at priority 1 for the whole
+// kernel instead of priority 1 around every MFMA segment; 8192: no priority changes.
 #ifndef PP_DIAG
 #define PP_DIAG 0
 #endif
@@ -511,7 +512,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   bf16x8 a[QM][2], b0[NA][2], b1[NB][2];
 
   auto mfma_quadrant = [&](int qm, auto& bb, int jbase, auto nj) {
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (!(PP_DIAG & (4096 | 8192))) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -520,7 +521,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
         for (int j = 0; j < decltype(nj)::value; ++j)
           acc[qm * QM + i][jbase + j] =
               __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][kk], a[i][kk], acc[qm * QM + i][jbase + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!(PP_DIAG & (4096 | 8192))) __builtin_amdgcn_s_setprio(0);
   };
   using NAc = std::integral_constant<int, NA>;
   using NBc = std::integral_constant<int, NB>;
@@ -561,6 +562,8 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<S::N3>();
   pp_barrier();
   if (!(PP_DIAG & 4) && wm == 1) pp_barrier();  // stagger: group 1 runs one barrier behind group 0
+  if constexpr ((PP_DIAG & 4096) != 0)  // static priority for the second-dispatched group instead of per-segment flips
+    if (wm == 1) __builtin_amdgcn_s_setprio(1);
 
   // >= this many epilogue stores of a full tile are younger than the DMA the next two waits retire
   constexpr int EPI_OPS =
