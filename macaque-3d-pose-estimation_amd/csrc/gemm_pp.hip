@@ -98,7 +98,8 @@ __device__ __forceinline__ bf16x8 pp_frag(const char* op, int row, int chunk) {
 // only (later K-steps reuse the registers); 16: no epilogue; 32: the bf16 epilogues without their stores; 64: the bf16
 // epilogues store every tile into C's first 256 x 256 block; 128: both wave groups run their epilogues in the same
 // barrier interval (group 0 defers its own past the next K-step's phase-0 DMA issue; rejected, r06r); 256: the bf16
-// epilogues store each wave's 16 KiB lane-linearly into a fixed region of its own; 512: the bf16 epilogues run all
+// epilogues store each wave's 16 KiB lane-linearly into a fixed region of its own (256 blocks x 128 KiB: only for
+// outputs of at least 32 MiB, e.g. fc1, qkv, deconv 1); 512: the bf16 epilogues run all
 // their arithmetic first, then issue their 16 stores back to back; 4096: wave group 1 at priority 1 for the whole
 // kernel instead of priority 1 around every MFMA segment; 8192: no priority changes.
 #ifndef PP_DIAG
