@@ -62,6 +62,8 @@ def main():
         Cm = torch.zeros((M, N), device="cuda", dtype=torch.bfloat16 if epi in (0, 1) else torch.float32)
         for rnd in range(args.rounds):
             for d, (lib, ctx) in libs.items():
+                if d & 256 and M * N * 2 < (32 << 20):  # (the lane-linear store region is 32 MiB)
+                    continue
                 def run():
                     assert lib.mq_gemm_bf16(ctx, C.c_void_p(A.data_ptr()), C.c_void_p(W.data_ptr()),
                                             C.c_void_p(Cm.data_ptr()), C.c_void_p(bias.data_ptr()), None, M, N, K, K, K,
@@ -80,17 +82,21 @@ def main():
         if args.check:
             outs = {}
             for d, (lib, ctx) in libs.items():
+                if d & 256 and M * N * 2 < (32 << 20):
+                    continue
                 Cm.fill_(7.0)
                 assert lib.mq_gemm_bf16(ctx, C.c_void_p(A.data_ptr()), C.c_void_p(W.data_ptr()), C.c_void_p(Cm.data_ptr()),
                                         C.c_void_p(bias.data_ptr()), None, M, N, K, K, K, N, 0, epi, s) == 0
                 torch.cuda.synchronize()
                 outs[d] = Cm.clone()
-            for d in libs:
+            for d in outs:
                 if d:
                     same = bool(torch.equal(outs[0].view(torch.int16) if outs[0].dtype == torch.bfloat16 else outs[0],
                                             outs[d].view(torch.int16) if outs[d].dtype == torch.bfloat16 else outs[d]))
                     print(f"{name} diag {d}: bit-identical to shipped = {same}", flush=True)
         for d in libs:
+            if (name, d) not in res:
+                continue
             v = sorted(res[(name, d)])
             print(f"{name} diag {d} ({what(d)}): median {v[len(v) // 2]:.1f} us  all {[round(x, 1) for x in res[(name, d)]]}",
                   flush=True)
