@@ -125,7 +125,10 @@ __device__ __forceinline__ void pp_barrier() {
 
 template <class S>
 __device__ __forceinline__ void pp_tile_coords(int wid, int tiles_m, int tiles_n, int& m0, int& n0) {
-  constexpr int GROUP_M = 8;
+#ifndef PP_GROUP_M
+#define PP_GROUP_M 8  // (diagnostic builds may set it: tools/gemm_diag.py --group-m)
+#endif
+  constexpr int GROUP_M = PP_GROUP_M;
   const int per_group = GROUP_M * tiles_n;
   const int grp = wid / per_group;
   const int first_m = grp * GROUP_M;

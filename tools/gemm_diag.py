@@ -21,6 +21,8 @@ BITS = {1: "no counted vmcnt waits", 2: "no LDS-DMA", 4: "no barriers", 8: "frag
 
 
 def what(d):
+    if d >= 100000:  # lib_diag1000NN: a build with PP_GROUP_M = NN (the tile walk's M-group)
+        return f"GROUP_M {d - 100000}"
     return "shipped" if d == 0 else ", ".join(v for b, v in BITS.items() if d & b)
 
 
@@ -60,8 +62,11 @@ def main():
         W = ((torch.rand((N, K), device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
         bias = torch.zeros((N,), device="cuda")
         Cm = torch.zeros((M, N), device="cuda", dtype=torch.bfloat16 if epi in (0, 1) else torch.float32)
+        keys = list(libs)
         for rnd in range(args.rounds):
-            for d, (lib, ctx) in libs.items():
+            # the order rotates every round, so no build always runs first (the clock ramps within a round)
+            for d in keys[rnd % len(keys):] + keys[:rnd % len(keys)]:
+                lib, ctx = libs[d]
                 if d & 256 and M * N * 2 < (32 << 20):  # (the lane-linear store region is 32 MiB)
                     continue
                 def run():
