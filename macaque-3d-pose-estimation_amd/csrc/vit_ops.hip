@@ -244,7 +244,8 @@ __device__ __forceinline__ float bfly32_max_raw(float x) {
 
 // -DATT_DIAG=<bits> diagnostic builds (tools/gemm_diag.py --attention; never the shipped library, results are
 // garbage): 1 no K / V / Q loads; 2 no exponentials (the argument itself); 4 no P V^T MFMAs; 8 no stores; 16 no
-// Q K^T MFMAs.  Values a removed part would have produced are laundered through an empty asm so the rest stays.
+// Q K^T MFMAs; 32 no K fragment reads from LDS.  Values a removed part would have produced are laundered through
+// an empty asm so the rest stays.
 #ifndef ATT_DIAG
 #define ATT_DIAG 0
 #endif
@@ -336,7 +337,12 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
       }
       bf16x8 ring[KR];
 #pragma unroll
-      for (int t = 0; t < KD; ++t) ring[t] = att_read_kfrag(kbase[t / NTB], t % NTB);
+      for (int t = 0; t < KD; ++t) {
+        if constexpr ((ATT_DIAG & 32) != 0)
+          asm volatile("" : "=v"(ring[t]) : "v"(kbase[t / NTB]));
+        else
+          ring[t] = att_read_kfrag(kbase[t / NTB], t % NTB);
+      }
 #pragma unroll
       for (int t = 0; t < NF; ++t) {
         // reads issued after fragment t: min(t + KD, NF) - (t + 1)
@@ -347,7 +353,12 @@ __global__ __launch_bounds__(ATT_THREADS, 4) void attention2_kernel(const bf16_t
         else
           asm volatile("" : "+v"(S[u][t % NTB]) : "v"(ring[t % KR]), "v"(qf[u][t / NTB]));
         __builtin_amdgcn_sched_barrier(0);
-        if (t + KD < NF) ring[(t + KD) % KR] = att_read_kfrag(kbase[(t + KD) / NTB], (t + KD) % NTB);
+        if (t + KD < NF) {
+          if constexpr ((ATT_DIAG & 32) != 0)
+            asm volatile("" : "=v"(ring[(t + KD) % KR]) : "v"(kbase[(t + KD) / NTB]));
+          else
+            ring[(t + KD) % KR] = att_read_kfrag(kbase[(t + KD) / NTB], (t + KD) % NTB);
+        }
       }
     } else {
 #pragma unroll

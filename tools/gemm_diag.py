@@ -107,7 +107,8 @@ def main():
                   flush=True)
 
 
-ATT_BITS = {1: "no K/V/Q loads", 2: "no exponentials", 4: "no PV MFMAs", 8: "no stores", 16: "no QK MFMAs"}
+ATT_BITS = {1: "no K/V/Q loads", 2: "no exponentials", 4: "no PV MFMAs", 8: "no stores", 16: "no QK MFMAs",
+            32: "no K fragment reads"}
 
 
 def attention(args, torch, libs, s):
