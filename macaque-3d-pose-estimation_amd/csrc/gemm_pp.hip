@@ -46,11 +46,7 @@
 
 namespace mq {
 
-#ifndef PP_DIAG
-#define PP_DIAG 0  // diagnostic builds only (the bits are listed at pp_wait_vm)
-#endif
 int g_gemm_pingpong = 1;
-int g_gemm_half = (PP_DIAG & 16384) ? 1 : 0;  // bf16-epilogue GEMMs on gemm_ph_kernel (experiment)
 
 constexpr int PP_BK = 64, PP_T = 512;
 constexpr int PP_STAGE = 64 * 1024;   // one BK slice of the A and W tiles (both shapes: (BM + BN) x 128 B)
@@ -694,274 +690,6 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   pp_wait_vm<0>();            // no DMA may outlive the block
 }
 
-// ---------------------------------------------------------------------------------------------------------
-// Half-tile ping-pong with a streamed epilogue (experiment, PP_DIAG bit 16384).  Tiles of
-// 256 x 128, 8 waves of 128 x 32 (8 x 2 fragments), two phases per K-step (M half 0, M half 1: 16 MFMAs each), a
-// three-stage LDS ring of 48 KiB stages: P0 = both groups' A rows of M half 0 + the 128 W rows (4 pieces per wave,
-// issued in phase 0 for stage g + 2), P1 = the other A rows (2 per wave, phase 1).  P0(g + 2) is waited in phase 1
-// of K-step g + 1 and P1(g + 2) in phase 0 of g + 2, each before the last barrier both groups pass ahead of the
-// reads.  The previous half-tile's accumulators stay live (64 VGPRs) and its 8 stores per wave go out in phase 1
-// of the odd K-steps 1..15 of the next half-tile (buffer stores: out-of-range lanes are dropped, so every store
-// issues); the other odd K-steps issue a 4-byte LDS-DMA into a junk slot instead, so every counted wait sees the
-// same number of younger operations: 12 in phase 0, 11 in phase 1.  Same accumulation order as gemm_pp_kernel.
-struct PHShape {
-  static constexpr int BM = 256, BN = 128;
-};
-constexpr int PH_STAGE = 48 * 1024, PH_OPA = 32 * 1024, PH_BIAS = 3 * PH_STAGE, PH_JUNK = PH_BIAS + 16 * 256;
-constexpr int PH_LDS = PH_JUNK + 8 * 256;
-
-__device__ __forceinline__ int ph_group_row(int slot, int wave, bool& is_w) {
-  if (slot >= 4) {  // P1: A rows 64-127 and 192-255
-    const int k = 2 * wave + (slot - 4);
-    is_w = false;
-    return (k >> 3) * 128 + 64 + (k & 7) * 8;
-  }
-  const int k = 4 * wave + slot;  // P0: A rows 0-63, 128-191, then the W rows
-  if (k < 16) {
-    is_w = false;
-    return (k >> 3) * 128 + (k & 7) * 8;
-  }
-  is_w = true;
-  return (k - 16) * 8;
-}
-
-template <int EPI>
-__global__ __launch_bounds__(PP_T, 2) void gemm_ph_kernel(GemmArgs p, int tiles_m, int tiles_n) {
-  static_assert(EPI == EPI_BF16 || EPI == EPI_GELU_BF16 || EPI == EPI_RELU_BF16, "bf16 epilogues");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int frow = lane & 15, fk = lane >> 4;
-  const int arow = wm * 128, wcol = wn * 32;
-  const int nt = tiles_m * tiles_n;
-  const int G = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
-  const int nbx = (G - xcd + 7) >> 3, xb = bid >> 3;
-  const int q = nt >> 3, r = nt & 7;
-  const int lo = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int len = q + (xcd < r ? 1 : 0);
-  const int my_tiles = xb < len ? (len - xb + nbx - 1) / nbx : 0;
-  const int nk = p.K / PP_BK;
-  const int total = my_tiles * nk;
-  if (total == 0) return;
-  const __amdgpu_buffer_rsrc_t rsA =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, (int)((size_t)p.M * p.lda * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsW =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, (int)((size_t)p.N * p.ldw * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsB =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, p.bias ? p.N * 4 : 0, 0x00020000);
-  const size_t c_bytes = p.head_dim ? (size_t)p.M * p.N * 2 : ((size_t)(p.M - 1) * p.ldc + p.N) * 2;
-  const __amdgpu_buffer_rsrc_t rsC = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, (int)c_bytes, 0x00020000);
-  int grow[6];
-  bool gw[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) grow[i] = ph_group_row(i, wave, gw[i]);
-  int iss_t = 0, iss_k = 0;
-  unsigned voff[6];
-  auto set_tile_ptrs = [&](int ti) {
-    int m0, n0;
-    pp_tile_coords<PHShape>(lo + xb + ti * nbx, tiles_m, tiles_n, m0, n0);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int row = grow[i] + (lane >> 3);
-      const int chunk = (lane & 7) ^ pp_swz(row);
-      voff[i] = gw[i] ? (unsigned)(((size_t)min(n0 + row, p.N - 1) * p.ldw + chunk * 8) * 2)
-                      : (unsigned)(((size_t)min(m0 + row, p.M - 1) * p.lda + chunk * 8) * 2);
-    }
-  };
-  set_tile_ptrs(0);
-  __amdgpu_buffer_rsrc_t srs[6];
-  int sdst[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    srs[i] = gw[i] ? rsW : rsA;
-    sdst[i] = (gw[i] ? PH_OPA : 0) + grow[i] * 128;
-  }
-  auto issue = [&](int i, int stage_slot) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(srs[i], MQ_LDS_LOCAL(smem + stage_slot * PH_STAGE + sdst[i]), 16, voff[i],
-                                             iss_k * PP_BK * 2, 0, 0);
-  };
-  auto advance = [&]() {
-    if (iss_k + 1 < nk) {
-      ++iss_k;
-    } else if (iss_t + 1 < my_tiles) {
-      ++iss_t;
-      iss_k = 0;
-      set_tile_ptrs(iss_t);
-    }
-  };
-  int ct = 0, kt = 0, cm0 = 0, cn0 = 0;
-  pp_tile_coords<PHShape>(lo + xb, tiles_m, tiles_n, cm0, cn0);
-  auto bias_slot = [&](int t) { return smem + PH_BIAS + ((t & 1) * 8 + wave) * 256; };
-  auto issue_bias = [&]() {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(bias_slot(ct)), 4,
-                                             (unsigned)((cn0 + wcol + (lane & 31)) * 4), 0, 0, 0);
-  };
-  auto junk = [&]() {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsB, MQ_LDS_LOCAL(smem + PH_JUNK + wave * 256), 4, 0u, 0, 0, 0);
-  };
-  f32x4 acc[8][2], prv[8][2];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      prv[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  bf16x8 a[4][2], b[2][2];
-  auto bar = [&]() { pp_barrier(); };
-  auto open_mfma = [&]() {
-    bar();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  auto mfma_half = [&](int h) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[h * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j][kk], a[i][kk], acc[h * 4 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  const int mm = lane & 15, nn = 4 * (lane >> 4);
-  const bool odd = (lane >> 4) & 1;
-  const int nbase = nn - (odd ? 4 : 0);
-  bool prev_valid = false;
-  int pm0 = 0, pn0 = 0, st_i = 0;
-  // one of the previous half-tile's 8 stores (fragment row st_i: its two fragments paired into 16-B row chunks)
-  auto store_one = [&](int i, int bias_tile) {
-    f32x4 bv0, bv1;
-    const unsigned addr = (unsigned)(uintptr_t)MQ_LDS_LOCAL(bias_slot(bias_tile) + nn * 4);
-    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:64\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(bv0), "=&v"(bv1)
-                 : "v"(addr)
-                 : "memory");
-    unsigned pk[2][2];
-    auto one = [&](const f32x4& x, const f32x4& c, unsigned* o) {
-      float v[4] = {x[0] + c[0], x[1] + c[1], x[2] + c[2], x[3] + c[3]};
-      if constexpr (EPI == EPI_GELU_BF16) {
-        const f32x2 g0 = gelu_sig2((f32x2){v[0], v[1]}), g1 = gelu_sig2((f32x2){v[2], v[3]});
-        v[0] = g0.x;
-        v[1] = g0.y;
-        v[2] = g1.x;
-        v[3] = g1.y;
-      }
-      if constexpr (EPI == EPI_RELU_BF16) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      o[0] = pack_bf16x2(v[0], v[1]);
-      o[1] = pack_bf16x2(v[2], v[3]);
-    };
-    one(prv[i][0], bv0, pk[0]);
-    one(prv[i][1], bv1, pk[1]);
-    const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
-    const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-    typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-    const u32x4v o = {s0[0], s1[0], s0[1], s1[1]};
-    const int m = pm0 + arow + i * 16 + mm;
-    const int n = pn0 + wcol + (odd ? 16 : 0) + nbase;
-    unsigned off = 0x80000000u;  // out of range: dropped by the buffer resource
-    if (m < p.M && n < p.N)
-      off = (unsigned)((size_t)(EPI == EPI_BF16 && p.head_dim ? gemm_out_bf16(p, m, n) - (unsigned short*)p.C
-                                                             : (size_t)m * p.ldc + n) * 2);
-    __builtin_amdgcn_raw_buffer_store_b128(o, rsC, off, 0, 0);
-  };
-
-  // prologue: stages 0 and 1, both landed (the steady-state waits count operations a warm ring has in flight)
-#pragma unroll
-  for (int i = 0; i < 6; ++i) issue(i, 0);
-  advance();
-#pragma unroll
-  for (int i = 0; i < 6; ++i) issue(i, 1);
-  advance();
-  pp_wait_vm<0>();
-  pp_barrier();
-  if (wm == 1) pp_barrier();  // stagger
-  for (int g = 0; g < total; ++g) {
-    const int slot = g % 3, nslot = (g + 2) % 3;
-    const char* As = smem + slot * PH_STAGE;
-    const char* Ws = As + PH_OPA;
-    // ---- phase 0: M half 0
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b[j][kk] = pp_frag(Ws, wcol + j * 16 + frow, kk * 4 + fk);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, arow + i * 16 + frow, kk * 4 + fk);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) issue(i, nslot);
-    issue_bias();
-    pp_wait_vm<12>();  // P1 of this stage (and everything older)
-    open_mfma();
-    mfma_half(0);
-    bar();
-    // ---- phase 1: M half 1 (+ one output of the previous half-tile on odd K-steps)
-    if (kt & 1) {
-      if (prev_valid && st_i < 8) {
-        switch (st_i) {  // (a constant fragment row per case: a runtime index would put prv in scratch)
-          case 0: store_one(0, ct - 1); break;
-          case 1: store_one(1, ct - 1); break;
-          case 2: store_one(2, ct - 1); break;
-          case 3: store_one(3, ct - 1); break;
-          case 4: store_one(4, ct - 1); break;
-          case 5: store_one(5, ct - 1); break;
-          case 6: store_one(6, ct - 1); break;
-          default: store_one(7, ct - 1); break;
-        }
-        ++st_i;
-      } else {
-        junk();
-      }
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i][kk] = pp_frag(As, arow + 64 + i * 16 + frow, kk * 4 + fk);
-#pragma unroll
-    for (int i = 4; i < 6; ++i) issue(i, nslot);
-    advance();
-    pp_wait_vm<11>();  // P0 of the next stage
-    open_mfma();
-    mfma_half(1);
-    bar();
-    if (++kt == nk) {
-      // (the previous half-tile's stores are all out: nk >= 16)
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          prv[i][j] = acc[i][j];
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      prev_valid = true;
-      pm0 = cm0;
-      pn0 = cn0;
-      st_i = 0;
-      kt = 0;
-      ++ct;
-      if (ct < my_tiles) pp_tile_coords<PHShape>(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
-    }
-  }
-  // the last half-tile's outputs (its bias landed: every DMA is retired first)
-  pp_wait_vm<0>();
-#pragma unroll
-  for (int i = 0; i < 8; ++i) store_one(i, ct - 1);
-  if (wm == 0) pp_barrier();  // balance the stagger
-  pp_wait_vm<0>();
-}
-
-template <int EPI>
-void launch_ph(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
-  static std::atomic<unsigned> attr{0};
-  if (first_on_device(attr))
-    (void)hipFuncSetAttribute((const void*)gemm_ph_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, PH_LDS);
-  hipLaunchKernelGGL((gemm_ph_kernel<EPI>), grid, dim3(PP_T), PH_LDS, stream, p, tiles_m, tiles_n);
-}
-
 template <int EPI, int MODE, class S>
 void launch_pp(dim3 grid, hipStream_t stream, const GemmArgs& p, int tiles_m, int tiles_n) {
   static std::atomic<unsigned> attr{0};
@@ -1051,19 +779,6 @@ bool gemm_pingpong_fits(const GemmArgs& p, int epi, int num_cus) {
 }
 
 int gemm_pingpong(const GemmArgs& p, int epi, int num_cus, hipStream_t stream) {
-  const int nk = p.K / PP_BK;
-  if (g_gemm_half && (epi == EPI_BF16 || epi == EPI_GELU_BF16 || epi == EPI_RELU_BF16) && p.conv_c == 0 &&
-      nk >= 16 && nk % 2 == 0 && p.N % 8 == 0 && p.ldc % 8 == 0 &&
-      (size_t)p.M * (p.head_dim ? p.N : p.ldc) * 2 < (1ull << 31)) {
-    const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 127) / 128, tiles = tiles_m * tiles_n;
-    const dim3 grid(tiles < num_cus ? tiles : num_cus);
-    switch (epi) {
-      case EPI_BF16: launch_ph<EPI_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-      case EPI_GELU_BF16: launch_ph<EPI_GELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-      default: launch_ph<EPI_RELU_BF16>(grid, stream, p, tiles_m, tiles_n); break;
-    }
-    return hipGetLastError() == hipSuccess ? 0 : -4;
-  }
   return launch_shape<Shape256>(p, epi, num_cus, stream);
 }
 
