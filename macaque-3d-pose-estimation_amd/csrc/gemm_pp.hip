@@ -101,7 +101,8 @@ __device__ __forceinline__ bf16x8 pp_frag(const char* op, int row, int chunk) {
 // epilogues store each wave's 16 KiB lane-linearly into a fixed region of its own (256 blocks x 128 KiB: only for
 // outputs of at least 32 MiB, e.g. fc1, qkv, deconv 1); 512: the bf16 epilogues run all
 // their arithmetic first, then issue their 16 stores back to back; 4096: wave group 1 at priority 1 for the whole
-// kernel instead of priority 1 around every MFMA segment; 8192: no priority changes.
+// kernel instead of priority 1 around every MFMA segment; 8192: no priority changes; 32768: no lgkmcnt(0) after the
+// barrier that opens an MFMA segment (the compiler's own counted waits before each MFMA's operands instead).
 #ifndef PP_DIAG
 #define PP_DIAG 0
 #endif
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
 #endif
   auto open_mfma = [&]() {
     bar();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (!(PP_DIAG & 32768)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
 
   // prologue: stage 0 into buffer 0; P0 (the slots of phases 0-1) must land before the first reads
