@@ -64,7 +64,7 @@ struct PPShape {
   // bias slice per wave: 16 WNF = 64 floats, one dword LDS-DMA (256 B)
   static_assert(WNF == 4, "the epilogue's bias read, paired stores and bias DMA are written for 4 fragments");
   static constexpr int BIAS_SLOT = 256;
-  static constexpr int LDS = PP_BIAS + 16 * BIAS_SLOT;  // two bias slots per wave (tile parity)
+  static constexpr int LDS = PP_BIAS + 8 * BIAS_SLOT;
   // DMA groups (8 rows x 128 B = one 1-KiB wave instruction) in first-read order: P0 A, P0 W, P1 W, P2 A
   static constexpr int GA0 = BM / 16;         // P0 A groups (M half 0 of both wave groups)
   static constexpr int GW0 = 4 * 2 * NA;      // P0 W groups (N part A of the 4 wave columns)
@@ -97,7 +97,7 @@ __device__ __forceinline__ bf16x8 pp_frag(const char* op, int row, int chunk) {
 // its waits); 4: no barriers (and no stagger: the wave groups run free); 8: the fragment reads of the first K-step
 // only (later K-steps reuse the registers); 16: no epilogue; 32: the bf16 epilogues without their stores; 64: the bf16
 // epilogues store every tile into C's first 256 x 256 block; 128: both wave groups run their epilogues in the same
-// barrier interval (group 0 defers its own past the next K-step's phase-0 DMA issue; rejected, r06r); 256: the bf16
+// barrier interval (removed again, in the git history: rejected, r06r); 256: the bf16
 // epilogues store each wave's 16 KiB lane-linearly into a fixed region of its own (256 blocks x 128 KiB: only for
 // outputs of at least 32 MiB, e.g. fc1, qkv, deconv 1); 512: the bf16 epilogues run all
 // their arithmetic first, then issue their 16 stores back to back; 4096: wave group 1 at priority 1 for the whole
@@ -499,9 +499,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
   // compute cursor: tile index, K-step in it, its origin, this wave's bias DMA offset (one column per lane)
   int ct = 0, kt = 0, cm0 = 0, cn0 = 0;
   pp_tile_coords<S>(lo + xb, tiles_m, tiles_n, cm0, cn0);
-  constexpr bool CO = (PP_DIAG & 128) != 0;
-  auto bias_slot = [&](int t) { return smem + PP_BIAS + ((CO ? (t & 1) * 8 : 0) + wave) * S::BIAS_SLOT; };
-  char* bias_lds = bias_slot(0);
+  char* bias_lds = smem + PP_BIAS + wave * S::BIAS_SLOT;
   auto bias_offset = [&](int n0) -> unsigned { return (unsigned)((n0 + wcol + lane) * 4); };
   unsigned bias_off = bias_offset(cn0);
   auto issue_bias = [&]() {
@@ -579,8 +577,6 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
       pp_epilogue<EPI, S, MODE == PP_DECONV>(p, acc, reinterpret_cast<const float*>(bl), m0, n0, wm, wn, lane);
   };
   auto tile_full = [&](int m0, int n0) { return !(PP_DIAG & 48) && (m0 + S::BM <= p.M) && (n0 + S::BN <= p.N); };
-  bool epi_pending = false;  // group 0: the previous tile's epilogue waits for the next K-step's phase-0 DMA issue
-  int pm0 = 0, pn0 = 0;
   for (int g = 0; g < total; ++g) {
 #ifdef PP_STAMP
     stamp_g = g;
@@ -601,8 +597,7 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
           a[i][kk] = pp_frag(As, arow + i * 16 + frow, kk * 4 + fk);
       }
     };
-    const bool defer = CO && epi_pending;
-    if (!defer) reads0();
+    reads0();
 #pragma unroll
     for (int i = 0; i < S::C0; ++i) issue(i, slot ^ 1);
     issue_bias();
@@ -611,13 +606,6 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
       PP_LOOP_WAIT(S::N0 + EPI_OPS);
     else
       PP_LOOP_WAIT(S::N0);
-    if (defer) {  // group 0, first K-step of a tile: the previous tile's epilogue beside group 1's
-      bar();
-      epilogue(bias_slot(ct - 1), pm0, pn0);
-      stores_pending = tile_full(pm0, pn0);
-      epi_pending = false;
-      reads0();
-    }
     open_mfma();
     mfma_quadrant(0, b0, 0, NAc{});
     bar();
@@ -658,27 +646,15 @@ __global__ __launch_bounds__(PP_T, 2) void gemm_pp_kernel(GemmArgs p, int tiles_
     mfma_quadrant(1, b1, NA, NBc{});
     bar();
     if (++kt == nk) {
-      if (CO && wm == 0) {
-        pm0 = cm0;
-        pn0 = cn0;
-        epi_pending = true;
-      } else {
-        epilogue(bias_lds, cm0, cn0);
-        stores_pending = tile_full(cm0, cn0);
-        if (CO) bar();  // group 0 passes it after its next phase-0 DMA issue, then runs its own epilogue
-      }
+      epilogue(bias_lds, cm0, cn0);
+      stores_pending = tile_full(cm0, cn0);
       kt = 0;
       ++ct;
       if (ct < my_tiles) {
         pp_tile_coords<S>(lo + xb + ct * nbx, tiles_m, tiles_n, cm0, cn0);
         bias_off = bias_offset(cn0);
       }
-      bias_lds = bias_slot(ct);
     }
-  }
-  if (CO && epi_pending) {  // group 0's last tile
-    bar();
-    epilogue(bias_slot(ct - 1), pm0, pn0);
   }
   if constexpr ((PP_DIAG & 16) != 0) {  // keep the accumulators live (a store the host never asks for)
     if (p.M < 0)

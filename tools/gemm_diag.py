@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 from gemm_probe import SHAPES  # noqa: E402
 
 PKG = os.path.join(ROOT, "macaque-3d-pose-estimation_amd")
-BITS = {1: "no counted vmcnt waits", 2: "no LDS-DMA", 4: "no barriers", 8: "fragment reads once", 16: "no epilogue", 32: "epilogue without stores", 64: "epilogue stores L2-resident", 128: "both groups' epilogues in one interval",
+BITS = {1: "no counted vmcnt waits", 2: "no LDS-DMA", 4: "no barriers", 8: "fragment reads once", 16: "no epilogue", 32: "epilogue without stores", 64: "epilogue stores L2-resident", 128: "both groups' epilogues in one interval (removed; git history)",
         256: "epilogue stores lane-linear per wave", 1024: "deferred-store kernel (removed; git history)",
         512: "epilogue arithmetic first, then the stores", 4096: "static priority for group 1",
         8192: "no priority changes", 16384: "half-tile kernel with the streamed epilogue (removed; git history)",
